@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Benchmark of the MDQT hot path on MI355X (one JSON line on rank 0).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c5] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+A "step" is one MD step of the reference time loop (SpeedUp:1369-1377): forces() once, then
+plasmaToQuantumTimestepRatio (= 25 at density 2) x (step(); qstep()), all on the GPU, state
+resident in HBM.  The metric is BASELINE.json's: particle-steps/s with QT on, reported in
+particle-qsteps/s (N x quantum substeps / wall time).
+
+Workload at N=1 is BASELINE.json configs[1] (C2): N0=3500 full MDQT, detuning=-1, Om=1,
+density 2 (realised N=3573 for seed 12346).  Synthetic inputs exactly as the reference's init()
+(drand48 seeded 12345+job).  With N>1 GPUs C2 does not shard (~10 µs
+of force per MD step), so each rank runs an independent replica (job = rank+1), like the
+reference's SLURM array (exampleSlurmFile.slurm:3): "replicas only", weak scaling.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFS = 78.6       # MI355X fp64 vector (spec), SURVEY §8d
+B_Q_PER_ION = 520.0        # algorithmic bytes per ion per fused-substep launch
+F_Q_PER_QSTEP = 1750.0     # fp64 flop per particle-qstep
+W_F_PER_PAIR = 30.0        # fp64 flop per distinct pair
+
+CONFIGS = {
+    # name: (params, qt, description)
+    "c2": (dict(N0=3500), 1, "C2: N0=3500 full MDQT, detuning=-1, Om=1, density=2, fp64"),
+    "c1": (dict(N0=500, Ge=0.1), 0, "C1: N0=500 Yukawa OCP MD-only, Ge=0.1"),
+    "c3": (dict(N0=100000, Ge=1.0 / 12), 0, "C3: N0=100000 MD-only, kappa=0.5"),
+    "c5": (dict(N0=250000, detuningDP=1.0), 1, "C5: N0=250000 full MDQT, detuningDP=+1"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(params, qt, seconds):
+    """The oracle (CPU restatement, race-free OpenMP) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+    if not os.path.exists(O.LIB_PATH):
+        O.build()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o = O.OracleSim(rng_mode=1, nthreads=threads, qt_enabled=qt, **params).init()
+    ratio = int(o.const("plasmaToQuantumTimestepRatio"))
+    o.md_steps(1)                                  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        o.md_steps(1)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 400:
+            break
+    rate = o.N * ratio * n / el
+    return {"value": rate, "unit": "particle-qsteps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} MD steps x {ratio} qsteps of the same workload (N={o.N}), oracle C "
+                      f"restatement, OpenMP {threads} threads, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import mdqtplasmasims_amd as M
+    params, qt, desc = CONFIGS[args.config]
+    job = rank + 1
+    sim = M.Simulation(device=local, seed=12345 + job, job=job, qt_enabled=qt, **params).init()
+    N = sim.N
+    ratio = int(sim.const("plasmaToQuantumTimestepRatio"))
+    sim.md_steps(args.warmup)
+    sim.synchronize()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    sim.enable_timing(True)
+    t0 = time.perf_counter()
+    sim.md_steps(args.steps)
+    sim.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    f_ms, nf, s_ms, ns = sim.kernel_time_totals()
+    sim.enable_timing(False)
+
+    tt = torch.tensor([el, float(N), f_ms, s_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        mx = tt.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        el_max, n_tot = float(mx[0]), float(sm[1])
+    else:
+        el_max, n_tot = el, float(N)
+
+    if rank == 0:
+        value = n_tot * ratio * args.steps / el_max
+        # roofline of the dominant kernel (per-launch averages from the HIP events above)
+        f_avg = f_ms / max(nf, 1) * 1e-3
+        s_avg = s_ms / max(ns, 1) * 1e-3
+        if qt and s_ms >= f_ms:
+            nsub_per_launch = ratio * args.steps / max(ns, 1)
+            bytes_launch = B_Q_PER_ION * N
+            ach = bytes_launch / s_avg / 1e9
+            flops = F_Q_PER_QSTEP * N * nsub_per_launch
+            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                    "kernel": "k_substeps (fused 25 x step+qstep)",
+                    "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
+                    "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS}
+        else:
+            pairs = N * (N - 1) / 2.0
+            flops = W_F_PER_PAIR * pairs
+            ach = flops / f_avg / 1e12
+            roof = {"bound": "hbm", "achieved": (24.0 * 2 * N) / f_avg / 1e9, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": (24.0 * 2 * N) / f_avg / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                    "kernel": "k_pairs<force> + segment reduction", "avg_launch_us": f_avg * 1e6,
+                    "fp64_tflops": ach, "fp64_frac": ach / FP64_PEAK_TFS}
+        out = {
+            "metric": "particle-steps/sec (MD+QT) at N=3.5k and N=1M; 1/2/4/8-GPU scaling",
+            "value": value,
+            "unit": "particle-qsteps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (reference init(): drand48 positions + random S superposition, seed 12345+job)",
+            "config": {"workload": desc, "N": N, "md_steps": args.steps, "qsteps_per_md_step": ratio,
+                       "particle_md_steps_per_s": value / ratio,
+                       "parallelism": "replicas" if world > 1 else "single",
+                       "rng": "philox4x32-10", "kernel_ms": {"force_total": f_ms, "force_launches": nf,
+                                                            "substeps_total": s_ms, "substep_launches": ns}},
+            "roofline": roof,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(params, qt, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    sim.close()
+
+
+if __name__ == "__main__":
+    main()

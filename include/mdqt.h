@@ -1,0 +1,149 @@
+/*
+ * mdqt.h — C ABI of the MI355X-native MDQT engine (libmdqt.so).
+ *
+ * Drop-in boundary for the hot path of the reference program
+ *   laserCoolingPlusExpansionMDQTSpeedUp.cpp        ("SpeedUp" below, tlangin/MDQTPlasmaSims)
+ * The reference has no plugin API: its seam is a set of void functions over globals
+ * (SpeedUp:176-185 prototypes) plus the process interface `exe <job>` (SpeedUp:1145).
+ * Every entry point below names the reference function it replaces (file:line).
+ *
+ * Conventions
+ *   - opaque context, int status (0 = ok, <0 = error; mdqt_last_error() has the message);
+ *   - host buffers are caller-owned; R/V/F are SoA [3][ld] row-major exactly like the
+ *     reference's `double R[3][N0+1000]` (SpeedUp:126-129) with the row stride `ld` explicit;
+ *   - psi is [N][12][2] interleaved (re, im): the storage order of `cx_mat wvFns[N]`
+ *     (12x1 column, SpeedUp:151);
+ *   - device state stays resident in HBM between calls; get/set are the only host syncs;
+ *   - one context is not reentrant; distinct contexts are independent (thread-safe).
+ * No torch types, no HIP types: the stream is passed as void* (a hipStream_t).
+ */
+#ifndef MDQT_H
+#define MDQT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDQT_NUM_STATES 12   /* numStates, SpeedUp:153 */
+#define MDQT_NBINS 2001      /* velocity-distribution bins, SpeedUp:120-123, :340-344 */
+
+/* User inputs of the reference (compile-time globals / #defines at SpeedUp:56-85), same
+ * names, same defaults (mdqt_default_params), plus the engine's own extensions. */
+typedef struct mdqt_params {
+    double Ge;            /* SpeedUp:60  Gamma_e; kappa = sqrt(3 Ge), lDeb = 1/kappa (:295)   */
+    double tmax;          /* SpeedUp:63  end time (omega_E^-1)                                */
+    double density;       /* SpeedUp:65  1e14 m^-3                                            */
+    double sig0;          /* SpeedUp:66  initial plasma size (mm)                             */
+    double Te;            /* SpeedUp:67  electron temperature (K)                             */
+    double fracOfSig;     /* SpeedUp:68  position in the expanding cloud (0 = no expansion)   */
+    double detuning;      /* SpeedUp:70  S-P detuning (units of gamma)                        */
+    double detuningDP;    /* SpeedUp:71  D-P detuning                                         */
+    double Om;            /* SpeedUp:72  S-P Rabi frequency                                   */
+    double OmDP;          /* SpeedUp:73  D-P Rabi frequency                                   */
+    int N0;               /* SpeedUp:69  nominal ion number                                   */
+    int newRun;           /* SpeedUp:61  1 = init(), 0 = readConditions(c0)                   */
+    int c0;               /* SpeedUp:62  MD-step index to resume from                          */
+    int sampleFreq;       /* SpeedUp:78  output every sampleFreq MD steps                     */
+    int reNormalizewvFns; /* SpeedUp:74                                                       */
+    /* ---- extensions ---- */
+    int qt_enabled;       /* 1 = MDQT (reference); 0 = MD-only (qstep body skipped, t advances) */
+    int rng_mode;         /* 1 = Philox4x32-10 keyed (seed, job) x (global ion, qstep) — the
+                           * only mode the device path implements this round; 0 (drand48 in
+                           * reference order) is rejected with an error                         */
+    uint32_t seed;        /* srand48 seed for init (reference: time(NULL)+job, SpeedUp:1219)   */
+    uint32_t job;         /* SpeedUp:1145 argv[1]                                               */
+    int device;           /* HIP device ordinal (-1 = current device)                           */
+    int world_size;       /* ions sharded over world_size contexts (1 = whole system here)     */
+    int rank;             /* this context's slab: ions [rank*S, min((rank+1)*S, N))             */
+    int force_segments;   /* j-split of the force sum (0 = auto, a function of N only)         */
+    char saveDirectory[256]; /* SpeedUp:56 */
+} mdqt_params;
+
+typedef struct mdqt_ctx mdqt_ctx;
+
+/* ---- lifecycle ---- */
+void        mdqt_default_params(mdqt_params* p);            /* SpeedUp:56-85 defaults          */
+int         mdqt_create(const mdqt_params* p, mdqt_ctx** out); /* + constant operators :1163-1215 */
+void        mdqt_destroy(mdqt_ctx* c);
+const char* mdqt_last_error(void);                           /* thread-local message            */
+int         mdqt_device_count(void);                         /* HIP devices visible             */
+const char* mdqt_version(void);
+
+/* ---- derived constants (SpeedUp:79-85, :146-149, :295-297, :1181-1215) ---- */
+double      mdqt_get_const(const mdqt_ctx* c, const char* name);
+
+/* ---- state ---- */
+int         mdqt_init(mdqt_ctx* c);                          /* init(), SpeedUp:289-348         */
+int         mdqt_get_N(const mdqt_ctx* c);
+double      mdqt_get_time(const mdqt_ctx* c);
+int         mdqt_set_time(mdqt_ctx* c, double t);
+uint64_t    mdqt_get_qstep_index(const mdqt_ctx* c);
+int         mdqt_set_qstep_index(mdqt_ctx* c, uint64_t q);
+int         mdqt_get_counters(const mdqt_ctx* c, int* c0, unsigned* counter, double* Epot, double* Epot0);
+/* Whole-system state (all N ions; with world_size > 1 only this rank's slab of V/F/psi/tPart
+ * is meaningful, R is the full gathered array). NULL pointers are skipped. */
+int         mdqt_set_state(mdqt_ctx* c, int N, const double* R, const double* V, size_t ld,
+                           const double* psi, const double* tPart, double t);
+int         mdqt_get_state(mdqt_ctx* c, double* R, double* V, double* F, size_t ld,
+                           double* psi, double* tPart, double* t);
+int         mdqt_set_forces(mdqt_ctx* c, const double* F, size_t ld);
+
+/* ---- hot path ---- */
+int         mdqt_forces(mdqt_ctx* c);                        /* forces(),  SpeedUp:192-236      */
+int         mdqt_step(mdqt_ctx* c);                          /* step(),    SpeedUp:418-430      */
+int         mdqt_qstep(mdqt_ctx* c);                         /* qstep(),   SpeedUp:438-717      */
+int         mdqt_substeps(mdqt_ctx* c, int n);               /* n x (step(); qstep()), F frozen;
+                                                                 the body of SpeedUp:1376-1377,
+                                                                 fused in one launch            */
+int         mdqt_md_steps(mdqt_ctx* c, int n);               /* n x (forces(); c0++;
+                                                                 ratio x (step(); qstep()))     */
+
+/* Stateless kernel-level entry points on caller host arrays (explicit box and screening
+ * length), for callers whose force law is the same Yukawa pair sum but whose box is not
+ * SpeedUp's — e.g. MonteCarloFollowedByMDAndTempAnisotropy.cpp calculateAccelerations
+ * (:387-448, acceleration = force at unit mass) and calculatePotentialEnergyForParticles
+ * (:207-244).  R, F are [3][ld]; nseg = j-split (0 = auto); U[i] = sum_{j != i} u(r_ij). */
+int         mdqt_forces_raw(int N, double L, double lDeb, const double* R, size_t ld, double* F,
+                            int nseg, int device);
+int         mdqt_potentials_raw(int N, double L, double lDeb, const double* R, size_t ld, double* U,
+                                int nseg, int device);
+
+/* ---- diagnostics / output ---- */
+int         mdqt_epotential(mdqt_ctx* c, double* Epot);      /* Epotential(), SpeedUp:244-281   */
+/* observables of output(), SpeedUp:917-1032: out7 = t, EkinX, EkinY, EkinZ, Epot,
+ * Etot-Epot0, <vx>; Pvel [3][2001] (may be NULL); pops [N][3] = S,P,D (may be NULL). */
+int         mdqt_observables(mdqt_ctx* c, double out7[7], double* Pvel, double* pops);
+int         mdqt_setup_directories(mdqt_ctx* c);             /* SpeedUp:1145-1160               */
+const char* mdqt_save_directory(const mdqt_ctx* c);
+int         mdqt_output(mdqt_ctx* c);                        /* output(),  SpeedUp:917-1032     */
+int         mdqt_write_conditions(mdqt_ctx* c, int c0);      /* writeConditions, :725-784       */
+int         mdqt_read_conditions(mdqt_ctx* c, int c0);       /* readConditions,  :785-916       */
+int         mdqt_run(mdqt_ctx* c);                           /* main() time loop, :1139-1383    */
+
+/* ---- streams, timing, multi-GPU plumbing ---- */
+int         mdqt_set_stream(mdqt_ctx* c, void* hip_stream);  /* NULL = the context's own stream */
+void*       mdqt_get_stream(mdqt_ctx* c);
+int         mdqt_synchronize(mdqt_ctx* c);
+/* slab of rank r: ions [lo, hi) with slab capacity S = ceil(N / world) (pure function) */
+int         mdqt_slab(int N, int world, int rank, int* lo, int* hi, int* S);
+/* device address of the gathered position array [world][3][S] (doubles) and S; the
+ * caller's collective (RCCL all-gather) fills the other ranks' slabs in place. */
+int         mdqt_positions_device(mdqt_ctx* c, void** dptr, int* S);
+/* Per-rank partial sums for output() under sharding: out[0] = sum vx, [1..3] = sum of the
+ * reference's EkinX/Y/Z terms about vxAvg, [4] = sum over owned i of the full-row pair
+ * potential, Pvel partial [3][2001] before normalisation.  Used by the sharded driver. */
+int         mdqt_partial_observables(mdqt_ctx* c, double vxAvg, double out5[5], double* Pvel_partial);
+/* kernel timing: while enabled, every force launch (incl. its segment reduction) and every
+ * fused-substep launch is bracketed by HIP events on the context stream; totals() syncs,
+ * returns the summed device time (ms) and launch counts since the last call, and resets. */
+int         mdqt_enable_timing(mdqt_ctx* c, int on);
+int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
+                                    int* nsub);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDQT_H */

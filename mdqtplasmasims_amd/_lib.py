@@ -1,0 +1,108 @@
+"""ctypes binding of libmdqt.so (the C ABI declared in include/mdqt.h).
+
+The library is built in-tree (``python -m mdqtplasmasims_amd.build`` or ``__graft_entry__.build()``)
+into ``mdqtplasmasims_amd/lib/libmdqt.so``.  There is no fallback: if the library is missing or
+cannot be loaded, :func:`lib` raises, and every simulation call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmdqt.so")
+CLI_PATH = os.path.join(HERE, "bin", "mdqt")
+
+_dp = C.POINTER(C.c_double)
+
+
+class MdqtParams(C.Structure):
+    """mirror of ``struct mdqt_params`` (include/mdqt.h)."""
+    _fields_ = [
+        ("Ge", C.c_double), ("tmax", C.c_double), ("density", C.c_double), ("sig0", C.c_double),
+        ("Te", C.c_double), ("fracOfSig", C.c_double), ("detuning", C.c_double),
+        ("detuningDP", C.c_double), ("Om", C.c_double), ("OmDP", C.c_double),
+        ("N0", C.c_int), ("newRun", C.c_int), ("c0", C.c_int), ("sampleFreq", C.c_int),
+        ("reNormalizewvFns", C.c_int), ("qt_enabled", C.c_int), ("rng_mode", C.c_int),
+        ("seed", C.c_uint32), ("job", C.c_uint32), ("device", C.c_int), ("world_size", C.c_int),
+        ("rank", C.c_int), ("force_segments", C.c_int), ("saveDirectory", C.c_char * 256),
+    ]
+
+
+# (name, restype, argtypes) of every symbol include/mdqt.h declares
+SIGNATURES = [
+    ("mdqt_default_params", None, [C.POINTER(MdqtParams)]),
+    ("mdqt_create", C.c_int, [C.POINTER(MdqtParams), C.POINTER(C.c_void_p)]),
+    ("mdqt_destroy", None, [C.c_void_p]),
+    ("mdqt_last_error", C.c_char_p, []),
+    ("mdqt_device_count", C.c_int, []),
+    ("mdqt_version", C.c_char_p, []),
+    ("mdqt_get_const", C.c_double, [C.c_void_p, C.c_char_p]),
+    ("mdqt_init", C.c_int, [C.c_void_p]),
+    ("mdqt_get_N", C.c_int, [C.c_void_p]),
+    ("mdqt_get_time", C.c_double, [C.c_void_p]),
+    ("mdqt_set_time", C.c_int, [C.c_void_p, C.c_double]),
+    ("mdqt_get_qstep_index", C.c_uint64, [C.c_void_p]),
+    ("mdqt_set_qstep_index", C.c_int, [C.c_void_p, C.c_uint64]),
+    ("mdqt_get_counters", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint), _dp, _dp]),
+    ("mdqt_set_state", C.c_int, [C.c_void_p, C.c_int, _dp, _dp, C.c_size_t, _dp, _dp, C.c_double]),
+    ("mdqt_get_state", C.c_int, [C.c_void_p, _dp, _dp, _dp, C.c_size_t, _dp, _dp, _dp]),
+    ("mdqt_set_forces", C.c_int, [C.c_void_p, _dp, C.c_size_t]),
+    ("mdqt_forces", C.c_int, [C.c_void_p]),
+    ("mdqt_step", C.c_int, [C.c_void_p]),
+    ("mdqt_qstep", C.c_int, [C.c_void_p]),
+    ("mdqt_substeps", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdqt_md_steps", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdqt_forces_raw", C.c_int, [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t, _dp, C.c_int, C.c_int]),
+    ("mdqt_potentials_raw", C.c_int, [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t, _dp, C.c_int,
+                                      C.c_int]),
+    ("mdqt_epotential", C.c_int, [C.c_void_p, _dp]),
+    ("mdqt_observables", C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+    ("mdqt_setup_directories", C.c_int, [C.c_void_p]),
+    ("mdqt_save_directory", C.c_char_p, [C.c_void_p]),
+    ("mdqt_output", C.c_int, [C.c_void_p]),
+    ("mdqt_write_conditions", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdqt_read_conditions", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdqt_run", C.c_int, [C.c_void_p]),
+    ("mdqt_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("mdqt_get_stream", C.c_void_p, [C.c_void_p]),
+    ("mdqt_synchronize", C.c_int, [C.c_void_p]),
+    ("mdqt_slab", C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                            C.POINTER(C.c_int)]),
+    ("mdqt_positions_device", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int)]),
+    ("mdqt_partial_observables", C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
+    ("mdqt_kernel_time_totals", C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int), _dp, C.POINTER(C.c_int)]),
+    ("mdqt_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
+]
+
+_lib = None
+
+
+class MdqtError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmdqt.so (raises if it has not been built: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MdqtError(f"{LIB_PATH} not built: run `python -m mdqtplasmasims_amd.build` "
+                            "(the MDQT engine has no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().mdqt_last_error().decode(errors="replace")
+        raise MdqtError(f"{what}: {msg}" if what else msg)
+
+
+def dptr(a):
+    return a.ctypes.data_as(_dp) if a is not None else None

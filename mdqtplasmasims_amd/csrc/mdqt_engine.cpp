@@ -1,0 +1,983 @@
+// Host engine of the MI355X MDQT path: the C ABI of include/mdqt.h.
+//
+// Owns the device-resident state of one simulation (or one rank's slab of it), builds the
+// reference's derived constants and QT operators, drives the gfx950 kernels of
+// mdqt_kernels.hip on one HIP stream, and reproduces the reference program's control flow
+// (main() time loop), initial conditions and text files.  Every function cites the lines of
+// laserCoolingPlusExpansionMDQTSpeedUp.cpp ("SpeedUp") it stands in for.
+#include <errno.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mdqt.h"
+#include "mdqt_internal.hpp"
+
+using namespace mdqt;
+
+namespace {
+
+constexpr double TIMESTEP = 0.002;   // SpeedUp:80
+constexpr int NINTERVALV = 13;       // numberOfIntervalV, SpeedUp:105
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+
+#define HIPCHK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+struct cx { double re, im; };
+inline cx cx_make(double r, double i) { return {r, i}; }
+inline cx cx_mul(cx a, cx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+inline cx cx_add(cx a, cx b) { return {a.re + b.re, a.im + b.im}; }
+inline cx cx_sub(cx a, cx b) { return {a.re - b.re, a.im - b.im}; }
+inline cx cx_conj(cx a) { return {a.re, -a.im}; }
+
+// glibc drand48 (SpeedUp:303-333, srand48 :1219), bit-exact.
+inline uint64_t srand48_state(uint32_t seed) { return (((uint64_t)seed) << 16) | 0x330Eull; }
+inline double drand48_next(uint64_t* x) {
+    *x = (0x5DEECE66Dull * (*x) + 0xBull) & 0xFFFFFFFFFFFFull;
+    return ldexp((double)(*x), -48);
+}
+
+}  // namespace
+
+struct mdqt_ctx {
+    mdqt_params p;
+    // derived constants (SpeedUp:79-85, :146-149, :295-297)
+    double gamToE, dtQ, pv2q, r, kRat, vKick, vKickDP, lDeb, L;
+    int ratio;
+    double gs[18];
+    QTConst qc;
+    double vel[NBINS];
+    // sizes
+    int N = 0, S = 0, lo = 0, hi = 0, nloc = 0;
+    int capS = 0, capNseg = 0, nseg = 1, seglen = 1;
+    // device
+    int dev = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    double *dR = nullptr, *dV = nullptr, *dF = nullptr, *dFpart = nullptr, *dPsi = nullptr,
+           *dTp = nullptr, *dScr = nullptr, *dKde = nullptr, *dUrow = nullptr;
+    int kdeChunks = 0;
+    // host-side state
+    double t = 0.;
+    uint64_t qidx = 0;
+    int c0 = 0;
+    unsigned counter = 0;
+    double Epot = 0., Epot0 = 0.;
+    uint64_t x48 = 0;
+    std::vector<double> Vholder;   // [13][3][N] VZERO_* files (SpeedUp:752-763, :898-913)
+    char saveDirectory[1024];
+    // timing
+    // per-launch HIP events of the hot kernels (kind 0 = force, 1 = substeps), recorded on
+    // the launch stream while timing is on; summed by mdqt_kernel_time_totals
+    bool timing = false;
+    std::vector<hipEvent_t> evpool[2];
+    int evused[2] = {0, 0};
+};
+
+// ---------------------------------------------------------------------------------------------
+// parameters and constants
+// ---------------------------------------------------------------------------------------------
+
+extern "C" void mdqt_default_params(mdqt_params* p) {
+    memset(p, 0, sizeof(*p));
+    p->Ge = 0.1; p->tmax = 30; p->density = 2; p->sig0 = 4.0; p->Te = 19.0; p->fracOfSig = 0;   // :60-68
+    p->detuning = -1; p->detuningDP = 1; p->Om = 1; p->OmDP = 1;                               // :70-73
+    p->N0 = 3500; p->newRun = 1; p->c0 = 0; p->sampleFreq = 40; p->reNormalizewvFns = 0;       // :61-78
+    p->qt_enabled = 1; p->rng_mode = 1; p->seed = 12345; p->job = 1;
+    p->device = -1; p->world_size = 1; p->rank = 0; p->force_segments = 0;
+    strcpy(p->saveDirectory, "dataLaserCool/");                                              // :56
+}
+
+extern "C" const char* mdqt_last_error(void) { return g_err.c_str(); }
+extern "C" const char* mdqt_version(void) { return "mdqt-mi355x 0.1 (gfx950)"; }
+
+extern "C" int mdqt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static void build_constants(mdqt_ctx* s) {
+    const mdqt_params* p = &s->p;
+    s->gamToE = 174.07 / sqrt(p->density);                      // :79
+    s->ratio = (int)ceil(34.81 / sqrt(p->density));             // :83
+    s->dtQ = TIMESTEP / s->ratio;                               // :84
+    s->pv2q = 1.1821 * pow(p->density, 1. / 6);                 // :85
+    s->r = 0.0617;                                              // :146
+    s->kRat = 0.395;                                            // :147
+    s->vKick = 0.001208 / s->pv2q;                              // :148
+    s->vKickDP = s->vKick * s->kRat;                            // :149
+    s->lDeb = 1. / sqrt(3. * p->Ge);                            // :295
+    s->L = pow(p->N0 * 4. * M_PI / 3., 0.333333333);            // :297
+    const double r = s->r;
+    double* gs = s->gs;                                         // :1181-1198
+    gs[0] = sqrt(1.); gs[1] = sqrt(2. / 3); gs[2] = sqrt(1. / 3); gs[3] = sqrt(2. / 3);
+    gs[4] = sqrt(1. / 3); gs[5] = sqrt(1.);
+    gs[6] = sqrt(r * 2. / 3); gs[7] = sqrt(r * 4. / 15); gs[8] = sqrt(r * 1. / 15);
+    gs[9] = sqrt(r * 2. / 5); gs[10] = sqrt(r * 2. / 5); gs[11] = sqrt(r * 1. / 5);
+    gs[12] = sqrt(r * 1. / 5); gs[13] = sqrt(r * 2. / 5); gs[14] = sqrt(r * 2. / 5);
+    gs[15] = sqrt(r * 1. / 15); gs[16] = sqrt(r * 4. / 15); gs[17] = sqrt(r * 2. / 3);
+    // cs[k] = |a><b| (0-based), :1163-1180
+    static const int A[18] = {1, 1, 0, 0, 1, 0, 6, 7, 8, 7, 8, 9, 8, 9, 10, 9, 10, 11};
+    static const int B[18] = {2, 3, 3, 4, 4, 5, 5, 5, 5, 4, 4, 4, 3, 3, 3, 2, 2, 2};
+    cx decay[NS][NS], hamDecay[NS][NS], ham[NS][NS];
+    memset(decay, 0, sizeof decay); memset(hamDecay, 0, sizeof hamDecay); memset(ham, 0, sizeof ham);
+    for (int j = 0; j < 18; ++j) {                              // :1201-1204
+        const int b = B[j];
+        const double g2 = gs[j] * gs[j];
+        hamDecay[b][b] = cx_sub(hamDecay[b][b], cx_make(0., 0.5 * g2));
+        decay[b][b] = cx_add(decay[b][b], cx_make(g2, 0.));
+    }
+    for (int k = 0; k < 6; ++k)                                 // :1206-1210
+        if (k != 1 && k != 3) {
+            const double v = ((-1. * gs[k]) * p->Om) / 2;
+            ham[B[k]][A[k]] = cx_add(ham[B[k]][A[k]], cx_make(v, 0.));
+        }
+    for (int k = 6; k < 18; ++k)                                // :1211-1215
+        if (k != 8 && k != 11 && k != 7 && k != 10 && k != 13 && k != 16) {
+            const double v = (((-1. * gs[k]) * p->OmDP) / 2) / sqrt(r);
+            ham[B[k]][A[k]] = cx_add(ham[B[k]][A[k]], cx_make(v, 0.));
+        }
+    QTConst& q = s->qc;
+    memset(&q, 0, sizeof q);
+    q.dtQ = s->dtQ; q.gamToE = s->gamToE;
+    q.h = s->dtQ * s->gamToE;                                   // :526, :530
+    q.dtHalf = s->dtQ * s->gamToE / 2;                          // :525
+    q.invh = 1. / (s->dtQ * s->gamToE);                         // :532
+    q.pv2q = s->pv2q; q.kRat = s->kRat; q.r = r;
+    q.det = p->detuning; q.detDP = p->detuningDP;
+    q.kickS = 1 * s->vKick * p->Om;                             // :503
+    q.kickD = s->vKickDP * (p->OmDP / r);
+    q.vKick = s->vKick; q.vKickDP = s->vKickDP;
+    q.pD = r / (r + 1);                                         // :589
+    for (int k = 0; k < 4; ++k) {
+        q.dP[k] = decay[2 + k][2 + k].re;
+        q.hdP[k] = hamDecay[2 + k][2 + k].im;
+    }
+    q.a8 = ((p->OmDP / 2) * gs[8]) / sqrt(r);                   // :508
+    q.a11 = ((p->OmDP / 2) * gs[11]) / sqrt(r);
+    // static off-diagonal M = I - i h H entries, built exactly as the dense algebra does
+    const cx sI = cx_make(0., s->dtQ * s->gamToE);
+    for (int e = 0; e < NSTATIC; ++e) {
+        const int a = kStaticRC[e][0], b = kStaticRC[e][1];
+        cx h = cx_add(cx_add(cx_make(0., 0.), ham[a][b]), cx_conj(ham[b][a]));
+        cx hamil = cx_add(h, hamDecay[a][b]);
+        cx M = cx_sub(cx_make(0., 0.), cx_mul(sI, hamil));
+        q.Mre[e] = M.re; q.Mim[e] = M.im;
+    }
+    q.thS3 = gs[2] * gs[2];                                     // :637-643
+    q.thS4 = gs[4] * gs[4];                                     // :652-658
+    q.thD[0][0] = gs[17] * gs[17] / r; q.thD[0][1] = gs[17] * gs[17] / r + gs[16] * gs[16] / r;   // :612-632
+    q.thD[1][0] = gs[14] * gs[14] / r; q.thD[1][1] = gs[14] * gs[14] / r + gs[13] * gs[13] / r;   // :644-650
+    q.thD[2][0] = gs[11] * gs[11] / r; q.thD[2][1] = gs[11] * gs[11] / r + gs[10] * gs[10] / r;   // :659-665
+    q.thD[3][0] = gs[8] * gs[8] / r;   q.thD[3][1] = gs[8] * gs[8] / r + gs[7] * gs[7] / r;       // :675-697
+    for (int k = 0; k < 18; ++k) q.gs[k] = gs[k];
+    q.renorm = p->reNormalizewvFns;
+    q.seed = p->seed; q.job = p->job;
+    for (int i = 0; i < NBINS; ++i) s->vel[i] = (double)i * 0.0025;   // :340-344
+}
+
+static double expDetuning_of(const mdqt_params* p, double t) {   // :447
+    return 0.0126 * p->fracOfSig * p->Te * t /
+           (sqrt(p->density) * p->sig0 * sqrt(1 + 0.00014314 * t * t * p->Te / (p->density * p->sig0 * p->sig0)));
+}
+
+// ---------------------------------------------------------------------------------------------
+// sizing and allocation
+// ---------------------------------------------------------------------------------------------
+
+extern "C" int mdqt_slab(int N, int world, int rank, int* lo, int* hi, int* S) {
+    if (N < 0 || world < 1 || rank < 0 || rank >= world) return fail("mdqt_slab: bad arguments");
+    int s = (N + world - 1) / world;
+    s = ((s + 63) / 64) * 64;
+    if (s == 0) s = 64;
+    int l = rank * s; if (l > N) l = N;
+    int h = (rank + 1) * s; if (h > N) h = N;
+    if (lo) *lo = l;
+    if (hi) *hi = h;
+    if (S) *S = s;
+    return 0;
+}
+
+// j segmentation of the force sum: a function of N only (partition invariance across world
+// sizes); enough (row x segment) threads to fill 256 CUs at small N, segments >= 64 ions.
+static void choose_segments(mdqt_ctx* s) {
+    const int N = s->N;
+    int nseg = s->p.force_segments;
+    if (nseg <= 0) {
+        const long target = 1L << 20;
+        long a = (target + N - 1) / (N > 0 ? N : 1);
+        long b = N / 64;
+        nseg = (int)(a < b ? a : b);
+        if (nseg < 1) nseg = 1;
+    }
+    if (nseg > N && N > 0) nseg = N;
+    if (nseg < 1) nseg = 1;
+    s->seglen = N > 0 ? (N + nseg - 1) / nseg : 1;
+    s->nseg = N > 0 ? (N + s->seglen - 1) / s->seglen : 1;
+}
+
+static void free_device(mdqt_ctx* s) {
+    double** ps[] = {&s->dR, &s->dV, &s->dF, &s->dFpart, &s->dPsi, &s->dTp, &s->dScr, &s->dKde, &s->dUrow};
+    for (double** q : ps) { if (*q) (void)hipFree(*q); *q = nullptr; }
+    s->capS = 0; s->capNseg = 0; s->kdeChunks = 0;
+}
+
+// (re)size everything for N ions; device contents are NOT preserved (callers upload after)
+static int resize(mdqt_ctx* s, int N) {
+    if (N < 0) return fail("negative N");
+    int lo, hi, S;
+    if (mdqt_slab(N, s->p.world_size, s->p.rank, &lo, &hi, &S)) return -1;
+    s->N = N; s->lo = lo; s->hi = hi; s->nloc = hi - lo;
+    choose_segments(s);
+    const int W = s->p.world_size;
+    if (S != s->capS || s->nseg > s->capNseg) {
+        free_device(s);
+        HIPCHK(hipSetDevice(s->dev));
+        const size_t sz = (size_t)S * sizeof(double);
+        HIPCHK(hipMalloc(&s->dR, sz * 3 * W));
+        HIPCHK(hipMalloc(&s->dV, sz * 3));
+        HIPCHK(hipMalloc(&s->dF, sz * 3));
+        const int nsegAlloc = s->nseg < 2 ? 2 : s->nseg;
+        HIPCHK(hipMalloc(&s->dFpart, sz * 3 * nsegAlloc));
+        HIPCHK(hipMalloc(&s->dPsi, sz * 24));
+        HIPCHK(hipMalloc(&s->dTp, sz));
+        HIPCHK(hipMalloc(&s->dUrow, sz));
+        HIPCHK(hipMalloc(&s->dScr, (64 + 3 * NBINS) * sizeof(double)));
+        s->kdeChunks = 64;
+        HIPCHK(hipMalloc(&s->dKde, (size_t)s->kdeChunks * 3 * NBINS * sizeof(double)));
+        s->capS = S; s->capNseg = nsegAlloc;
+        HIPCHK(hipMemsetAsync(s->dR, 0, sz * 3 * W, s->stream));
+        HIPCHK(hipMemsetAsync(s->dV, 0, sz * 3, s->stream));
+        HIPCHK(hipMemsetAsync(s->dF, 0, sz * 3, s->stream));
+        HIPCHK(hipMemsetAsync(s->dPsi, 0, sz * 24, s->stream));
+        HIPCHK(hipMemsetAsync(s->dTp, 0, sz, s->stream));
+    }
+    s->S = S;
+    s->Vholder.assign((size_t)NINTERVALV * 3 * (N > 0 ? N : 1), 0.);
+    return 0;
+}
+
+extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
+    if (!p || !out) return fail("mdqt_create: NULL argument");
+    *out = nullptr;
+    if (p->rng_mode != 1)
+        return fail("rng_mode %d not implemented on the device path (only 1 = Philox)", p->rng_mode);
+    if (p->world_size < 1 || p->rank < 0 || p->rank >= p->world_size) return fail("bad world_size/rank");
+    if (p->N0 < 1) return fail("N0 must be >= 1");
+    if (p->sampleFreq < 1) return fail("sampleFreq must be >= 1");
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev < 1) return fail("no HIP device available (%s)", hipGetErrorString(e));
+    mdqt_ctx* s = new mdqt_ctx();
+    s->p = *p;
+    s->p.saveDirectory[sizeof(s->p.saveDirectory) - 1] = 0;
+    if (p->device >= 0) {
+        if (p->device >= ndev) { delete s; return fail("device %d >= device count %d", p->device, ndev); }
+        s->dev = p->device;
+    } else {
+        (void)hipGetDevice(&s->dev);
+    }
+    if (hipSetDevice(s->dev) != hipSuccess || hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking) != hipSuccess) {
+        delete s;
+        return fail("cannot create HIP stream on device %d", p->device);
+    }
+    s->stream = s->own;
+    build_constants(s);
+    s->t = 0.; s->qidx = 0; s->c0 = p->c0; s->counter = 0;
+    s->x48 = srand48_state(p->seed);
+    strncpy(s->saveDirectory, s->p.saveDirectory, sizeof(s->saveDirectory) - 1);
+    s->saveDirectory[sizeof(s->saveDirectory) - 1] = 0;
+    if (resize(s, 0)) { mdqt_destroy(s); return -1; }
+    *out = s;
+    return 0;
+}
+
+extern "C" void mdqt_destroy(mdqt_ctx* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->dev);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    free_device(s);
+    for (auto& pool : s->evpool)
+        for (hipEvent_t ev : pool) (void)hipEventDestroy(ev);
+    if (s->own) (void)hipStreamDestroy(s->own);
+    delete s;
+}
+
+extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
+    if (!strcmp(n, "gamToEinsteinFreq")) return s->gamToE;
+    if (!strcmp(n, "quantumTimestep")) return s->dtQ;
+    if (!strcmp(n, "plasmaToQuantumTimestepRatio")) return s->ratio;
+    if (!strcmp(n, "plasVelToQuantVel")) return s->pv2q;
+    if (!strcmp(n, "vKick")) return s->vKick;
+    if (!strcmp(n, "vKickDP")) return s->vKickDP;
+    if (!strcmp(n, "lDeb")) return s->lDeb;
+    if (!strcmp(n, "L")) return s->L;
+    if (!strcmp(n, "decayRatioD5Halves")) return s->r;
+    if (!strcmp(n, "kRat")) return s->kRat;
+    if (!strcmp(n, "force_segments")) return s->nseg;
+    if (!strcmp(n, "slab_S")) return s->S;
+    if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
+    return NAN;
+}
+
+// ---------------------------------------------------------------------------------------------
+// state transfer (host <-> HBM); psi: host [N][12][2] interleaved <-> device [24][S]
+// ---------------------------------------------------------------------------------------------
+
+static int upload(mdqt_ctx* s, const double* R, const double* V, size_t ld, const double* psi,
+                  const double* tPart) {
+    const int N = s->N, S = s->S, W = s->p.world_size;
+    HIPCHK(hipSetDevice(s->dev));
+    if (R) {
+        std::vector<double> h((size_t)3 * S * W, 0.);
+        for (int g = 0; g < N; ++g) {
+            const int w = g / S, l = g - w * S;
+            for (int c = 0; c < 3; ++c) h[(size_t)w * 3 * S + (size_t)c * S + l] = R[(size_t)c * ld + g];
+        }
+        HIPCHK(hipMemcpyAsync(s->dR, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    const int lo = s->lo, n = s->nloc;
+    if (V) {
+        std::vector<double> h((size_t)3 * S, 0.);
+        for (int c = 0; c < 3; ++c)
+            for (int i = 0; i < n; ++i) h[(size_t)c * S + i] = V[(size_t)c * ld + lo + i];
+        HIPCHK(hipMemcpyAsync(s->dV, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    if (psi) {
+        std::vector<double> h((size_t)24 * S, 0.);
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < 24; ++k) h[(size_t)k * S + i] = psi[(size_t)(lo + i) * 24 + k];
+        HIPCHK(hipMemcpyAsync(s->dPsi, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    if (tPart) {
+        std::vector<double> h((size_t)S, 0.);
+        for (int i = 0; i < n; ++i) h[i] = tPart[lo + i];
+        HIPCHK(hipMemcpyAsync(s->dTp, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    return 0;
+}
+
+extern "C" int mdqt_set_state(mdqt_ctx* s, int N, const double* R, const double* V, size_t ld,
+                              const double* psi, const double* tPart, double t) {
+    if (!s) return fail("NULL context");
+    if (N != s->N && resize(s, N)) return -1;
+    if (ld < (size_t)N) return fail("ld < N");
+    if (upload(s, R, V, ld, psi, tPart)) return -1;
+    s->t = t;
+    return 0;
+}
+
+extern "C" int mdqt_set_forces(mdqt_ctx* s, const double* F, size_t ld) {
+    const int S = s->S, lo = s->lo, n = s->nloc;
+    std::vector<double> h((size_t)3 * S, 0.);
+    for (int c = 0; c < 3; ++c)
+        for (int i = 0; i < n; ++i) h[(size_t)c * S + i] = F[(size_t)c * ld + lo + i];
+    HIPCHK(hipSetDevice(s->dev));
+    HIPCHK(hipMemcpyAsync(s->dF, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int mdqt_get_state(mdqt_ctx* s, double* R, double* V, double* F, size_t ld, double* psi,
+                              double* tPart, double* t) {
+    if (!s) return fail("NULL context");
+    const int N = s->N, S = s->S, W = s->p.world_size, lo = s->lo, n = s->nloc;
+    if (ld < (size_t)N) return fail("ld < N");
+    HIPCHK(hipSetDevice(s->dev));
+    if (R) {
+        std::vector<double> h((size_t)3 * S * W);
+        HIPCHK(hipMemcpyAsync(h.data(), s->dR, h.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        for (int g = 0; g < N; ++g) {
+            const int w = g / S, l = g - w * S;
+            for (int c = 0; c < 3; ++c) R[(size_t)c * ld + g] = h[(size_t)w * 3 * S + (size_t)c * S + l];
+        }
+    }
+    auto get3 = [&](const double* d, double* out) -> int {
+        std::vector<double> h((size_t)3 * S);
+        HIPCHK(hipMemcpyAsync(h.data(), d, h.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        for (int c = 0; c < 3; ++c)
+            for (int i = 0; i < n; ++i) out[(size_t)c * ld + lo + i] = h[(size_t)c * S + i];
+        return 0;
+    };
+    if (V && get3(s->dV, V)) return -1;
+    if (F && get3(s->dF, F)) return -1;
+    if (psi) {
+        std::vector<double> h((size_t)24 * S);
+        HIPCHK(hipMemcpyAsync(h.data(), s->dPsi, h.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < 24; ++k) psi[(size_t)(lo + i) * 24 + k] = h[(size_t)k * S + i];
+    }
+    if (tPart) {
+        std::vector<double> h((size_t)S);
+        HIPCHK(hipMemcpyAsync(h.data(), s->dTp, h.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        for (int i = 0; i < n; ++i) tPart[lo + i] = h[i];
+    }
+    if (t) *t = s->t;
+    return 0;
+}
+
+extern "C" int mdqt_get_N(const mdqt_ctx* s) { return s ? s->N : -1; }
+extern "C" double mdqt_get_time(const mdqt_ctx* s) { return s->t; }
+extern "C" int mdqt_set_time(mdqt_ctx* s, double t) { s->t = t; return 0; }
+extern "C" uint64_t mdqt_get_qstep_index(const mdqt_ctx* s) { return s->qidx; }
+extern "C" int mdqt_set_qstep_index(mdqt_ctx* s, uint64_t q) { s->qidx = q; return 0; }
+extern "C" int mdqt_get_counters(const mdqt_ctx* s, int* c0, unsigned* counter, double* Epot, double* Epot0) {
+    if (c0) *c0 = s->c0;
+    if (counter) *counter = s->counter;
+    if (Epot) *Epot = s->Epot;
+    if (Epot0) *Epot0 = s->Epot0;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// init (SpeedUp:289-348): drand48 rejection sampling, bit-exact with the reference stream
+// ---------------------------------------------------------------------------------------------
+
+extern "C" int mdqt_init(mdqt_ctx* s) {
+    if (!s) return fail("NULL context");
+    const double L = s->L;
+    const double N9L = (unsigned)(9. * 9. * 9. * (L * L * L) * 3. / (4. * M_PI));   // :299
+    std::vector<double> X, Y, Z, psi;
+    const size_t guess = (size_t)s->p.N0 + 1000;
+    X.reserve(guess); Y.reserve(guess); Z.reserve(guess); psi.reserve(guess * 24);
+    s->x48 = srand48_state(s->p.seed);                                                // :1219
+    for (long i = 0; i < N9L; i++) {                                                  // :303
+        const double x = 9. * L * drand48_next(&s->x48) - 4. * L;
+        const double y = 9. * L * drand48_next(&s->x48) - 4. * L;
+        const double z = 9. * L * drand48_next(&s->x48) - 4. * L;
+        if (x <= L && y <= L && z <= L && x > 0 && y > 0 && z > 0) {                 // :308
+            X.push_back(x); Y.push_back(y); Z.push_back(z);
+            const double rand1 = drand48_next(&s->x48);                                // :317-328
+            const double rand2 = drand48_next(&s->x48);
+            const double rand3 = drand48_next(&s->x48);
+            double sign = 1;
+            if (rand3 < 0.5) sign = -1;
+            const double rand4 = drand48_next(&s->x48);
+            double sign2 = 1;
+            if (rand4 < 0.5) sign2 = -1;
+            double w[24] = {0};                                                        // :329-332
+            w[0] = sqrt(rand1);
+            w[2] = sign2 * sqrt(1 - rand1) * sqrt(rand2);
+            w[3] = sign * sqrt(1 - rand1) * sqrt(1 - rand2);
+            psi.insert(psi.end(), w, w + 24);
+        }
+    }
+    const int N = (int)X.size();
+    std::vector<double> R((size_t)3 * N), V((size_t)3 * N, 0.), tp((size_t)N, 0.);
+    for (int i = 0; i < N; ++i) { R[i] = X[i]; R[(size_t)N + i] = Y[i]; R[(size_t)2 * N + i] = Z[i]; }
+    if (resize(s, N)) return -1;
+    if (upload(s, R.data(), V.data(), N, psi.data(), tp.data())) return -1;
+    double e;
+    if (mdqt_epotential(s, &e)) return -1;                                           // :345-347
+    s->Epot0 = s->Epot;
+    s->c0 = -1;
+    s->t = 0.;
+    s->qidx = 0;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// hot path
+// ---------------------------------------------------------------------------------------------
+
+static ForceArgs force_args(mdqt_ctx* s, double* out) {
+    ForceArgs a;
+    a.Rall = s->dR;
+    a.Fpart = out;
+    a.N = s->N; a.S = s->S;
+    a.row_lo = s->lo; a.nrows = s->nloc;
+    a.nseg = s->nseg; a.seglen = s->seglen;
+    a.L = s->L; a.lDeb = s->lDeb; a.Rcut = s->L / 2.;     // :196
+    return a;
+}
+
+// record the next timing event of kind k (start/stop alternate)
+static int mark(mdqt_ctx* s, int k) {
+    auto& pool = s->evpool[k];
+    if (s->evused[k] == (int)pool.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        pool.push_back(e);
+    }
+    HIPCHK(hipEventRecord(pool[s->evused[k]++], s->stream));
+    return 0;
+}
+
+extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:192-236
+    if (!s) return fail("NULL context");
+    if (s->nloc == 0) return 0;
+    HIPCHK(hipSetDevice(s->dev));
+    if (s->timing && mark(s, 0)) return -1;
+    if (s->nseg == 1) {
+        HIPCHK(launch_forces(force_args(s, s->dF), s->stream));
+    } else {
+        HIPCHK(launch_forces(force_args(s, s->dFpart), s->stream));
+        HIPCHK(launch_reduce_segments(s->dFpart, s->dF, s->nseg, s->nloc, s->S, 3, s->stream));
+    }
+    if (s->timing && mark(s, 0)) return -1;
+    return 0;
+}
+
+// n substeps of (step if do_step; qstep if do_qt_flag) — t advances only when advance_t
+static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int advance_t) {
+    HIPCHK(hipSetDevice(s->dev));
+    const int do_qt = do_qt_flag && s->p.qt_enabled;
+    while (n > 0) {
+        const int m = n < MAXSUB ? n : MAXSUB;
+        SubstepArgs a;
+        memset(&a, 0, sizeof a);
+        a.R = s->dR + (size_t)s->p.rank * 3 * s->S;
+        a.V = s->dV; a.F = s->dF; a.psi = s->dPsi; a.tPart = s->dTp;
+        a.n = s->nloc; a.S = s->S; a.gid0 = (uint64_t)s->lo;
+        a.q0 = s->qidx;
+        a.nsub = m; a.do_step = do_step; a.do_qt = do_qt;
+        a.L = s->L;
+        a.qc = s->qc;
+        double t = s->t;
+        for (int k = 0; k < m; ++k) {
+            a.t[k] = t;
+            a.expDet[k] = expDetuning_of(&s->p, t);
+            if (advance_t) t += s->dtQ;                    // qstep: t += dtQuant (:716)
+        }
+        if (s->timing && mark(s, 1)) return -1;
+        HIPCHK(launch_substeps(a, s->stream));
+        if (s->timing && mark(s, 1)) return -1;
+        if (advance_t) {
+            s->t = t;
+            s->qidx += (uint64_t)m;
+        }
+        n -= m;
+    }
+    return 0;
+}
+
+extern "C" int mdqt_step(mdqt_ctx* s) { return s ? run_substeps(s, 1, 1, 0, 0) : fail("NULL context"); }
+extern "C" int mdqt_qstep(mdqt_ctx* s) { return s ? run_substeps(s, 1, 0, 1, 1) : fail("NULL context"); }
+extern "C" int mdqt_substeps(mdqt_ctx* s, int n) {
+    if (!s) return fail("NULL context");
+    if (n < 0) return fail("negative substep count");
+    return run_substeps(s, n, 1, 1, 1);
+}
+
+extern "C" int mdqt_md_steps(mdqt_ctx* s, int n) {
+    if (!s) return fail("NULL context");
+    for (int k = 0; k < n; ++k) {
+        if (mdqt_forces(s)) return -1;
+        s->c0++;
+        if (mdqt_substeps(s, s->ratio)) return -1;
+    }
+    return 0;
+}
+
+// stateless pair kernels on host arrays (tests, and the MD-only programs' force seam)
+static int pairs_raw(int mode, int N, double L, double lDeb, const double* R, size_t ld, double* out,
+                     int nseg_req, int device) {
+    if (N < 1 || !R || !out || ld < (size_t)N) return fail("pairs_raw: bad arguments");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail("no HIP device available");
+    if (device >= 0) HIPCHK(hipSetDevice(device));
+    int lo, hi, S;
+    if (mdqt_slab(N, 1, 0, &lo, &hi, &S)) return -1;
+    mdqt_ctx tmp;                                   // only for choose_segments
+    tmp.N = N; tmp.p.force_segments = nseg_req;
+    choose_segments(&tmp);
+    const int nseg = tmp.nseg;
+    std::vector<double> h((size_t)3 * S, 0.);
+    for (int c = 0; c < 3; ++c)
+        for (int i = 0; i < N; ++i) h[(size_t)c * S + i] = R[(size_t)c * ld + i];
+    double *dR = nullptr, *dP = nullptr, *dO = nullptr;
+    hipStream_t st;
+    HIPCHK(hipStreamCreate(&st));
+    HIPCHK(hipMalloc(&dR, h.size() * sizeof(double)));
+    HIPCHK(hipMalloc(&dP, (size_t)3 * S * nseg * sizeof(double)));
+    HIPCHK(hipMalloc(&dO, (size_t)3 * S * sizeof(double)));
+    HIPCHK(hipMemcpyAsync(dR, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    ForceArgs a;
+    a.Rall = dR; a.Fpart = dP; a.N = N; a.S = S; a.row_lo = 0; a.nrows = N;
+    a.nseg = nseg; a.seglen = tmp.seglen; a.L = L; a.lDeb = lDeb; a.Rcut = L / 2.;
+    HIPCHK(mode == 0 ? launch_forces(a, st) : launch_potential_rows(a, st));
+    HIPCHK(launch_reduce_segments(dP, dO, nseg, N, S, mode == 0 ? 3 : 1, st));
+    HIPCHK(hipMemcpyAsync(h.data(), dO, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipFree(dR)); HIPCHK(hipFree(dP)); HIPCHK(hipFree(dO));
+    HIPCHK(hipStreamDestroy(st));
+    if (mode == 0) {
+        for (int c = 0; c < 3; ++c)
+            for (int i = 0; i < N; ++i) out[(size_t)c * ld + i] = h[(size_t)c * S + i];
+    } else {
+        for (int i = 0; i < N; ++i) out[i] = h[i];
+    }
+    return 0;
+}
+
+extern "C" int mdqt_forces_raw(int N, double L, double lDeb, const double* R, size_t ld, double* F,
+                               int nseg, int device) {
+    return pairs_raw(0, N, L, lDeb, R, ld, F, nseg, device);
+}
+
+extern "C" int mdqt_potentials_raw(int N, double L, double lDeb, const double* R, size_t ld, double* U,
+                                   int nseg, int device) {
+    return pairs_raw(1, N, L, lDeb, R, ld, U, nseg, device);
+}
+
+// ---------------------------------------------------------------------------------------------
+// observables (Epotential :244-281, output :917-1032)
+// ---------------------------------------------------------------------------------------------
+
+// device: scratch[0] = sum over owned rows of the full-row pair potential
+static int potential_rows(mdqt_ctx* s, double* urow_dev) {
+    if (s->nloc == 0) return 0;
+    HIPCHK(launch_potential_rows(force_args(s, s->dFpart), s->stream));
+    HIPCHK(launch_reduce_segments(s->dFpart, urow_dev, s->nseg, s->nloc, s->S, 1, s->stream));
+    return 0;
+}
+
+extern "C" int mdqt_partial_observables(mdqt_ctx* s, double vxAvg, double out5[5], double* Pvel) {
+    if (!s) return fail("NULL context");
+    HIPCHK(hipSetDevice(s->dev));
+    double* scr = s->dScr;           // [0] sum vx, [8] vxAvg, [16..19] sums, [64..] KDE bins
+    if (potential_rows(s, s->dUrow)) return -1;
+    HIPCHK(launch_sum_vx(s->dV, s->nloc, scr, s->stream));
+    HIPCHK(hipMemcpyAsync(scr + 8, &vxAvg, sizeof(double), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(launch_energy_sums(s->dV, s->nloc, s->S, scr + 8, s->dUrow, scr + 16, s->stream));
+    int nch = s->nloc / 256;
+    if (nch < 1) nch = 1;
+    if (nch > s->kdeChunks) nch = s->kdeChunks;
+    double* Pout = scr + 64;
+    if (s->nloc > 0) HIPCHK(launch_kde(s->dV, s->nloc, s->S, scr + 8, s->dKde, nch, Pout, s->stream));
+    else HIPCHK(hipMemsetAsync(Pout, 0, 3 * NBINS * sizeof(double), s->stream));
+    double h[64 + 3 * NBINS];
+    HIPCHK(hipMemcpyAsync(h, scr, sizeof h, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    out5[0] = s->nloc ? h[0] : 0.;
+    out5[1] = s->nloc ? h[16] : 0.; out5[2] = s->nloc ? h[17] : 0.; out5[3] = s->nloc ? h[18] : 0.;
+    out5[4] = s->nloc ? h[19] : 0.;
+    if (Pvel) memcpy(Pvel, h + 64, 3 * NBINS * sizeof(double));
+    return 0;
+}
+
+extern "C" int mdqt_epotential(mdqt_ctx* s, double* Epot) {   // Epotential(), :244-281
+    if (!s) return fail("NULL context");
+    if (s->p.world_size != 1) return fail("mdqt_epotential: use mdqt_partial_observables under sharding");
+    double o[5];
+    if (mdqt_partial_observables(s, 0., o, nullptr)) return -1;
+    // sum_{i<j} u = (sum_i sum_{j != i} u) / 2 ; Epot /= N (:280)
+    s->Epot = s->N > 0 ? (o[4] / 2.) / (double)s->N : 0.;
+    if (Epot) *Epot = s->Epot;
+    return 0;
+}
+
+extern "C" int mdqt_observables(mdqt_ctx* s, double out7[7], double* Pvel, double* pops) {
+    if (!s) return fail("NULL context");
+    if (s->p.world_size != 1) return fail("mdqt_observables: use mdqt_partial_observables under sharding");
+    const int N = s->N;
+    double o[5];
+    // pass 1: <vx> (:934-938)
+    HIPCHK(hipSetDevice(s->dev));
+    HIPCHK(launch_sum_vx(s->dV, s->nloc, s->dScr, s->stream));
+    double sumvx = 0.;
+    HIPCHK(hipMemcpyAsync(&sumvx, s->dScr, sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    const double velXAvg = N > 0 ? sumvx / (double)N : 0.;
+    std::vector<double> P((size_t)3 * NBINS);
+    if (mdqt_partial_observables(s, velXAvg, o, P.data())) return -1;
+    const double EkinX = o[1] / (double)N, EkinY = o[2] / (double)N, EkinZ = o[3] / (double)N;   // :945-947
+    s->Epot = (o[4] / 2.) / (double)N;                                                          // :948
+    out7[0] = s->t; out7[1] = EkinX; out7[2] = EkinY; out7[3] = EkinZ; out7[4] = s->Epot;
+    out7[5] = EkinX + EkinY + EkinZ + s->Epot - s->Epot0; out7[6] = velXAvg;                   // :954
+    if (Pvel) {
+        const double norm = (6.0 * sqrt(2 * M_PI * 0.002 * 0.002));                            // :975-978
+        for (int j = 0; j < 3 * NBINS; ++j) Pvel[j] = P[j] / norm;
+    }
+    if (pops) {                                                                                 // :1016-1023
+        std::vector<double> psi((size_t)24 * N);
+        if (mdqt_get_state(s, nullptr, nullptr, nullptr, N, psi.data(), nullptr, nullptr)) return -1;
+        for (int i = 0; i < N; i++) {
+            const double* w = psi.data() + (size_t)24 * i;
+            auto nrm = [&](int k) { return w[2 * k] * w[2 * k] + w[2 * k + 1] * w[2 * k + 1]; };
+            pops[3 * i + 0] = nrm(0) + nrm(1);
+            pops[3 * i + 1] = nrm(2) + nrm(3) + nrm(4) + nrm(5);
+            pops[3 * i + 2] = nrm(6) + nrm(7) + nrm(8) + nrm(9) + nrm(10) + nrm(11);
+        }
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// files (reference formats, SpeedUp:725-1032) and the time loop (main, :1139-1383)
+// ---------------------------------------------------------------------------------------------
+
+static FILE* open_in(const mdqt_ctx* s, const char* name, const char* mode) {
+    char path[1400];
+    snprintf(path, sizeof(path), "%s%s", s->saveDirectory, name);
+    FILE* f = fopen(path, mode);
+    if (!f) fail("cannot open %s: %s", path, strerror(errno));
+    return f;
+}
+
+extern "C" const char* mdqt_save_directory(const mdqt_ctx* s) { return s->saveDirectory; }
+
+// the reference's "(unsigned)(x)" printed with %d (x86-64 runtime behaviour)
+static int ref_udcast(double x) { return (int)(uint32_t)(int64_t)x; }
+
+extern "C" int mdqt_setup_directories(mdqt_ctx* s) {       // SpeedUp:1145-1160
+    const mdqt_params* p = &s->p;
+    char base[512];
+    strncpy(base, p->saveDirectory, sizeof(base) - 1);
+    base[sizeof(base) - 1] = 0;
+    mkdir(base, 0777);
+    char name[256];
+    snprintf(name, sizeof name, "Ge%dDensity%dE+11Sig0%dTe%dSigFrac%dDetSP%dDetDP%dOmSP%dOmDP%dNumIons%d",
+             ref_udcast(100 * p->Ge), ref_udcast(p->density * 1000), ref_udcast(10 * p->sig0), ref_udcast(p->Te),
+             ref_udcast(p->fracOfSig * 100), ref_udcast(p->detuning * 100), ref_udcast(p->detuningDP * 100),
+             ref_udcast(p->Om * 100), ref_udcast(p->OmDP * 100), ref_udcast((double)p->N0));
+    snprintf(s->saveDirectory, sizeof(s->saveDirectory), "%s%s", base, name);
+    mkdir(s->saveDirectory, 0777);
+    char jb[64];
+    snprintf(jb, sizeof jb, "/job%d/", (int)p->job);
+    strncat(s->saveDirectory, jb, sizeof(s->saveDirectory) - strlen(s->saveDirectory) - 1);
+    mkdir(s->saveDirectory, 0777);
+    struct stat st;
+    if (stat(s->saveDirectory, &st) != 0 || !S_ISDIR(st.st_mode))
+        return fail("cannot create output directory %s", s->saveDirectory);
+    return 0;
+}
+
+extern "C" int mdqt_output(mdqt_ctx* s) {                 // output(), SpeedUp:917-1032
+    const int N = s->N;
+    double o[7];
+    std::vector<double> P((size_t)3 * NBINS), pops((size_t)3 * (N > 0 ? N : 1)), V((size_t)3 * (N > 0 ? N : 1));
+    if (mdqt_observables(s, o, P.data(), pops.data())) return -1;
+    if (mdqt_get_state(s, nullptr, V.data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
+    FILE* fa = open_in(s, "energies.dat", "a");
+    if (!fa) return -1;
+    fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\t%lg\n", o[0], o[1], o[2], o[3], o[4], o[5], o[6]);   // :954
+    fclose(fa);
+    char b1[64], b2[64], b3[64];
+    snprintf(b1, sizeof b1, "vel_distX_time%06d.dat", s->counter);
+    snprintf(b2, sizeof b2, "vel_distY_time%06d.dat", s->counter);
+    snprintf(b3, sizeof b3, "vel_distZ_time%06d.dat", s->counter);
+    FILE *f1 = open_in(s, b1, "w"), *f2 = open_in(s, b2, "w"), *f3 = open_in(s, b3, "w");
+    if (!f1 || !f2 || !f3) {
+        if (f1) fclose(f1);
+        if (f2) fclose(f2);
+        if (f3) fclose(f3);
+        return -1;
+    }
+    for (int i = 0; i < NBINS; i++) {                                                    // :983-1006
+        fprintf(f1, "%lg\t%lg\n", s->vel[i] + o[6], P[i]);
+        fprintf(f2, "%lg\t%lg\n", s->vel[i], P[NBINS + i]);
+        fprintf(f3, "%lg\t%lg\n", s->vel[i], P[2 * NBINS + i]);
+    }
+    fclose(f1); fclose(f2); fclose(f3);
+    snprintf(b1, sizeof b1, "statePopulationsVsVTime%06d.dat", s->counter);
+    fa = open_in(s, b1, "w");
+    if (!fa) return -1;
+    for (int i = 0; i < N; i++)                                                          // :1010-1024
+        fprintf(fa, "%lg\t%lg\t%lg\t%lg\n", V[i], pops[3 * i], pops[3 * i + 1], pops[3 * i + 2]);
+    fclose(fa);
+    s->counter++;                                                                        // :1027
+    return 0;
+}
+
+extern "C" int mdqt_write_conditions(mdqt_ctx* s, int c0) {   // writeConditions, :725-784
+    const int N = s->N;
+    std::vector<double> R((size_t)3 * (N > 0 ? N : 1)), V(R.size()), psi((size_t)24 * (N > 0 ? N : 1));
+    if (mdqt_get_state(s, R.data(), V.data(), nullptr, N, psi.data(), nullptr, nullptr)) return -1;
+    char b[96];
+    snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
+    FILE* fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    fprintf(fa, "%i\t%i", N, s->counter);                                                // :737
+    fclose(fa);
+    snprintf(b, sizeof b, "conditions_timestep%06d.dat", c0);
+    fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    for (int i = 0; i < N; i++)                                                          // :747
+        fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\t\n", R[i], R[(size_t)N + i], R[(size_t)2 * N + i], V[i],
+                V[(size_t)N + i], V[(size_t)2 * N + i]);
+    fclose(fa);
+    for (int v = 0; v < NINTERVALV; v++) {                                              // :752-763
+        snprintf(b, sizeof b, "VZERO_timestep%06d_interval%d.dat", c0, v);
+        fa = open_in(s, b, "w");
+        if (!fa) return -1;
+        const double* vh = s->Vholder.data() + (size_t)v * 3 * N;
+        for (int i = 0; i < N; i++) fprintf(fa, "%lg\t%lg\t%lg\n", vh[i], vh[(size_t)N + i], vh[(size_t)2 * N + i]);
+        fclose(fa);
+    }
+    snprintf(b, sizeof b, "wvFns_timestep%06d.dat", c0);
+    fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    for (int j = 0; j < N; j++) {                                                        // :777-779
+        const double* ps = psi.data() + (size_t)24 * j;
+        for (int k = 0; k < NS; k++) fprintf(fa, "%lg\t%lg\t", ps[2 * k], ps[2 * k + 1]);
+        fprintf(fa, "\n");
+    }
+    fclose(fa);
+    return 0;
+}
+
+extern "C" int mdqt_read_conditions(mdqt_ctx* s, int c0) {    // readConditions, :785-916
+    s->t = ((double)c0 - 9.) * TIMESTEP + 0.02;                                         // :789
+    char b[96];
+    snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
+    FILE* fa = open_in(s, b, "r");
+    if (!fa) return -1;
+    int j, m, N = -1;
+    while (fscanf(fa, "%i\t%i", &j, &m) == 2) { N = j; s->counter = (unsigned)m; }      // :805-814
+    fclose(fa);
+    if (N < 0) return fail("%s: no ion count", b);
+    std::vector<double> R((size_t)3 * (N > 0 ? N : 1), 0.), V(R.size(), 0.), psi((size_t)24 * (N > 0 ? N : 1), 0.);
+    snprintf(b, sizeof b, "conditions_timestep%06d.dat", c0);
+    fa = open_in(s, b, "r");
+    if (!fa) return -1;
+    double a, bb, z, d, e, f;
+    int i = 0;
+    while (i < N && fscanf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\n", &a, &bb, &z, &d, &e, &f) == 6) {   // :818-832
+        R[i] = a; R[(size_t)N + i] = bb; R[(size_t)2 * N + i] = z;
+        V[i] = d; V[(size_t)N + i] = e; V[(size_t)2 * N + i] = f;
+        i++;
+    }
+    fclose(fa);
+    if (i != N) return fail("%s: %d of %d rows", b, i, N);
+    snprintf(b, sizeof b, "wvFns_timestep%06d.dat", c0);
+    fa = open_in(s, b, "r");
+    if (!fa) return -1;
+    i = 0;
+    double w[24];
+    while (i < N &&
+           fscanf(fa, "%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\t%lg%lg\n",
+                  &w[0], &w[1], &w[2], &w[3], &w[4], &w[5], &w[6], &w[7], &w[8], &w[9], &w[10], &w[11], &w[12],
+                  &w[13], &w[14], &w[15], &w[16], &w[17], &w[18], &w[19], &w[20], &w[21], &w[22], &w[23]) == 24) {  // :859-894
+        memcpy(psi.data() + (size_t)24 * i, w, sizeof(w));
+        i++;
+    }
+    fclose(fa);
+    if (i != N) return fail("%s: %d of %d rows", b, i, N);
+    const double t = s->t;
+    if (resize(s, N)) return -1;
+    for (int v = 0; v < NINTERVALV; v++) {                                              // :898-913
+        snprintf(b, sizeof b, "VZERO_timestep%06d_interval%d.dat", c0, v);
+        fa = open_in(s, b, "r");
+        if (!fa) return -1;
+        double* vh = s->Vholder.data() + (size_t)v * 3 * N;
+        i = 0;
+        while (i < N && fscanf(fa, "%lg\t%lg\t%lg", &a, &bb, &z) == 3) {
+            vh[i] = a; vh[(size_t)N + i] = bb; vh[(size_t)2 * N + i] = z;
+            i++;
+        }
+        fclose(fa);
+    }
+    std::vector<double> tp((size_t)(N > 0 ? N : 1), 0.);       // tPart not restored (App. C-8)
+    if (upload(s, R.data(), V.data(), N, psi.data(), tp.data())) return -1;
+    s->t = t;
+    s->c0 = c0;
+    s->qidx = (uint64_t)(c0 + 1) * (uint64_t)s->ratio;
+    return 0;
+}
+
+extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp:1139-1383
+    if (!s) return fail("NULL context");
+    if (s->p.world_size != 1) return fail("mdqt_run drives one GPU; the sharded loop lives in the host driver");
+    if (mdqt_setup_directories(s)) return -1;
+    if (s->p.newRun == 1) {
+        if (mdqt_init(s)) return -1;
+    } else {
+        s->c0 = s->p.c0;
+        if (mdqt_read_conditions(s, s->c0)) return -1;
+    }
+    const double tend = s->p.tmax + 0.0009;
+    const int sf = s->p.sampleFreq, ratio = s->ratio;
+    int tsc = ratio;                                                                    // :1235
+    while (s->t <= tend) {                                                              // :1248
+        if ((s->c0 + 1) % sf == 0 && tsc == 1)                                          // :1365
+            if (mdqt_output(s)) return -1;
+        if (tsc == ratio) {                                                             // :1369
+            if (mdqt_forces(s)) return -1;
+            s->c0++;
+            tsc = 0;
+        }
+        // fuse the following iterations while they are pure step();qstep() (App. C-9)
+        int n = 0, ts = tsc;
+        double tt = s->t;
+        do {
+            n++; ts++; tt += s->dtQ;
+        } while (n < MAXSUB && tt <= tend && !((s->c0 + 1) % sf == 0 && ts == 1) && ts != ratio);
+        if (mdqt_substeps(s, n)) return -1;                                            // :1376-1377
+        tsc += n;
+    }
+    return mdqt_write_conditions(s, s->c0);                                            // :1381
+}
+
+// ---------------------------------------------------------------------------------------------
+// streams, timing, multi-GPU plumbing
+// ---------------------------------------------------------------------------------------------
+
+extern "C" int mdqt_set_stream(mdqt_ctx* s, void* st) {
+    s->stream = st ? (hipStream_t)st : s->own;
+    return 0;
+}
+extern "C" void* mdqt_get_stream(mdqt_ctx* s) { return (void*)s->stream; }
+extern "C" int mdqt_synchronize(mdqt_ctx* s) {
+    HIPCHK(hipSetDevice(s->dev));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return 0;
+}
+extern "C" int mdqt_positions_device(mdqt_ctx* s, void** dptr, int* S) {
+    if (dptr) *dptr = (void*)s->dR;
+    if (S) *S = s->S;
+    return 0;
+}
+extern "C" int mdqt_enable_timing(mdqt_ctx* s, int on) {
+    s->timing = on != 0;
+    s->evused[0] = s->evused[1] = 0;
+    return 0;
+}
+
+extern "C" int mdqt_kernel_time_totals(mdqt_ctx* s, double* force_ms, int* nforce, double* sub_ms, int* nsub) {
+    HIPCHK(hipSetDevice(s->dev));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    double tot[2] = {0., 0.};
+    for (int k = 0; k < 2; ++k)
+        for (int i = 0; i + 1 < s->evused[k]; i += 2) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, s->evpool[k][i], s->evpool[k][i + 1]));
+            tot[k] += ms;
+        }
+    if (force_ms) *force_ms = tot[0];
+    if (nforce) *nforce = s->evused[0] / 2;
+    if (sub_ms) *sub_ms = tot[1];
+    if (nsub) *nsub = s->evused[1] / 2;
+    s->evused[0] = s->evused[1] = 0;
+    return 0;
+}

@@ -1,0 +1,85 @@
+// Internal interface between the host engine (mdqt_engine.cpp) and the gfx950 kernels
+// (mdqt_kernels.hip).  Plain structs passed BY VALUE as kernel arguments (no __constant__
+// globals: several contexts with different parameters may live in one process).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mdqt {
+
+constexpr int NS = 12;          // numStates, SpeedUp:153
+constexpr int NBINS = 2001;     // SpeedUp:120-123
+constexpr int MAXSUB = 32;      // substeps fused into one launch (ratio = 25 at density 2)
+constexpr int NSTATIC = 20;     // static off-diagonal entries of M = I - i h H (App. A)
+
+// Static couplings of the non-Hermitian Hamiltonian, as (row, col) of M; order of this
+// table is the index used by the kernels (SpeedUp:1206-1215, cs[] at :1163-1180).
+constexpr int kStaticRC[NSTATIC][2] = {
+    {0, 3}, {0, 5}, {1, 2}, {1, 4}, {2, 1}, {2, 9}, {2, 11}, {3, 0}, {3, 8}, {3, 10},
+    {4, 1}, {4, 7}, {5, 0}, {5, 6}, {6, 5}, {7, 4}, {8, 3}, {9, 2}, {10, 3}, {11, 2}};
+
+// Constants of qstep() (SpeedUp:438-717), all precomputed on the host with the reference's
+// own operation order so that device and oracle agree bit for bit where the math allows.
+struct QTConst {
+    double dtQ, gamToE;         // quantumTimestep, gamToEinsteinFreq (:79, :84)
+    double h, dtHalf, invh;     // dtQ*gamToE, dtQ*gamToE/2, 1/(dtQ*gamToE)  (:525-567)
+    double pv2q;                // plasVelToQuantVel (:85)
+    double kRat, r;             // :146-147
+    double det, detDP;          // detuning, detuningDP (:70-71)
+    double kickS, kickD;        // 1*vKick*Om, vKickDP*(OmDP/r) (:503)
+    double vKick, vKickDP;      // jump kicks (:589-610)
+    double pD;                  // r/(r+1): D-decay branch probability (:589)
+    double dP[4];               // decayMatrix diagonal on P levels 2..5 (:1203)
+    double hdP[4];              // imag of hamDecayTerm diagonal on P levels (:1202)
+    double a8, a11;             // OmDP/2*gs[8]/sqrt(r), OmDP/2*gs[11]/sqrt(r) (:508)
+    double Mre[NSTATIC], Mim[NSTATIC];   // static off-diagonal M entries
+    double thS3, thS4;          // gs[2]^2, gs[4]^2 (S-decay target thresholds)
+    double thD[4][2];           // cumulative D-decay thresholds per P level (:612-697)
+    double gs[18];
+    int renorm;                 // reNormalizewvFns (:706-712)
+    uint32_t seed, job;         // Philox key
+};
+
+struct SubstepArgs {
+    double* R;          // this rank's slab of the gathered positions, [3][S]
+    double* V;          // [3][S]
+    const double* F;    // [3][S]
+    double* psi;        // [24][S]: component-major (re0, im0, re1, ... im11)
+    double* tPart;      // [S]
+    int n;              // ions in this slab
+    int S;              // slab stride (doubles)
+    uint64_t gid0;      // global id of local ion 0
+    uint64_t q0;        // qstep index of the first substep
+    int nsub, do_step, do_qt;
+    double L;
+    double t[MAXSUB];       // global time at each substep (t before qstep advances it)
+    double expDet[MAXSUB];  // expDetuning(t) (:447)
+    QTConst qc;
+};
+
+struct ForceArgs {
+    const double* Rall; // gathered positions [world][3][S]
+    double* Fpart;      // [nseg][3][S]: partial sums of the owned rows per j-segment
+    int N, S;           // ions, slab stride
+    int row_lo, nrows;  // owned global rows [row_lo, row_lo + nrows)
+    int nseg, seglen;   // j segmentation (a function of N only)
+    double L, lDeb, Rcut;
+};
+
+// ---- launchers (mdqt_kernels.hip) ----
+hipError_t launch_forces(const ForceArgs& a, hipStream_t s);
+hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
+                                  hipStream_t s);
+hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[seg][0][i]
+hipError_t launch_substeps(const SubstepArgs& a, hipStream_t s);
+// deterministic sums: out[0] = sum vx; needs scratch >= 1024 doubles
+hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s);
+// out[0..2] = sum 0.5 (vx-avg)^2, 0.5 vy^2, 0.5 vz^2 ; out[3] = sum of rows[0..nrows) of
+// the potential partials reduced over segments (caller passes the reduced row buffer)
+hipError_t launch_energy_sums(const double* V, int n, int S, const double* vxAvg,
+                              const double* urow, double* out, hipStream_t s);
+// KDE partials: P[ichunk][3][2001]; then reduce into Pout[3][2001] (unnormalised)
+hipError_t launch_kde(const double* V, int n, int S, const double* vxAvg, double* Ppart,
+                      int nchunk, double* Pout, hipStream_t s);
+
+}  // namespace mdqt

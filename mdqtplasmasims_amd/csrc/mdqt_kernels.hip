@@ -1,0 +1,495 @@
+// gfx950 kernels of the MDQT hot path.
+//
+//   k_pairs<FORCE>      Yukawa all-pairs force, forces() SpeedUp:192-236
+//   k_pairs<POTENTIAL>  pair potential rows,    Epotential() SpeedUp:244-281
+//   k_substeps          n x (step(); qstep()) fused per ion, SpeedUp:356-430 + :438-717
+//   k_sum_vx / k_energy_sums / k_kde*   observables of output(), SpeedUp:917-1032
+//
+// Built with -ffp-contract=off and without fast-math: every floating-point expression keeps
+// the reference's operation order (x86-64 g++ -O3 contracts nothing), so the only
+// device/host differences left are libm ulps (exp, sin, cos).  See DESIGN.md §Parity.
+#include "mdqt_internal.hpp"
+
+#include <math.h>
+
+namespace mdqt {
+
+// ------------------------------------------------------------------------------------------
+// position addressing: gathered array [world][3][S]; global ion g lives in slab g / S
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ const double* pos_base(const double* Rall, int g, int S) {
+    const int w = g / S;
+    return Rall + (size_t)w * 3 * S + (g - w * S);
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 1: all-pairs Yukawa force / potential, owner-computes rows, LDS-staged j tiles.
+// Row i of the owned slab accumulates f(i, j) over its j segment in ASCENDING j — in the
+// single-thread reference F_i is exactly that ascending sum, so with one
+// segment the result matches the reference order; with nseg > 1 the segment partials are
+// summed in ascending segment order by k_reduce_segments (deterministic).
+// ------------------------------------------------------------------------------------------
+constexpr int FT = 256;   // threads per block = rows per block = j tile
+
+template <int MODE>   // 0: force, 1: potential
+__global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
+    __shared__ double sx[FT], sy[FT], sz[FT];
+    const int tid = threadIdx.x;
+    const int li = blockIdx.x * FT + tid;
+    const int seg = blockIdx.y;
+    const bool active = li < a.nrows;
+    const int gi = a.row_lo + li;
+    double rx = 0., ry = 0., rz = 0.;
+    if (active) {
+        const double* p = pos_base(a.Rall, gi, a.S);
+        rx = p[0]; ry = p[a.S]; rz = p[2 * a.S];
+    }
+    const double L = a.L, lDeb = a.lDeb, Rcut = a.Rcut;
+    double fx = 0., fy = 0., fz = 0.;
+    const int j0 = seg * a.seglen;
+    const int j1 = min(a.N, j0 + a.seglen);
+    for (int jt = j0; jt < j1; jt += FT) {
+        const int jl = jt + tid;
+        __syncthreads();
+        if (jl < j1) {
+            const double* p = pos_base(a.Rall, jl, a.S);
+            sx[tid] = p[0]; sy[tid] = p[a.S]; sz[tid] = p[2 * a.S];
+        }
+        __syncthreads();
+        const int nj = min(FT, j1 - jt);
+        if (active) {
+            for (int k = 0; k < nj; ++k) {
+                if (jt + k == gi) continue;
+                double dx = rx - sx[k];                    // SpeedUp:213-215
+                double dy = ry - sy[k];
+                double dz = rz - sz[k];
+                dx -= L * round(dx / L);                   // minimum image :218-220
+                dy -= L * round(dy / L);
+                dz -= L * round(dz / L);
+                const double dr = sqrt(dx * dx + dy * dy + dz * dz);   // :221
+                if (dr > 0 && dr < Rcut) {                 // :222
+                    if (MODE == 0) {
+                        const double ftotal = (1. / dr + 1. / lDeb) * exp(-dr / lDeb) / (dr * dr); // :224
+                        fx += dx * ftotal;                 // :225-230 (i's view)
+                        fy += dy * ftotal;
+                        fz += dz * ftotal;
+                    } else {
+                        fx += exp(-dr / lDeb) / (dr);      // :265
+                    }
+                }
+            }
+        }
+    }
+    if (active) {
+        double* o = a.Fpart + (size_t)seg * 3 * a.S;
+        o[li] = fx;
+        if (MODE == 0) { o[a.S + li] = fy; o[2 * a.S + li] = fz; }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_reduce_segments(const double* __restrict__ Fpart,
+                                                         double* __restrict__ F, int nseg,
+                                                         int nrows, int S, int ncomp) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= nrows || c >= ncomp) return;
+    double acc = Fpart[(size_t)c * S + i];
+    for (int s = 1; s < nseg; ++s) acc += Fpart[((size_t)s * 3 + c) * S + i];
+    F[(size_t)c * S + i] = acc;
+}
+
+static int seg_blocks(int nrows) { return (nrows + FT - 1) / FT; }
+
+hipError_t launch_forces(const ForceArgs& a, hipStream_t s) {
+    if (a.nrows <= 0) return hipSuccess;
+    dim3 grid(seg_blocks(a.nrows), a.nseg);
+    hipLaunchKernelGGL(k_pairs<0>, grid, dim3(FT), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s) {
+    if (a.nrows <= 0) return hipSuccess;
+    dim3 grid(seg_blocks(a.nrows), a.nseg);
+    hipLaunchKernelGGL(k_pairs<1>, grid, dim3(FT), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
+                                  hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    if (ncomp < 1 || ncomp > 3) return hipErrorInvalidValue;
+    dim3 grid((nrows + 255) / 256, ncomp);
+    hipLaunchKernelGGL(k_reduce_segments, grid, dim3(256), 0, s, Fpart, F, nseg, nrows, S, ncomp);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. SC'11): the counter-based stream keyed by (seed, job) with
+// counter (global ion, qstep index, draw pair); layout in DESIGN.md §RNG (the parity tests
+// check it against the CPU restatement's stream).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1, uint32_t o[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    o[0] = c0; o[1] = c1; o[2] = c2; o[3] = c3;
+}
+
+__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
+    const uint64_t b = ((((uint64_t)hi) << 32) | lo) >> 11;
+    return (double)b * 0x1.0p-53;
+}
+
+// draws 2p and 2p+1 of (ion, q)
+__device__ __forceinline__ void philox_pair(const QTConst& qc, uint64_t ion, uint64_t q, int p,
+                                            double& ua, double& ub) {
+    uint32_t o[4];
+    philox4x32_10((uint32_t)ion, (uint32_t)q, (uint32_t)(q >> 32),
+                  ((uint32_t)(ion >> 32) << 8) | (uint32_t)p, qc.seed, qc.job, o);
+    ua = u53(o[0], o[1]);
+    ub = u53(o[2], o[3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 2: fused integrator + quantum-trajectory substeps, one thread per ion, the whole
+// state (R, V, F, psi, tPart) held in registers across the nsub substeps of one launch
+// (legal: between forces() calls no ion reads another ion).
+// ------------------------------------------------------------------------------------------
+struct cxd { double re, im; };
+
+__device__ __forceinline__ cxd cmul(cxd a, cxd b) {   // std::complex<double> operator*
+    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__device__ __forceinline__ cxd cadd(cxd a, cxd b) { return {a.re + b.re, a.im + b.im}; }
+
+// Re(h * y^H D y) with D = decayMatrix (diagonal, P levels only): SpeedUp:484-485, :530-531
+__device__ __forceinline__ double dp_of(const QTConst& qc, const cxd* y) {
+    double v = (y[2].re * qc.dP[0]) * y[2].re + (y[2].im * qc.dP[0]) * y[2].im;
+    v = v + ((y[3].re * qc.dP[1]) * y[3].re + (y[3].im * qc.dP[1]) * y[3].im);
+    v = v + ((y[4].re * qc.dP[2]) * y[4].re + (y[4].im * qc.dP[2]) * y[4].im);
+    v = v + ((y[5].re * qc.dP[3]) * y[5].re + (y[5].im * qc.dP[3]) * y[5].im);
+    return qc.h * v;
+}
+
+#define MS(i) cxd{qc.Mre[i], qc.Mim[i]}
+
+// out = M y, M sparse (App. A); terms summed in ascending column order as the dense
+// Armadillo product (exact zero terms dropped: they cannot change a non-zero sum).
+__device__ __forceinline__ void matvec(const QTConst& qc, const cxd* Md, const cxd& M49,
+                                       const cxd& M58, const cxd& M85, const cxd& M94,
+                                       const cxd* y, cxd* o) {
+    o[0] = cadd(cadd(cmul(Md[0], y[0]), cmul(MS(0), y[3])), cmul(MS(1), y[5]));
+    o[1] = cadd(cadd(cmul(Md[1], y[1]), cmul(MS(2), y[2])), cmul(MS(3), y[4]));
+    o[2] = cadd(cadd(cadd(cmul(MS(4), y[1]), cmul(Md[2], y[2])), cmul(MS(5), y[9])), cmul(MS(6), y[11]));
+    o[3] = cadd(cadd(cadd(cmul(MS(7), y[0]), cmul(Md[3], y[3])), cmul(MS(8), y[8])), cmul(MS(9), y[10]));
+    o[4] = cadd(cadd(cadd(cmul(MS(10), y[1]), cmul(Md[4], y[4])), cmul(MS(11), y[7])), cmul(M49, y[9]));
+    o[5] = cadd(cadd(cadd(cmul(MS(12), y[0]), cmul(Md[5], y[5])), cmul(MS(13), y[6])), cmul(M58, y[8]));
+    o[6] = cadd(cmul(MS(14), y[5]), cmul(Md[6], y[6]));
+    o[7] = cadd(cmul(MS(15), y[4]), cmul(Md[7], y[7]));
+    o[8] = cadd(cadd(cmul(MS(16), y[3]), cmul(M85, y[5])), cmul(Md[8], y[8]));
+    o[9] = cadd(cadd(cmul(MS(17), y[2]), cmul(M94, y[4])), cmul(Md[9], y[9]));
+    o[10] = cadd(cmul(MS(18), y[3]), cmul(Md[10], y[10]));
+    o[11] = cadd(cmul(MS(19), y[2]), cmul(Md[11], y[11]));
+}
+
+__device__ __forceinline__ double rho_im(cxd a, cxd b) {   // Im(a * conj(b)), SpeedUp:490-502
+    return a.re * (-b.im) + a.im * b.re;
+}
+
+// One ion through qstep() (SpeedUp:478-712).  Returns the velocity kick.
+__device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double vx,
+                                            double& tPart, cxd* w, uint64_t gid, uint64_t q) {
+    const double velQuant = vx * qc.pv2q;                                  // :481-482
+    tPart += qc.dtQ;                                                        // :483
+    const double dp = dp_of(qc, w);                                         // :484-485
+    double u1, u2;
+    philox_pair(qc, gid, q, 0, u1, u2);                                     // :486
+    double kick;
+    if (u1 > dp) {                                                          // :487
+        const double p23 = rho_im(w[1], w[2]), p14 = rho_im(w[0], w[3]);
+        const double p25 = rho_im(w[1], w[4]), p16 = rho_im(w[0], w[5]);
+        const double p96 = rho_im(w[8], w[5]), p105 = rho_im(w[9], w[4]);
+        const double p114 = rho_im(w[10], w[3]), p123 = rho_im(w[11], w[2]);
+        const double p76 = rho_im(w[6], w[5]), p85 = rho_im(w[7], w[4]);
+        const double p94 = rho_im(w[8], w[3]), p103 = rho_im(w[9], w[2]);
+        const double* gs = qc.gs;
+        kick = qc.kickS * (p23 * gs[0] + p14 * gs[2] - p25 * gs[4] - p16 * gs[5]) * qc.dtQ * qc.gamToE +
+               qc.kickD * (p96 * gs[8] + p105 * gs[11] + p114 * gs[14] + p123 * gs[17] - p76 * gs[6] -
+                           p85 * gs[9] - p94 * gs[12] - p103 * gs[15]) * qc.dtQ * qc.gamToE;   // :503
+        // Hamiltonian (:506-521) -> M = I - i h H (:525-526)
+        const double vq = velQuant + eD;
+        const double ER = -qc.det - velQuant - eD;                          // :506
+        const double EL = -qc.det + velQuant + eD;                          // :507
+        const double E67 = (-qc.det + qc.detDP + (1 - qc.kRat) * (velQuant + eD));
+        const double E1011 = (-qc.det + qc.detDP + (qc.kRat - 1) * (velQuant + eD));
+        const double E89 = (-qc.det + qc.detDP - velQuant - eD - qc.kRat * (velQuant + eD));
+        const double phi = 2. * vq * (1 + qc.kRat) * tPart * qc.gamToE;   // :508
+        double sn, cs;
+        sincos(phi, &sn, &cs);
+        const double h = qc.h;
+        cxd Md[NS];
+        Md[0] = {1., -(h * 0.)};
+        Md[1] = Md[0];
+        Md[2] = {1. + h * qc.hdP[0], -(h * ER)};
+        Md[3] = {1. + h * qc.hdP[1], -(h * ER)};
+        Md[4] = {1. + h * qc.hdP[2], -(h * EL)};
+        Md[5] = {1. + h * qc.hdP[3], -(h * EL)};
+        Md[6] = {1., -(h * E67)};
+        Md[7] = Md[6];
+        Md[8] = {1., -(h * E89)};
+        Md[9] = Md[8];
+        Md[10] = {1., -(h * E1011)};
+        Md[11] = Md[10];
+        const double a8s = qc.a8 * sn, a8c = qc.a8 * cs, a11s = qc.a11 * sn, a11c = qc.a11 * cs;
+        const cxd M85 = {-(h * a8s), h * a8c};
+        const cxd M58 = {h * a8s, h * a8c};
+        const cxd M94 = {-(h * a11s), h * a11c};
+        const cxd M49 = {h * a11s, h * a11c};
+        // k1..k4 (:530-567): k(y) = (M y / sqrt(1 - dp(y)) - y) / h
+        cxd y[NS], ws[NS], acc[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) y[k] = w[k];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const double pref = 1 / sqrt(1 - (st == 0 ? dp : dp_of(qc, y)));
+            matvec(qc, Md, M49, M58, M85, M94, y, ws);
+            const double step = (st == 2) ? h : qc.dtHalf;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                const cxd kk = {qc.invh * (pref * ws[k].re - y[k].re), qc.invh * (pref * ws[k].im - y[k].im)};
+                if (st == 0) {
+                    acc[k] = kk;
+                } else if (st < 3) {
+                    acc[k] = {acc[k].re + 3. * kk.re, acc[k].im + 3. * kk.im};
+                } else {
+                    const cxd sum = {acc[k].re + kk.re, acc[k].im + kk.im};
+                    w[k] = {w[k].re + h * (sum.re / 8), w[k].im + h * (sum.im / 8)};
+                }
+                if (st < 3) y[k] = {w[k].re + step * kk.re, w[k].im + step * kk.im};
+            }
+        }
+    } else {                                                                // :573-703
+        tPart = 0;
+        const double rand2 = u2;
+        const double n3 = w[2].re * w[2].re + w[2].im * w[2].im;
+        const double n4 = w[3].re * w[3].re + w[3].im * w[3].im;
+        const double n5 = w[4].re * w[4].re + w[4].im * w[4].im;
+        const double n6 = w[5].re * w[5].re + w[5].im * w[5].im;
+        const double tot = n3 + n4 + n5 + n6;
+        const double prob3 = n3 / tot, prob4 = n4 / tot, prob5 = n5 / tot;
+        double randDOrS, randDir, rand3, dummy;
+        philox_pair(qc, gid, q, 1, randDOrS, randDir);
+        philox_pair(qc, gid, q, 2, rand3, dummy);
+        (void)dummy;
+        const bool sDecay = !(randDOrS < qc.pD);
+        if (!sDecay) kick = (randDir < 0.5) ? qc.vKickDP : -qc.vKickDP;
+        else kick = (randDir < 0.5) ? qc.vKick : -qc.vKick;
+        int target;
+        if (rand2 < prob3) {
+            if (sDecay) target = 1;
+            else target = (rand3 < qc.thD[0][0]) ? 11 : (rand3 < qc.thD[0][1]) ? 10 : 9;
+        } else if (rand2 < prob3 + prob4) {
+            if (sDecay) target = (rand3 < qc.thS3) ? 0 : 1;
+            else target = (rand3 < qc.thD[1][0]) ? 10 : (rand3 < qc.thD[1][1]) ? 9 : 8;
+        } else if (rand2 < prob3 + prob4 + prob5) {
+            if (sDecay) target = (rand3 < qc.thS4) ? 1 : 0;
+            else target = (rand3 < qc.thD[2][0]) ? 9 : (rand3 < qc.thD[2][1]) ? 8 : 7;
+        } else {
+            if (sDecay) target = 0;
+            else target = (rand3 < qc.thD[3][0]) ? 8 : (rand3 < qc.thD[3][1]) ? 7 : 6;
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k) w[k] = {k == target ? 1. : 0., 0.};
+    }
+    if (qc.renorm) {                                                        // :706-712
+        double popS = (w[0].re * w[0].re + w[0].im * w[0].im) + (w[1].re * w[1].re + w[1].im * w[1].im);
+        double popP = 0., popD = 0.;
+#pragma unroll
+        for (int k = 2; k < 6; ++k) popP = popP + (w[k].re * w[k].re + w[k].im * w[k].im);
+#pragma unroll
+        for (int k = 6; k < 12; ++k) popD = popD + (w[k].re * w[k].re + w[k].im * w[k].im);
+        const double nrm = sqrt(popS + popP + popD);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) w[k] = {w[k].re / nrm, w[k].im / nrm};
+    }
+    return kick;
+}
+
+__global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const int S = a.S;
+    double x = a.R[i], y = a.R[S + i], z = a.R[2 * S + i];
+    double vx = a.V[i], vy = a.V[S + i], vz = a.V[2 * S + i];
+    const double fx = a.F[i], fy = a.F[S + i], fz = a.F[2 * S + i];
+    double tPart = a.tPart[i];
+    cxd w[NS];
+    if (a.do_qt) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) w[k] = {a.psi[(size_t)(2 * k) * S + i], a.psi[(size_t)(2 * k + 1) * S + i]};
+    }
+    const double L = a.L;
+    const double dt = a.qc.dtQ;
+    const double DT = 0.5 * dt;                                  // step(): step_R(0.5*dt) :426
+    const uint64_t gid = a.gid0 + (uint64_t)i;
+    for (int s = 0; s < a.nsub; ++s) {
+        if (a.do_step) {
+            const bool moving = a.t[s] > 0;                      // step_R :360
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                if (moving) {                                    // :362-367
+                    x += DT * vx; y += DT * vy; z += DT * vz;
+                } else {                                         // :372-378
+                    x += DT * vx + DT * DT * fx;
+                    y += DT * vy + DT * DT * fy;
+                    z += DT * vz + DT * DT * fz;
+                }
+                if (x < 0) x += L;                               // :381-389
+                if (x > L) x -= L;
+                if (y < 0) y += L;
+                if (y > L) y -= L;
+                if (z < 0) z += L;
+                if (z > L) z -= L;
+                if (half == 0) {                                 // step_V(dt) :398-409
+                    vx += dt * fx; vy += dt * fy; vz += dt * fz;
+                }
+            }
+        }
+        if (a.do_qt) {
+            const double kick = qstep_ion(a.qc, a.expDet[s], vx, tPart, w, gid, a.q0 + (uint64_t)s);
+            vx = vx + kick;                                      // :705
+        }
+    }
+    a.R[i] = x; a.R[S + i] = y; a.R[2 * S + i] = z;
+    a.V[i] = vx; a.V[S + i] = vy; a.V[2 * S + i] = vz;
+    if (a.do_qt) {
+        a.tPart[i] = tPart;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            a.psi[(size_t)(2 * k) * S + i] = w[k].re;
+            a.psi[(size_t)(2 * k + 1) * S + i] = w[k].im;
+        }
+    }
+}
+
+hipError_t launch_substeps(const SubstepArgs& a, hipStream_t s) {
+    if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_substeps, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Observables (output(), SpeedUp:917-1032).  Deterministic fixed-shape reductions.
+// ------------------------------------------------------------------------------------------
+constexpr int RT = 1024;
+
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int w = RT / 2; w > 0; w >>= 1) {
+        if (t < w) sh[t] = sh[t] + sh[t + w];
+        __syncthreads();
+    }
+    const double r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(RT) void k_sum_vx(const double* __restrict__ V, int n, double* out) {
+    __shared__ double sh[RT];
+    double acc = 0.;
+    for (int i = threadIdx.x; i < n; i += RT) acc += V[i];
+    const double r = block_sum(acc, sh);
+    if (threadIdx.x == 0) out[0] = r;
+}
+
+__global__ __launch_bounds__(RT) void k_energy_sums(const double* __restrict__ V, int n, int S,
+                                                    const double* __restrict__ vxAvg,
+                                                    const double* __restrict__ urow, double* out) {
+    __shared__ double sh[RT];
+    const double avg = vxAvg[0];
+    double ex = 0., ey = 0., ez = 0., u = 0.;
+    for (int i = threadIdx.x; i < n; i += RT) {
+        const double vx = V[i], vy = V[S + i], vz = V[2 * S + i];
+        ex += 0.5 * ((vx - avg) * (vx - avg));                  // :939-944
+        ey += 0.5 * (vy * vy);
+        ez += 0.5 * (vz * vz);
+        if (urow) u += urow[i];
+    }
+    const double rx = block_sum(ex, sh);
+    const double ry = block_sum(ey, sh);
+    const double rz = block_sum(ez, sh);
+    const double ru = block_sum(u, sh);
+    if (threadIdx.x == 0) { out[0] = rx; out[1] = ry; out[2] = rz; out[3] = ru; }
+}
+
+hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_vx, dim3(1), dim3(RT), 0, s, V, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_energy_sums(const double* V, int n, int S, const double* vxAvg,
+                              const double* urow, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_energy_sums, dim3(1), dim3(RT), 0, s, V, n, S, vxAvg, urow, out);
+    return hipGetLastError();
+}
+
+// Gaussian KDE of the velocity distributions (:957-979): bin j of axis c sums, over the
+// ions of chunk z in ascending order, exp(-V2 (b_j - v)^2) + exp(-V2 (b_j + v)^2).
+constexpr int KT = 256;
+__global__ __launch_bounds__(KT) void k_kde(const double* __restrict__ V, int n, int S,
+                                            const double* __restrict__ vxAvg, double* Ppart,
+                                            int chunk) {
+    __shared__ double sv[KT];
+    const int j = blockIdx.x * KT + threadIdx.x;
+    const int c = blockIdx.y;
+    const int z = blockIdx.z;
+    const double V2 = 1. / (2. * 0.002 * 0.002);
+    const double b = (double)j * 0.0025;                         // vel[j], :340-344
+    const double avg = (c == 0) ? vxAvg[0] : 0.;
+    const int i0 = z * chunk, i1 = min(n, i0 + chunk);
+    double acc = 0.;
+    for (int it = i0; it < i1; it += KT) {
+        __syncthreads();
+        if (it + (int)threadIdx.x < i1) {
+            const double v = V[(size_t)c * S + it + threadIdx.x];
+            sv[threadIdx.x] = (c == 0) ? (v - avg) : v;
+        }
+        __syncthreads();
+        const int m = min(KT, i1 - it);
+        for (int k = 0; k < m; ++k) {
+            const double v = sv[k];
+            acc += exp(-V2 * (b - v) * (b - v)) + exp(-V2 * (b + v) * (b + v));
+        }
+    }
+    if (j < NBINS) Ppart[((size_t)z * 3 + c) * NBINS + j] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_kde_reduce(const double* __restrict__ Ppart, int nchunk,
+                                                    double* __restrict__ Pout) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= 3 * NBINS) return;
+    double acc = Ppart[j];
+    for (int z = 1; z < nchunk; ++z) acc += Ppart[(size_t)z * 3 * NBINS + j];
+    Pout[j] = acc;
+}
+
+hipError_t launch_kde(const double* V, int n, int S, const double* vxAvg, double* Ppart,
+                      int nchunk, double* Pout, hipStream_t s) {
+    const int chunk = (n + nchunk - 1) / nchunk;
+    dim3 grid((NBINS + KT - 1) / KT, 3, nchunk);
+    hipLaunchKernelGGL(k_kde, grid, dim3(KT), 0, s, V, n, S, vxAvg, Ppart, chunk);
+    hipLaunchKernelGGL(k_kde_reduce, dim3((3 * NBINS + 255) / 256), dim3(256), 0, s, Ppart, nchunk, Pout);
+    return hipGetLastError();
+}
+
+}  // namespace mdqt

@@ -1,0 +1,246 @@
+"""Python host API of the MI355X MDQT engine — a thin mirror of the reference's function seam.
+
+The reference program (laserCoolingPlusExpansionMDQTSpeedUp.cpp, "SpeedUp") exposes no library:
+its hot path is a set of ``void f(void)`` functions over globals (SpeedUp:176-185).  This class keeps
+those names and their meaning, over one device-resident simulation held by libmdqt.so:
+
+    ===========================  ==================================  ==========================
+    reference (SpeedUp)          here                                C ABI (include/mdqt.h)
+    ===========================  ==================================  ==========================
+    init()            :289-348   Simulation.init()                   mdqt_init
+    forces()          :192-236   Simulation.forces()                 mdqt_forces
+    step()            :418-430   Simulation.step()                   mdqt_step
+    qstep()           :438-717   Simulation.qstep()                  mdqt_qstep
+    step();qstep() x n           Simulation.substeps(n)              mdqt_substeps (fused)
+    Epotential()      :244-281   Simulation.Epotential()             mdqt_epotential
+    output()          :917-1032  Simulation.output()                 mdqt_output
+    writeConditions() :725-784   Simulation.writeConditions(c0)      mdqt_write_conditions
+    readConditions()  :785-916   Simulation.readConditions(c0)       mdqt_read_conditions
+    main()            :1139-1383 Simulation.run()                    mdqt_run
+    ===========================  ==================================  ==========================
+
+Parameters keep the reference's names and defaults (SpeedUp:56-85).  Errors raise MdqtError
+(the reference has no error reporting at all: unchecked fopen, void returns).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import MdqtError, MdqtParams, check, dptr, lib
+
+NBINS = 2001
+NUM_STATES = 12
+
+# reference parameter names (SpeedUp:56-85) plus the engine's extensions
+PARAM_NAMES = [f[0] for f in MdqtParams._fields_]
+
+
+def default_params(**kw) -> MdqtParams:
+    p = MdqtParams()
+    lib().mdqt_default_params(C.byref(p))
+    for k, v in kw.items():
+        if k not in PARAM_NAMES:
+            raise KeyError(f"unknown parameter {k!r}")
+        if k == "saveDirectory":
+            p.saveDirectory = v.encode() if isinstance(v, str) else v
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def device_count() -> int:
+    return lib().mdqt_device_count()
+
+
+def slab(N: int, world: int, rank: int):
+    """(lo, hi, S): ions [lo, hi) owned by `rank`, slab stride S (pure function of N, world)."""
+    lo, hi, S = C.c_int(), C.c_int(), C.c_int()
+    check(lib().mdqt_slab(N, world, rank, C.byref(lo), C.byref(hi), C.byref(S)), "mdqt_slab")
+    return lo.value, hi.value, S.value
+
+
+def forces_raw(R, L: float, lDeb: float, nseg: int = 0, device: int = -1):
+    """Yukawa forces of positions R[3][N] in a periodic box L (kernel 1, stateless)."""
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    N = R.shape[1]
+    F = np.zeros((3, N))
+    check(lib().mdqt_forces_raw(N, float(L), float(lDeb), dptr(R), N, dptr(F), int(nseg), int(device)),
+          "forces_raw")
+    return F
+
+
+def potentials_raw(R, L: float, lDeb: float, nseg: int = 0, device: int = -1):
+    """U[i] = sum_{j != i} exp(-r/lDeb)/r inside L/2 (kernel 1 potential mode, stateless)."""
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    N = R.shape[1]
+    U = np.zeros(N)
+    check(lib().mdqt_potentials_raw(N, float(L), float(lDeb), dptr(R), N, dptr(U), int(nseg), int(device)),
+          "potentials_raw")
+    return U
+
+
+class Simulation:
+    """One MDQT system (or one rank's slab of it) resident on one MI355X."""
+
+    def __init__(self, **params):
+        self.params = default_params(**params)
+        h = C.c_void_p()
+        check(lib().mdqt_create(C.byref(self.params), C.byref(h)), "mdqt_create")
+        self.h = h
+
+    # ---- lifecycle ----
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mdqt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- constants / counters ----
+    def const(self, name: str) -> float:
+        return lib().mdqt_get_const(self.h, name.encode())
+
+    @property
+    def N(self) -> int:
+        return lib().mdqt_get_N(self.h)
+
+    @property
+    def t(self) -> float:
+        return lib().mdqt_get_time(self.h)
+
+    @t.setter
+    def t(self, v: float):
+        check(lib().mdqt_set_time(self.h, float(v)))
+
+    @property
+    def qstep_index(self) -> int:
+        return lib().mdqt_get_qstep_index(self.h)
+
+    @qstep_index.setter
+    def qstep_index(self, q: int):
+        check(lib().mdqt_set_qstep_index(self.h, int(q)))
+
+    def counters(self):
+        c0 = C.c_int(); cnt = C.c_uint(); e = C.c_double(); e0 = C.c_double()
+        check(lib().mdqt_get_counters(self.h, C.byref(c0), C.byref(cnt), C.byref(e), C.byref(e0)))
+        return dict(c0=c0.value, counter=cnt.value, Epot=e.value, Epot0=e0.value)
+
+    # ---- state (host numpy <-> HBM) ----
+    def init(self):
+        check(lib().mdqt_init(self.h), "init")
+        return self
+
+    def set_state(self, R, V, psi, tPart, t):
+        R = np.ascontiguousarray(R, dtype=np.float64)
+        N = R.shape[1]
+        V = np.ascontiguousarray(V, dtype=np.float64)
+        psi = np.ascontiguousarray(psi, dtype=np.float64).reshape(N, NUM_STATES, 2)
+        tPart = np.ascontiguousarray(tPart, dtype=np.float64)
+        check(lib().mdqt_set_state(self.h, N, dptr(R), dptr(V), N, dptr(psi), dptr(tPart), float(t)),
+              "set_state")
+
+    def set_forces(self, F):
+        F = np.ascontiguousarray(F, dtype=np.float64)
+        check(lib().mdqt_set_forces(self.h, dptr(F), F.shape[1]), "set_forces")
+
+    def get_state(self):
+        N = self.N
+        R = np.zeros((3, N)); V = np.zeros((3, N)); F = np.zeros((3, N))
+        psi = np.zeros((N, NUM_STATES, 2)); tp = np.zeros(N); t = C.c_double()
+        check(lib().mdqt_get_state(self.h, dptr(R), dptr(V), dptr(F), N, dptr(psi), dptr(tp),
+                                   C.byref(t)), "get_state")
+        return dict(R=R, V=V, F=F, psi=psi, tPart=tp, t=t.value)
+
+    # ---- the reference's function seam ----
+    def forces(self):
+        check(lib().mdqt_forces(self.h), "forces")
+
+    def step(self):
+        check(lib().mdqt_step(self.h), "step")
+
+    def qstep(self):
+        check(lib().mdqt_qstep(self.h), "qstep")
+
+    def substeps(self, n: int):
+        check(lib().mdqt_substeps(self.h, int(n)), "substeps")
+
+    def md_steps(self, n: int):
+        check(lib().mdqt_md_steps(self.h, int(n)), "md_steps")
+
+    def Epotential(self) -> float:
+        e = C.c_double()
+        check(lib().mdqt_epotential(self.h, C.byref(e)), "Epotential")
+        return e.value
+
+    epotential = Epotential
+
+    def observables(self, kde: bool = True, pops: bool = True):
+        o = np.zeros(7)
+        P = np.zeros((3, NBINS)) if kde else None
+        pp = np.zeros((self.N, 3)) if pops else None
+        check(lib().mdqt_observables(self.h, dptr(o), dptr(P), dptr(pp)), "observables")
+        return o, P, pp
+
+    def partial_observables(self, vxAvg: float):
+        o = np.zeros(5)
+        P = np.zeros((3, NBINS))
+        check(lib().mdqt_partial_observables(self.h, float(vxAvg), dptr(o), dptr(P)), "partial_observables")
+        return o, P
+
+    def setup_directories(self):
+        check(lib().mdqt_setup_directories(self.h), "setup_directories")
+
+    @property
+    def save_directory(self) -> str:
+        return lib().mdqt_save_directory(self.h).decode()
+
+    def output(self):
+        check(lib().mdqt_output(self.h), "output")
+
+    def writeConditions(self, c0: int):
+        check(lib().mdqt_write_conditions(self.h, int(c0)), "writeConditions")
+
+    def readConditions(self, c0: int):
+        check(lib().mdqt_read_conditions(self.h, int(c0)), "readConditions")
+
+    write_conditions = writeConditions
+    read_conditions = readConditions
+
+    def run(self):
+        check(lib().mdqt_run(self.h), "run")
+
+    # ---- streams / timing / sharding plumbing ----
+    def set_stream(self, stream_handle: int | None):
+        check(lib().mdqt_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None))
+
+    def synchronize(self):
+        check(lib().mdqt_synchronize(self.h), "synchronize")
+
+    def positions_device(self):
+        p = C.c_void_p(); S = C.c_int()
+        check(lib().mdqt_positions_device(self.h, C.byref(p), C.byref(S)))
+        return p.value, S.value
+
+    def enable_timing(self, on: bool = True):
+        check(lib().mdqt_enable_timing(self.h, int(on)))
+
+    def kernel_time_totals(self):
+        """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""
+        a = C.c_double(); b = C.c_double(); na = C.c_int(); nb = C.c_int()
+        check(lib().mdqt_kernel_time_totals(self.h, C.byref(a), C.byref(na), C.byref(b), C.byref(nb)))
+        return a.value, na.value, b.value, nb.value
+
+
+__all__ = ["forces_raw", "potentials_raw", "Simulation", "MdqtError", "default_params", "device_count", "slab", "NBINS", "NUM_STATES"]

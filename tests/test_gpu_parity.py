@@ -1,0 +1,299 @@
+"""GPU parity of the HIP path (through the C ABI) against the oracle and the reference goldens.
+
+Tolerances (written per test) follow BASELINE.md's parity gates:
+  forces <= 1e-13 relative (max-norm), single qstep <= 1e-12, short-horizon energies and velocity
+  distributions <= 1e-6 relative.  Pure +,*,/ arithmetic (integrator, init) is compared bit for bit;
+  libm differences (exp/sin/cos: ROCm ocml vs glibc, <= 1 ulp) are what the tolerances absorb.
+The device path runs the Philox stream (rng_mode=1); the oracle is run in the same mode.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "ref_md_n4096.npz")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import mdqtplasmasims_amd as M
+    if M.device_count() < 1:
+        pytest.fail("no GPU visible to the gpu-marked tests")
+    return M
+
+
+def rel(a, b):
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+# ---------------------------------------------------------------------------------------------
+# kernel 1 vs the reference's own compiled force / potential (golden vectors)
+# ---------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("case", [0, 1])
+@pytest.mark.parametrize("nseg", [1, 0, 7])
+def test_forces_match_reference_golden(eng, case, nseg):
+    from mdqtplasmasims_amd.engine import forces_raw
+    g = np.load(GOLD)
+    L, kappa = float(g["L"]), float(g["kappa"])
+    F = forces_raw(g[f"R{case}"], L, 1.0 / kappa, nseg=nseg)
+    A = g[f"A{case}"]
+    assert rel(F, A) < 1e-13
+    assert np.allclose(F, A, rtol=1e-11, atol=1e-12 * np.abs(A).max())
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_potentials_match_reference_golden(eng, case):
+    from mdqtplasmasims_amd.engine import potentials_raw
+    g = np.load(GOLD)
+    U = potentials_raw(g[f"R{case}"], float(g["L"]), 1.0 / float(g["kappa"]))
+    assert rel(U, g[f"U{case}"]) < 1e-13
+
+
+def test_forces_match_oracle_bitwise_order(eng, orc):
+    """one j-segment = the reference's ascending-j order: only exp ulps may differ"""
+    from mdqtplasmasims_amd.engine import forces_raw
+    rng = np.random.default_rng(4)
+    L = 12.794389
+    R = rng.uniform(0, L, (3, 777))
+    F = forces_raw(R, L, 1.8257418583505538, nseg=1)
+    O = orc.forces_raw(R, L, 1.8257418583505538)
+    assert rel(F, O) < 1e-14
+
+
+# ---------------------------------------------------------------------------------------------
+# simulation state: init, step, qstep, md steps vs the oracle
+# ---------------------------------------------------------------------------------------------
+
+def pair(eng, orc, **kw):
+    kw.setdefault("rng_mode", 1)
+    s = eng.Simulation(**kw).init()
+    o = orc.OracleSim(**kw).init()
+    return s, o
+
+
+@pytest.mark.parametrize("N0", [60, 500, 3500])
+def test_init_matches_oracle_bitwise(eng, orc, N0):
+    s, o = pair(eng, orc, N0=N0, seed=12346)
+    assert s.N == o.N
+    a, b = s.get_state(), o.get_state()
+    for k in ("R", "V", "psi", "tPart"):
+        assert np.array_equal(a[k], b[k]), k
+    if N0 == 3500:
+        assert s.N == 3573
+    ca, cb = s.counters(), o.counters()
+    assert ca["c0"] == cb["c0"] == -1
+    assert abs(ca["Epot0"] - cb["Epot0"]) <= 1e-12 * abs(cb["Epot0"])
+
+
+def test_forces_match_oracle_after_init(eng, orc):
+    s, o = pair(eng, orc, N0=3500, seed=12346)
+    s.forces(); o.forces()
+    assert rel(s.get_state()["F"], o.get_state()["F"]) < 1e-13
+
+
+@pytest.mark.parametrize("t0", [0.0, 0.5])
+def test_step_matches_oracle_bitwise(eng, orc, t0):
+    """step() = step_R(dt/2); step_V(dt); step_R(dt/2) incl. the t==0 branch and the wrap"""
+    s, o = pair(eng, orc, N0=500, seed=3)
+    rng = np.random.default_rng(9)
+    st = o.get_state()
+    V = rng.normal(0, 40.0, st["V"].shape)          # large velocities: many wraps
+    F = rng.normal(0, 50.0, st["V"].shape)
+    for x in (s, o):
+        x.set_state(st["R"], V, st["psi"], st["tPart"], t0)
+        x.set_forces(F)
+        x.step()
+    a, b = s.get_state(), o.get_state()
+    assert np.array_equal(a["R"], b["R"])
+    assert np.array_equal(a["V"], b["V"])
+    assert a["t"] == b["t"] == t0
+
+
+def _evolved_state(orc, N0=300, seed=21, nmd=4):
+    o = orc.OracleSim(N0=N0, seed=seed, rng_mode=1, nthreads=4).init()
+    o.md_steps(nmd)
+    return o
+
+
+def test_qstep_matches_oracle(eng, orc):
+    o = _evolved_state(orc)
+    st = o.get_state()
+    s = eng.Simulation(N0=300, seed=21, rng_mode=1)
+    s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+    s.set_forces(st["F"])
+    s.qstep_index = o.qstep_index
+    s.qstep(); o.qstep()
+    a, b = s.get_state(), o.get_state()
+    assert np.abs(a["psi"] - b["psi"]).max() < 1e-12
+    assert np.abs(a["V"] - b["V"]).max() < 1e-15
+    assert np.array_equal(a["tPart"], b["tPart"])
+    assert a["t"] == b["t"] and s.qstep_index == o.qstep_index
+
+
+def test_qstep_jump_branch_exercised(eng, orc):
+    """ions with large P population jump with probability ~dp: force many jumps and compare"""
+    o = _evolved_state(orc, nmd=1)
+    st = o.get_state()
+    psi = np.zeros_like(st["psi"])
+    rng = np.random.default_rng(1)
+    z = rng.normal(size=(psi.shape[0], 12)) + 1j * rng.normal(size=(psi.shape[0], 12))
+    z /= np.linalg.norm(z, axis=1, keepdims=True)
+    psi[:, :, 0], psi[:, :, 1] = z.real, z.imag
+    s = eng.Simulation(N0=300, seed=21, rng_mode=1, Om=3.0, OmDP=2.0)
+    o2 = orc.OracleSim(N0=300, seed=21, rng_mode=1, Om=3.0, OmDP=2.0)
+    for x in (s, o2):
+        x.set_state(st["R"], st["V"], psi, st["tPart"] + 0.01, 0.3)
+        x.set_forces(st["F"])
+        x.qstep_index = 1000
+    njump = 0
+    for _ in range(40):
+        s.qstep(); o2.qstep()
+    a, b = s.get_state(), o2.get_state()
+    njump = int((b["tPart"] < 0.002).sum())
+    assert njump > 5                                   # the branch really ran
+    assert np.array_equal(a["tPart"] < 0.002, b["tPart"] < 0.002)
+    assert np.abs(a["psi"] - b["psi"]).max() < 1e-10
+    assert np.abs(a["V"] - b["V"]).max() < 1e-12
+
+
+@pytest.mark.parametrize("qt", [1, 0])
+def test_md_steps_short_horizon(eng, orc, qt):
+    kw = dict(N0=500, seed=77, rng_mode=1, qt_enabled=qt)
+    s = eng.Simulation(**kw).init()
+    o = orc.OracleSim(nthreads=8, **kw).init()
+    s.md_steps(3); o.md_steps(3)
+    a, b = s.get_state(), o.get_state()
+    assert a["t"] == b["t"]
+    assert np.abs(a["R"] - b["R"]).max() < 1e-10
+    assert np.abs(a["V"] - b["V"]).max() < 1e-10
+    if qt:
+        assert np.abs(a["psi"] - b["psi"]).max() < 1e-9
+        assert np.array_equal(a["tPart"] == 0, b["tPart"] == 0)
+
+
+def test_substeps_fusion_equals_single_substeps(eng):
+    """one fused launch of n substeps == n launches of one (bit for bit)"""
+    a = eng.Simulation(N0=400, seed=5).init()
+    b = eng.Simulation(N0=400, seed=5).init()
+    a.forces(); b.forces()
+    a.substeps(25)
+    for _ in range(25):
+        b.substeps(1)
+    sa, sb = a.get_state(), b.get_state()
+    for k in ("R", "V", "psi", "tPart"):
+        assert np.array_equal(sa[k], sb[k]), k
+    c = eng.Simulation(N0=400, seed=5).init()
+    c.forces()
+    for _ in range(25):
+        c.step(); c.qstep()
+    sc = c.get_state()
+    for k in ("R", "V", "psi", "tPart"):
+        assert np.array_equal(sa[k], sc[k]), k
+
+
+# ---------------------------------------------------------------------------------------------
+# observables and files
+# ---------------------------------------------------------------------------------------------
+
+def test_observables_match_oracle(eng, orc):
+    kw = dict(N0=500, seed=8, rng_mode=1)
+    s = eng.Simulation(**kw).init()
+    o = orc.OracleSim(nthreads=8, **kw).init()
+    s.md_steps(2); o.md_steps(2)
+    st = o.get_state()
+    s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])   # identical state
+    a7, aP, ap = s.observables()
+    b7, bP, bp = o.observables()
+    assert a7[0] == b7[0]
+    idx = [1, 2, 3, 4, 6]                          # EkinX, EkinY, EkinZ, Epot, <vx>
+    assert np.allclose(a7[idx], b7[idx], rtol=1e-12, atol=1e-15)
+    # Etot - Epot0 cancels to ~1e-7 of Epot: compare on the scale of the terms
+    assert abs(a7[5] - b7[5]) <= 1e-12 * abs(b7[4])
+    assert rel(aP, bP) < 1e-12
+    assert np.allclose(ap, bp, rtol=1e-14, atol=1e-16)
+    assert abs(s.Epotential() - o.epotential()) <= 1e-12 * abs(o.epotential())
+
+
+def _read_dir(d):
+    out = {}
+    for f in sorted(os.listdir(d)):
+        out[f] = open(os.path.join(d, f)).read()
+    return out
+
+
+def test_run_writes_reference_layout(eng, orc, tmp_path):
+    kw = dict(N0=60, tmax=0.09, sampleFreq=5, seed=99, job=3, rng_mode=1)
+    s = eng.Simulation(saveDirectory=str(tmp_path / "gpu") + "/", **kw)
+    s.run()
+    o = orc.OracleSim(saveDirectory=str(tmp_path / "cpu") + "/", **kw)
+    assert o.run() == 0
+    A, B = _read_dir(s.save_directory), _read_dir(o.save_directory)
+    assert s.save_directory.endswith(
+        "Ge10Density2000E+11Sig040Te19SigFrac0DetSP-100DetDP100OmSP100OmDP100NumIons60/job3/")
+    assert sorted(A) == sorted(B)
+    assert s.counters()["c0"] == o.counters()["c0"] and s.counters()["counter"] == o.counters()["counter"]
+    for f in A:
+        a, b = A[f], B[f]
+        if f.startswith("ions_"):
+            assert a == b
+            continue
+        la, lb = a.splitlines(), b.splitlines()
+        assert len(la) == len(lb), f
+        xa = np.array([[float(v) for v in l.split()] for l in la if l.strip()])
+        xb = np.array([[float(v) for v in l.split()] for l in lb if l.strip()])
+        assert xa.shape == xb.shape, f
+        # %lg keeps 6 significant digits: files agree to the printed precision
+        assert np.allclose(xa, xb, rtol=2e-5, atol=1e-9 * max(1.0, np.abs(xb).max())), f
+
+
+def test_resume_roundtrip(eng, tmp_path):
+    kw = dict(N0=60, tmax=0.05, sampleFreq=1000, seed=5, job=1, saveDirectory=str(tmp_path) + "/")
+    s = eng.Simulation(**kw)
+    s.run()
+    c0 = s.counters()["c0"]
+    st = s.get_state()
+    r = eng.Simulation(newRun=0, c0=c0, **{k: v for k, v in kw.items()})
+    r.setup_directories()
+    r.readConditions(c0)
+    st2 = r.get_state()
+    assert r.N == s.N
+    assert np.allclose(st2["R"], st["R"], rtol=1e-5, atol=1e-6)
+    assert np.allclose(st2["psi"], st["psi"], rtol=1e-5, atol=1e-6)
+    assert r.t == (c0 - 9.0) * 0.002 + 0.02          # SpeedUp:789
+    assert (st2["tPart"] == 0).all()
+
+
+def test_cli_runs(eng, tmp_path):
+    import subprocess
+    from mdqtplasmasims_amd import CLI_PATH
+    r = subprocess.run([CLI_PATH, "2", "--N0=80", "--tmax=0.02", "--seed=4",
+                        f"--saveDirectory={tmp_path}/"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = tmp_path / "Ge10Density2000E+11Sig040Te19SigFrac0DetSP-100DetDP100OmSP100OmDP100NumIons80" / "job2"
+    assert (d / "ions_timestep000010.dat").exists()
+
+
+# ---------------------------------------------------------------------------------------------
+# size-independent properties at the benchmark sizes
+# ---------------------------------------------------------------------------------------------
+
+def test_momentum_conservation_of_forces_c2(eng):
+    s = eng.Simulation(N0=3500, seed=12346).init()
+    s.forces()
+    F = s.get_state()["F"]
+    assert np.abs(F.sum(axis=1)).max() < 1e-10 * np.abs(F).sum() / F.shape[1]
+
+
+def test_norm_decay_and_partition_of_qt(eng):
+    """the no-jump propagator keeps |psi| ~ 1 (normalised non-Hermitian step, App. A) and
+    populations stay in [0,1] over an MD step at the C2 size"""
+    s = eng.Simulation(N0=3500, seed=12346).init()
+    s.md_steps(2)
+    st = s.get_state()
+    nrm = (st["psi"] ** 2).sum(axis=(1, 2))
+    assert np.abs(nrm - 1).max() < 1e-3
+    o7, P, pops = s.observables()
+    assert np.all(pops >= -1e-15) and np.all(pops.sum(1) < 1.001)

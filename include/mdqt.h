@@ -105,11 +105,12 @@ int         mdqt_md_steps(mdqt_ctx* c, int n);               /* n x (forces(); c
  * length), for callers whose force law is the same Yukawa pair sum but whose box is not
  * SpeedUp's — e.g. MonteCarloFollowedByMDAndTempAnisotropy.cpp calculateAccelerations
  * (:387-448, acceleration = force at unit mass) and calculatePotentialEnergyForParticles
- * (:207-244).  R, F are [3][ld]; nseg = j-split (0 = auto); U[i] = sum_{j != i} u(r_ij). */
+ * (:207-244).  R, F are [3][ld]; nseg = j-split (0 = auto); U[i] = sum_{j != i} u(r_ij);
+ * variant 0 = the reference's exact operations, 1 = fast reciprocal form (<= 1e-13 rel). */
 int         mdqt_forces_raw(int N, double L, double lDeb, const double* R, size_t ld, double* F,
-                            int nseg, int device);
+                            int nseg, int device, int variant);
 int         mdqt_potentials_raw(int N, double L, double lDeb, const double* R, size_t ld, double* U,
-                                int nseg, int device);
+                                int nseg, int device, int variant);
 
 /* ---- diagnostics / output ---- */
 int         mdqt_epotential(mdqt_ctx* c, double* Epot);      /* Epotential(), SpeedUp:244-281   */
@@ -123,15 +124,34 @@ int         mdqt_write_conditions(mdqt_ctx* c, int c0);      /* writeConditions,
 int         mdqt_read_conditions(mdqt_ctx* c, int c0);       /* readConditions,  :785-916       */
 int         mdqt_run(mdqt_ctx* c);                           /* main() time loop, :1139-1383    */
 
+/* ---- tuning knobs (results are bit-identical across every setting) ----
+ *   "substep_kernel": 0 = auto, 1 = thread per ion, 2 = 16-lane group per ion
+ *   "force_kernel":   1 = fast reciprocal form (default), 0 = the reference's exact operations
+ *                     (the two differ by a few ulp per pair; both meet the 1e-13 force gate) */
+int         mdqt_set_option(mdqt_ctx* c, const char* name, int value);
+
 /* ---- streams, timing, multi-GPU plumbing ---- */
 int         mdqt_set_stream(mdqt_ctx* c, void* hip_stream);  /* NULL = the context's own stream */
 void*       mdqt_get_stream(mdqt_ctx* c);
 int         mdqt_synchronize(mdqt_ctx* c);
 /* slab of rank r: ions [lo, hi) with slab capacity S = ceil(N / world) (pure function) */
 int         mdqt_slab(int N, int world, int rank, int* lo, int* hi, int* S);
-/* device address of the gathered position array [world][3][S] (doubles) and S; the
- * caller's collective (RCCL all-gather) fills the other ranks' slabs in place. */
+/* device address of the gathered position array [world][3][S] (doubles) and S */
 int         mdqt_positions_device(mdqt_ctx* c, void** dptr, int* S);
+int         mdqt_slab_bounds(const mdqt_ctx* c, int* lo, int* hi);
+int         mdqt_set_counters(mdqt_ctx* c, int c0, unsigned counter, double Epot, double Epot0);
+/* RCCL (one process per GPU).  Rank 0 makes the 128-byte unique id, the launcher
+ * broadcasts it (torch.distributed), every rank calls mdqt_comm_init.  With a communicator,
+ * mdqt_md_steps / mdqt_run all-gather the position slabs (in place, [world][3][S]) before
+ * every force call, and epotential / observables / output / write_conditions become
+ * collectives (sum all-reduces; rank 0 writes the files). */
+int         mdqt_comm_unique_id(void* out, size_t len);
+int         mdqt_comm_init(mdqt_ctx* c, const void* uid, size_t len);
+/* in-process group of world_size contexts (tests on one GPU): the all-gather becomes device
+ * copies; the caller steps the ranks in lockstep (all all-gathers, then all forces ...) */
+int         mdqt_comm_init_local(mdqt_ctx* const* ctxs, int n);
+int         mdqt_allgather_positions(mdqt_ctx* c);
+int         mdqt_allreduce_sum(mdqt_ctx* c, double* host_buf, size_t n);
 /* Per-rank partial sums for output() under sharding: out[0] = sum vx, [1..3] = sum of the
  * reference's EkinX/Y/Z terms about vxAvg, [4] = sum over owned i of the full-row pair
  * potential, Pvel partial [3][2001] before normalisation.  Used by the sharded driver. */

@@ -53,9 +53,10 @@ SIGNATURES = [
     ("mdqt_qstep", C.c_int, [C.c_void_p]),
     ("mdqt_substeps", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_md_steps", C.c_int, [C.c_void_p, C.c_int]),
-    ("mdqt_forces_raw", C.c_int, [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t, _dp, C.c_int, C.c_int]),
+    ("mdqt_forces_raw", C.c_int, [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t, _dp, C.c_int, C.c_int,
+                                  C.c_int]),
     ("mdqt_potentials_raw", C.c_int, [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t, _dp, C.c_int,
-                                      C.c_int]),
+                                      C.c_int, C.c_int]),
     ("mdqt_epotential", C.c_int, [C.c_void_p, _dp]),
     ("mdqt_observables", C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     ("mdqt_setup_directories", C.c_int, [C.c_void_p]),
@@ -64,6 +65,7 @@ SIGNATURES = [
     ("mdqt_write_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_read_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_run", C.c_int, [C.c_void_p]),
+    ("mdqt_set_option", C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     ("mdqt_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("mdqt_get_stream", C.c_void_p, [C.c_void_p]),
     ("mdqt_synchronize", C.c_int, [C.c_void_p]),
@@ -71,6 +73,13 @@ SIGNATURES = [
                             C.POINTER(C.c_int)]),
     ("mdqt_positions_device", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int)]),
     ("mdqt_partial_observables", C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
+    ("mdqt_slab_bounds", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("mdqt_set_counters", C.c_int, [C.c_void_p, C.c_int, C.c_uint, C.c_double, C.c_double]),
+    ("mdqt_comm_unique_id", C.c_int, [C.c_char_p, C.c_size_t]),
+    ("mdqt_comm_init", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    ("mdqt_comm_init_local", C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    ("mdqt_allgather_positions", C.c_int, [C.c_void_p]),
+    ("mdqt_allreduce_sum", C.c_int, [C.c_void_p, _dp, C.c_size_t]),
     ("mdqt_kernel_time_totals", C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int), _dp, C.POINTER(C.c_int)]),
     ("mdqt_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
 ]

@@ -14,7 +14,10 @@
 #include <sys/stat.h>
 
 #include <string>
+#include <algorithm>
 #include <vector>
+
+#include <rccl/rccl.h>
 
 #include "../../include/mdqt.h"
 #include "mdqt_internal.hpp"
@@ -78,6 +81,15 @@ struct mdqt_ctx {
     double *dR = nullptr, *dV = nullptr, *dF = nullptr, *dFpart = nullptr, *dPsi = nullptr,
            *dTp = nullptr, *dScr = nullptr, *dKde = nullptr, *dUrow = nullptr;
     int kdeChunks = 0;
+    LaneTab tab;                   // lane-per-state QT kernel tables (host copy)
+    LaneTab* dTab = nullptr;       // device copy (uploaded once at create)
+    int substep_mode = 0;          // 0 auto, 1 thread-per-ion, 2 lane-per-state
+    int force_variant = 1;         // 0 exact reference operations, 1 fast reciprocal form
+    bool f_pending = false;        // dFpart holds unreduced force partials (nseg > 1)
+    ncclComm_t comm = nullptr;     // RCCL communicator over the world_size ranks (sharded runs)
+    double* dComm = nullptr;       // device staging for small all-reduces
+    std::vector<mdqt_ctx*> local;  // in-process group (tests on one GPU): all-gather by D2D copies
+    size_t dCommCap = 0;
     // host-side state
     double t = 0.;
     uint64_t qidx = 0;
@@ -94,6 +106,8 @@ struct mdqt_ctx {
     std::vector<hipEvent_t> evpool[2];
     int evused[2] = {0, 0};
 };
+
+static int settle_forces(mdqt_ctx* s);
 
 // ---------------------------------------------------------------------------------------------
 // parameters and constants
@@ -196,6 +210,45 @@ static void build_constants(mdqt_ctx* s) {
     q.renorm = p->reNormalizewvFns;
     q.seed = p->seed; q.job = p->job;
     for (int i = 0; i < NBINS; ++i) s->vel[i] = (double)i * 0.0025;   // :340-344
+    // lane tables of the lane-per-state kernel: row k of M, slots A < B < C by column
+    LaneTab& t = s->tab;
+    memset(&t, 0, sizeof t);
+    static const int cols[NS][3] = {{3, 5, -1}, {2, 4, -1}, {1, 9, 11}, {0, 8, 10}, {1, 7, 9}, {0, 6, 8},
+                                    {5, -1, -1}, {4, -1, -1}, {3, 5, -1}, {2, 4, -1}, {3, -1, -1}, {2, -1, -1}};
+    static const int order[NS] = {0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 2, 2};
+    auto static_idx = [](int r, int c) {
+        for (int e = 0; e < NSTATIC; ++e)
+            if (kStaticRC[e][0] == r && kStaticRC[e][1] == c) return e;
+        return -1;
+    };
+    for (int k = 0; k < 16; ++k) {
+        t.colA[k] = t.colB[k] = t.colC[k] = 0;
+        t.order[k] = 2;
+    }
+    for (int k = 0; k < NS; ++k) {
+        t.order[k] = order[k];
+        int* slot[3] = {&t.colA[k], &t.colB[k], &t.colC[k]};
+        double* cre[3] = {&t.cAre[k], &t.cBre[k], &t.cCre[k]};
+        double* cim[3] = {&t.cAim[k], &t.cBim[k], &t.cCim[k]};
+        for (int j = 0; j < 3; ++j) {
+            const int c = cols[k][j];
+            if (c < 0) continue;
+            *slot[j] = c;
+            const int e = static_idx(k, c);
+            if (e >= 0) { *cre[j] = q.Mre[e]; *cim[j] = q.Mim[e]; }
+        }
+        t.hasB[k] = cols[k][1] >= 0;
+        t.hasC[k] = cols[k][2] >= 0;
+        if (k >= 2 && k < 6) { t.dP[k] = q.dP[k - 2]; t.hd[k] = q.hdP[k - 2]; }
+    }
+    t.dynC[4] = 1; t.dynScale[4] = q.a11;      // M49
+    t.dynC[5] = 1; t.dynScale[5] = q.a8;       // M58
+    t.dynB[8] = 1; t.dynScale[8] = q.a8;       // M85
+    t.dynB[9] = 1; t.dynScale[9] = q.a11;      // M94
+    // kick weights: lane k multiplies rho_im(w_k, w_colA) by gA, rho_im(w_k, w_colB) by gB (:503)
+    t.gA[1] = gs[0]; t.gA[0] = gs[2]; t.gB[1] = gs[4]; t.gB[0] = gs[5];
+    t.gB[8] = gs[8]; t.gB[9] = gs[11]; t.gA[10] = gs[14]; t.gA[11] = gs[17];
+    t.gA[6] = gs[6]; t.gA[7] = gs[9]; t.gA[8] = gs[12]; t.gA[9] = gs[15];
 }
 
 static double expDetuning_of(const mdqt_params* p, double t) {   // :447
@@ -304,7 +357,12 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
         return fail("cannot create HIP stream on device %d", p->device);
     }
     s->stream = s->own;
+    if (hipMalloc(&s->dTab, sizeof(LaneTab)) != hipSuccess) { mdqt_destroy(s); return fail("hipMalloc lane table"); }
     build_constants(s);
+    if (hipMemcpy(s->dTab, &s->tab, sizeof(LaneTab), hipMemcpyHostToDevice) != hipSuccess) {
+        mdqt_destroy(s);
+        return fail("upload of the lane table failed");
+    }
     s->t = 0.; s->qidx = 0; s->c0 = p->c0; s->counter = 0;
     s->x48 = srand48_state(p->seed);
     strncpy(s->saveDirectory, s->p.saveDirectory, sizeof(s->saveDirectory) - 1);
@@ -319,6 +377,9 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     (void)hipSetDevice(s->dev);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     free_device(s);
+    if (s->dTab) (void)hipFree(s->dTab);
+    if (s->dComm) (void)hipFree(s->dComm);
+    if (s->comm) (void)ncclCommDestroy(s->comm);
     for (auto& pool : s->evpool)
         for (hipEvent_t ev : pool) (void)hipEventDestroy(ev);
     if (s->own) (void)hipStreamDestroy(s->own);
@@ -394,6 +455,7 @@ extern "C" int mdqt_set_state(mdqt_ctx* s, int N, const double* R, const double*
 }
 
 extern "C" int mdqt_set_forces(mdqt_ctx* s, const double* F, size_t ld) {
+    s->f_pending = false;
     const int S = s->S, lo = s->lo, n = s->nloc;
     std::vector<double> h((size_t)3 * S, 0.);
     for (int c = 0; c < 3; ++c)
@@ -410,6 +472,7 @@ extern "C" int mdqt_get_state(mdqt_ctx* s, double* R, double* V, double* F, size
     const int N = s->N, S = s->S, W = s->p.world_size, lo = s->lo, n = s->nloc;
     if (ld < (size_t)N) return fail("ld < N");
     HIPCHK(hipSetDevice(s->dev));
+    if (F && settle_forces(s)) return -1;
     if (R) {
         std::vector<double> h((size_t)3 * S * W);
         HIPCHK(hipMemcpyAsync(h.data(), s->dR, h.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
@@ -510,6 +573,23 @@ extern "C" int mdqt_init(mdqt_ctx* s) {
 // hot path
 // ---------------------------------------------------------------------------------------------
 
+// smallest d with fl(d / L) >= 0.5 in IEEE double (the device's division is IEEE too), so that
+// round(dx/L) == (dx >= T) - (dx <= -T) for |dx| < 1.25 L: the minimum image without a division
+static double mic_threshold(double L) {
+    double d = 0.5 * L;
+    while (d > 0 && d / L >= 0.5) d = nextafter(d, 0.);
+    while (d / L < 0.5) d = nextafter(d, INFINITY);
+    return d;
+}
+
+static void fill_pair_consts(ForceArgs& a, double L, double lDeb, int variant) {
+    a.L = L; a.lDeb = lDeb; a.Rcut = L / 2.;               // :196
+    a.invlDeb = 1. / lDeb;                                  // :224
+    a.micT = mic_threshold(L);
+    a.micGuard = 1.25 * L;
+    a.variant = variant;
+}
+
 static ForceArgs force_args(mdqt_ctx* s, double* out) {
     ForceArgs a;
     a.Rall = s->dR;
@@ -517,8 +597,16 @@ static ForceArgs force_args(mdqt_ctx* s, double* out) {
     a.N = s->N; a.S = s->S;
     a.row_lo = s->lo; a.nrows = s->nloc;
     a.nseg = s->nseg; a.seglen = s->seglen;
-    a.L = s->L; a.lDeb = s->lDeb; a.Rcut = s->L / 2.;     // :196
+    fill_pair_consts(a, s->L, s->lDeb, s->force_variant);
     return a;
+}
+
+// fold pending force partials into F (consumers other than the substep kernels)
+static int settle_forces(mdqt_ctx* s) {
+    if (!s->f_pending) return 0;
+    HIPCHK(launch_reduce_segments(s->dFpart, s->dF, s->nseg, s->nloc, s->S, 3, s->stream));
+    s->f_pending = false;
+    return 0;
 }
 
 // record the next timing event of kind k (start/stop alternate)
@@ -542,7 +630,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         HIPCHK(launch_forces(force_args(s, s->dF), s->stream));
     } else {
         HIPCHK(launch_forces(force_args(s, s->dFpart), s->stream));
-        HIPCHK(launch_reduce_segments(s->dFpart, s->dF, s->nseg, s->nloc, s->S, 3, s->stream));
+        s->f_pending = true;       // summed by the next substep launch (or settle_forces)
     }
     if (s->timing && mark(s, 0)) return -1;
     return 0;
@@ -558,6 +646,8 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         memset(&a, 0, sizeof a);
         a.R = s->dR + (size_t)s->p.rank * 3 * s->S;
         a.V = s->dV; a.F = s->dF; a.psi = s->dPsi; a.tPart = s->dTp;
+        a.Fpart = s->dFpart; a.nseg = s->f_pending ? s->nseg : 1;
+        s->f_pending = false;
         a.n = s->nloc; a.S = s->S; a.gid0 = (uint64_t)s->lo;
         a.q0 = s->qidx;
         a.nsub = m; a.do_step = do_step; a.do_qt = do_qt;
@@ -570,7 +660,7 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             if (advance_t) t += s->dtQ;                    // qstep: t += dtQuant (:716)
         }
         if (s->timing && mark(s, 1)) return -1;
-        HIPCHK(launch_substeps(a, s->stream));
+        HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->stream));
         if (s->timing && mark(s, 1)) return -1;
         if (advance_t) {
             s->t = t;
@@ -592,6 +682,7 @@ extern "C" int mdqt_substeps(mdqt_ctx* s, int n) {
 extern "C" int mdqt_md_steps(mdqt_ctx* s, int n) {
     if (!s) return fail("NULL context");
     for (int k = 0; k < n; ++k) {
+        if (mdqt_allgather_positions(s)) return -1;     // sharded: other slabs' R
         if (mdqt_forces(s)) return -1;
         s->c0++;
         if (mdqt_substeps(s, s->ratio)) return -1;
@@ -601,7 +692,7 @@ extern "C" int mdqt_md_steps(mdqt_ctx* s, int n) {
 
 // stateless pair kernels on host arrays (tests, and the MD-only programs' force seam)
 static int pairs_raw(int mode, int N, double L, double lDeb, const double* R, size_t ld, double* out,
-                     int nseg_req, int device) {
+                     int nseg_req, int device, int variant) {
     if (N < 1 || !R || !out || ld < (size_t)N) return fail("pairs_raw: bad arguments");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail("no HIP device available");
@@ -624,7 +715,8 @@ static int pairs_raw(int mode, int N, double L, double lDeb, const double* R, si
     HIPCHK(hipMemcpyAsync(dR, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, st));
     ForceArgs a;
     a.Rall = dR; a.Fpart = dP; a.N = N; a.S = S; a.row_lo = 0; a.nrows = N;
-    a.nseg = nseg; a.seglen = tmp.seglen; a.L = L; a.lDeb = lDeb; a.Rcut = L / 2.;
+    a.nseg = nseg; a.seglen = tmp.seglen;
+    fill_pair_consts(a, L, lDeb, variant);
     HIPCHK(mode == 0 ? launch_forces(a, st) : launch_potential_rows(a, st));
     HIPCHK(launch_reduce_segments(dP, dO, nseg, N, S, mode == 0 ? 3 : 1, st));
     HIPCHK(hipMemcpyAsync(h.data(), dO, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -641,13 +733,13 @@ static int pairs_raw(int mode, int N, double L, double lDeb, const double* R, si
 }
 
 extern "C" int mdqt_forces_raw(int N, double L, double lDeb, const double* R, size_t ld, double* F,
-                               int nseg, int device) {
-    return pairs_raw(0, N, L, lDeb, R, ld, F, nseg, device);
+                               int nseg, int device, int variant) {
+    return pairs_raw(0, N, L, lDeb, R, ld, F, nseg, device, variant);
 }
 
 extern "C" int mdqt_potentials_raw(int N, double L, double lDeb, const double* R, size_t ld, double* U,
-                                   int nseg, int device) {
-    return pairs_raw(1, N, L, lDeb, R, ld, U, nseg, device);
+                                   int nseg, int device, int variant) {
+    return pairs_raw(1, N, L, lDeb, R, ld, U, nseg, device, variant);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -657,6 +749,7 @@ extern "C" int mdqt_potentials_raw(int N, double L, double lDeb, const double* R
 // device: scratch[0] = sum over owned rows of the full-row pair potential
 static int potential_rows(mdqt_ctx* s, double* urow_dev) {
     if (s->nloc == 0) return 0;
+    if (settle_forces(s)) return -1;     // the potential rows reuse the partials buffer
     HIPCHK(launch_potential_rows(force_args(s, s->dFpart), s->stream));
     HIPCHK(launch_reduce_segments(s->dFpart, urow_dev, s->nseg, s->nloc, s->S, 1, s->stream));
     return 0;
@@ -688,9 +781,10 @@ extern "C" int mdqt_partial_observables(mdqt_ctx* s, double vxAvg, double out5[5
 
 extern "C" int mdqt_epotential(mdqt_ctx* s, double* Epot) {   // Epotential(), :244-281
     if (!s) return fail("NULL context");
-    if (s->p.world_size != 1) return fail("mdqt_epotential: use mdqt_partial_observables under sharding");
     double o[5];
+    if (mdqt_allgather_positions(s)) return -1;          // collective when sharded
     if (mdqt_partial_observables(s, 0., o, nullptr)) return -1;
+    if (mdqt_allreduce_sum(s, o, 5)) return -1;
     // sum_{i<j} u = (sum_i sum_{j != i} u) / 2 ; Epot /= N (:280)
     s->Epot = s->N > 0 ? (o[4] / 2.) / (double)s->N : 0.;
     if (Epot) *Epot = s->Epot;
@@ -699,18 +793,23 @@ extern "C" int mdqt_epotential(mdqt_ctx* s, double* Epot) {   // Epotential(), :
 
 extern "C" int mdqt_observables(mdqt_ctx* s, double out7[7], double* Pvel, double* pops) {
     if (!s) return fail("NULL context");
-    if (s->p.world_size != 1) return fail("mdqt_observables: use mdqt_partial_observables under sharding");
     const int N = s->N;
     double o[5];
+    if (mdqt_allgather_positions(s)) return -1;          // collective when sharded
     // pass 1: <vx> (:934-938)
     HIPCHK(hipSetDevice(s->dev));
     HIPCHK(launch_sum_vx(s->dV, s->nloc, s->dScr, s->stream));
     double sumvx = 0.;
     HIPCHK(hipMemcpyAsync(&sumvx, s->dScr, sizeof(double), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
+    if (s->nloc == 0) sumvx = 0.;
+    if (mdqt_allreduce_sum(s, &sumvx, 1)) return -1;
     const double velXAvg = N > 0 ? sumvx / (double)N : 0.;
-    std::vector<double> P((size_t)3 * NBINS);
+    std::vector<double> P((size_t)3 * NBINS + 5);
     if (mdqt_partial_observables(s, velXAvg, o, P.data())) return -1;
+    memcpy(P.data() + 3 * NBINS, o, sizeof o);
+    if (mdqt_allreduce_sum(s, P.data(), P.size())) return -1;
+    memcpy(o, P.data() + 3 * NBINS, sizeof o);
     const double EkinX = o[1] / (double)N, EkinY = o[2] / (double)N, EkinZ = o[3] / (double)N;   // :945-947
     s->Epot = (o[4] / 2.) / (double)N;                                                          // :948
     out7[0] = s->t; out7[1] = EkinX; out7[2] = EkinY; out7[3] = EkinZ; out7[4] = s->Epot;
@@ -720,8 +819,9 @@ extern "C" int mdqt_observables(mdqt_ctx* s, double out7[7], double* Pvel, doubl
         for (int j = 0; j < 3 * NBINS; ++j) Pvel[j] = P[j] / norm;
     }
     if (pops) {                                                                                 // :1016-1023
-        std::vector<double> psi((size_t)24 * N);
+        std::vector<double> psi((size_t)24 * N, 0.);
         if (mdqt_get_state(s, nullptr, nullptr, nullptr, N, psi.data(), nullptr, nullptr)) return -1;
+        if (mdqt_allreduce_sum(s, psi.data(), psi.size())) return -1;   // zero-padded gather
         for (int i = 0; i < N; i++) {
             const double* w = psi.data() + (size_t)24 * i;
             auto nrm = [&](int k) { return w[2 * k] * w[2 * k] + w[2 * k + 1] * w[2 * k + 1]; };
@@ -778,7 +878,10 @@ extern "C" int mdqt_output(mdqt_ctx* s) {                 // output(), SpeedUp:9
     double o[7];
     std::vector<double> P((size_t)3 * NBINS), pops((size_t)3 * (N > 0 ? N : 1)), V((size_t)3 * (N > 0 ? N : 1));
     if (mdqt_observables(s, o, P.data(), pops.data())) return -1;
+    std::fill(V.begin(), V.end(), 0.);
     if (mdqt_get_state(s, nullptr, V.data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
+    if (mdqt_allreduce_sum(s, V.data(), (size_t)N)) return -1;      // vx column, zero-padded gather
+    if (s->p.rank != 0) { s->counter++; return 0; }                 // files are rank 0's
     FILE* fa = open_in(s, "energies.dat", "a");
     if (!fa) return -1;
     fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\t%lg\n", o[0], o[1], o[2], o[3], o[4], o[5], o[6]);   // :954
@@ -812,8 +915,12 @@ extern "C" int mdqt_output(mdqt_ctx* s) {                 // output(), SpeedUp:9
 
 extern "C" int mdqt_write_conditions(mdqt_ctx* s, int c0) {   // writeConditions, :725-784
     const int N = s->N;
-    std::vector<double> R((size_t)3 * (N > 0 ? N : 1)), V(R.size()), psi((size_t)24 * (N > 0 ? N : 1));
+    std::vector<double> R((size_t)3 * (N > 0 ? N : 1), 0.), V(R.size(), 0.), psi((size_t)24 * (N > 0 ? N : 1), 0.);
+    if (mdqt_allgather_positions(s)) return -1;           // collective when sharded
     if (mdqt_get_state(s, R.data(), V.data(), nullptr, N, psi.data(), nullptr, nullptr)) return -1;
+    if (mdqt_allreduce_sum(s, V.data(), V.size())) return -1;
+    if (mdqt_allreduce_sum(s, psi.data(), psi.size())) return -1;
+    if (s->p.rank != 0) return 0;
     char b[96];
     snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
     FILE* fa = open_in(s, b, "w");
@@ -908,7 +1015,7 @@ extern "C" int mdqt_read_conditions(mdqt_ctx* s, int c0) {    // readConditions,
 
 extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp:1139-1383
     if (!s) return fail("NULL context");
-    if (s->p.world_size != 1) return fail("mdqt_run drives one GPU; the sharded loop lives in the host driver");
+    if (s->p.world_size > 1 && !s->comm) return fail("mdqt_run: sharded run needs mdqt_comm_init first");
     if (mdqt_setup_directories(s)) return -1;
     if (s->p.newRun == 1) {
         if (mdqt_init(s)) return -1;
@@ -923,6 +1030,7 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
         if ((s->c0 + 1) % sf == 0 && tsc == 1)                                          // :1365
             if (mdqt_output(s)) return -1;
         if (tsc == ratio) {                                                             // :1369
+            if (mdqt_allgather_positions(s)) return -1;                                 // §8e
             if (mdqt_forces(s)) return -1;
             s->c0++;
             tsc = 0;
@@ -942,6 +1050,21 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
 // ---------------------------------------------------------------------------------------------
 // streams, timing, multi-GPU plumbing
 // ---------------------------------------------------------------------------------------------
+
+extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
+    if (!s || !name) return fail("mdqt_set_option: NULL argument");
+    if (!strcmp(name, "force_kernel")) {
+        if (value < 0 || value > 1) return fail("force_kernel must be 0 (exact) or 1 (fast)");
+        s->force_variant = value;
+        return 0;
+    }
+    if (!strcmp(name, "substep_kernel")) {
+        if (value < 0 || value > 2) return fail("substep_kernel must be 0 (auto), 1 (thread/ion) or 2 (lanes/ion)");
+        s->substep_mode = value;
+        return 0;
+    }
+    return fail("unknown option %s", name);
+}
 
 extern "C" int mdqt_set_stream(mdqt_ctx* s, void* st) {
     s->stream = st ? (hipStream_t)st : s->own;
@@ -979,5 +1102,98 @@ extern "C" int mdqt_kernel_time_totals(mdqt_ctx* s, double* force_ms, int* nforc
     if (sub_ms) *sub_ms = tot[1];
     if (nsub) *nsub = s->evused[1] / 2;
     s->evused[0] = s->evused[1] = 0;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// RCCL: one communicator per context over world_size ranks (one process per GPU).  The only
+// data-path collective is the per-MD-step all-gather of the position slabs;
+// output steps all-reduce a few scalars, the KDE bins and the per-ion file columns.
+// ---------------------------------------------------------------------------------------------
+
+#define NCCLCHK(expr)                                                                   \
+    do {                                                                                \
+        ncclResult_t r_ = (expr);                                                       \
+        if (r_ != ncclSuccess) return fail("%s failed: %s", #expr, ncclGetErrorString(r_)); \
+    } while (0)
+
+extern "C" int mdqt_comm_unique_id(void* out, size_t len) {
+    if (!out || len < sizeof(ncclUniqueId)) return fail("mdqt_comm_unique_id: need %zu bytes", sizeof(ncclUniqueId));
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof id);
+    return 0;
+}
+
+extern "C" int mdqt_comm_init(mdqt_ctx* s, const void* uid, size_t len) {
+    if (!s || !uid || len < sizeof(ncclUniqueId)) return fail("mdqt_comm_init: bad arguments");
+    if (s->comm) return fail("mdqt_comm_init: communicator already initialised");
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof id);
+    HIPCHK(hipSetDevice(s->dev));
+    NCCLCHK(ncclCommInitRank(&s->comm, s->p.world_size, id, s->p.rank));
+    return 0;
+}
+
+extern "C" int mdqt_comm_init_local(mdqt_ctx* const* ctxs, int n) {
+    if (!ctxs || n < 1) return fail("mdqt_comm_init_local: bad arguments");
+    for (int r = 0; r < n; ++r) {
+        if (!ctxs[r] || ctxs[r]->p.world_size != n || ctxs[r]->p.rank != r)
+            return fail("mdqt_comm_init_local: context %d is not rank %d of %d", r, r, n);
+        if (ctxs[r]->S != ctxs[0]->S || ctxs[r]->N != ctxs[0]->N)
+            return fail("mdqt_comm_init_local: contexts disagree on N");
+    }
+    for (int r = 0; r < n; ++r) ctxs[r]->local.assign(ctxs, ctxs + n);
+    return 0;
+}
+
+extern "C" int mdqt_allgather_positions(mdqt_ctx* s) {
+    if (!s) return fail("NULL context");
+    if (s->p.world_size == 1) return 0;
+    const size_t cnt = (size_t)3 * s->S;
+    if (!s->comm && !s->local.empty()) {
+        // in-process group: push this rank's slab into every peer (callers run the ranks in
+        // lockstep: every rank pushes before any rank computes forces)
+        HIPCHK(hipSetDevice(s->dev));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        for (mdqt_ctx* q : s->local) {
+            if (q == s) continue;
+            HIPCHK(hipMemcpyPeer(q->dR + (size_t)s->p.rank * cnt, q->dev, s->dR + (size_t)s->p.rank * cnt,
+                                 s->dev, cnt * sizeof(double)));
+        }
+        return 0;
+    }
+    if (!s->comm) return fail("mdqt_allgather_positions: no communicator (mdqt_comm_init)");
+    HIPCHK(hipSetDevice(s->dev));
+    NCCLCHK(ncclAllGather(s->dR + (size_t)s->p.rank * cnt, s->dR, cnt, ncclDouble, s->comm, s->stream));
+    return 0;
+}
+
+extern "C" int mdqt_allreduce_sum(mdqt_ctx* s, double* buf, size_t n) {
+    if (!s || (!buf && n)) return fail("mdqt_allreduce_sum: bad arguments");
+    if (s->p.world_size == 1 || n == 0) return 0;
+    if (!s->comm) return fail("mdqt_allreduce_sum: no communicator (mdqt_comm_init)");
+    HIPCHK(hipSetDevice(s->dev));
+    if (n > s->dCommCap) {
+        if (s->dComm) HIPCHK(hipFree(s->dComm));
+        s->dComm = nullptr;
+        HIPCHK(hipMalloc(&s->dComm, n * sizeof(double)));
+        s->dCommCap = n;
+    }
+    HIPCHK(hipMemcpyAsync(s->dComm, buf, n * sizeof(double), hipMemcpyHostToDevice, s->stream));
+    NCCLCHK(ncclAllReduce(s->dComm, s->dComm, n, ncclDouble, ncclSum, s->comm, s->stream));
+    HIPCHK(hipMemcpyAsync(buf, s->dComm, n * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int mdqt_slab_bounds(const mdqt_ctx* s, int* lo, int* hi) {
+    if (lo) *lo = s->lo;
+    if (hi) *hi = s->hi;
+    return 0;
+}
+
+extern "C" int mdqt_set_counters(mdqt_ctx* s, int c0, unsigned counter, double Epot, double Epot0) {
+    s->c0 = c0; s->counter = counter; s->Epot = Epot; s->Epot0 = Epot0;
     return 0;
 }

@@ -40,10 +40,27 @@ struct QTConst {
     uint32_t seed, job;         // Philox key
 };
 
+// Per-lane tables of the lane-per-state QT kernel (16 lanes per ion, lane k <-> state k).
+// Row k of M has its diagonal and up to three off-diagonal entries, in slots A < B < C by
+// column; `order` says where the diagonal falls in the ascending-column sum:
+//   0: D,A,B   1: A,D,B,C   2: A,D   3: A,B,D
+struct LaneTab {
+    int colA[16], colB[16], colC[16];
+    int order[16], hasB[16], hasC[16];
+    int dynB[16], dynC[16];      // slot holds a time-dependent entry: 1 = (8,5)/(9,4) form, 2 = (5,8)/(4,9)
+    double cAre[16], cAim[16], cBre[16], cBim[16], cCre[16], cCim[16];   // static M entries
+    double dynScale[16];         // a8 or a11 for the dynamic slot of rows 4, 5, 8, 9
+    double gA[16], gB[16];       // optical-kick weights of rho_im(w_k, w_colA/colB) (:503)
+    double dP[16];               // decayMatrix diagonal (0 off the P levels)
+    double hd[16];               // imag of hamDecayTerm diagonal (0 off the P levels)
+};
+
 struct SubstepArgs {
     double* R;          // this rank's slab of the gathered positions, [3][S]
     double* V;          // [3][S]
-    const double* F;    // [3][S]
+    double* F;          // [3][S]
+    const double* Fpart;// if nseg > 1: force partials [nseg][3][S] summed here (in segment
+    int nseg;           //   order) into F before the first substep, and F is written back
     double* psi;        // [24][S]: component-major (re0, im0, re1, ... im11)
     double* tPart;      // [S]
     int n;              // ions in this slab
@@ -64,6 +81,10 @@ struct ForceArgs {
     int row_lo, nrows;  // owned global rows [row_lo, row_lo + nrows)
     int nseg, seglen;   // j segmentation (a function of N only)
     double L, lDeb, Rcut;
+    double invlDeb;     // 1./lDeb (the reference recomputes it per pair; same IEEE value)
+    double micT;        // smallest d with fl(d/L) >= 0.5: round(dx/L) = [dx >= micT] - [dx <= -micT]
+    double micGuard;    // |dx| below this is inside the threshold rule's validity (|dx/L| < 1.5)
+    int variant;        // 0 = exact (the reference's operations), 1 = fast (rsqrt/reciprocal form)
 };
 
 // ---- launchers (mdqt_kernels.hip) ----
@@ -71,7 +92,10 @@ hipError_t launch_forces(const ForceArgs& a, hipStream_t s);
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
                                   hipStream_t s);
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[seg][0][i]
-hipError_t launch_substeps(const SubstepArgs& a, hipStream_t s);
+// mode: 0 = auto (lane-per-state below kLaneKernelMaxIons ions, thread-per-ion above),
+//       1 = thread-per-ion, 2 = lane-per-state.  Both are bit-identical.
+constexpr int kLaneKernelMaxIons = 98304;
+hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, hipStream_t s);
 // deterministic sums: out[0] = sum vx; needs scratch >= 1024 doubles
 hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s);
 // out[0..2] = sum 0.5 (vx-avg)^2, 0.5 vy^2, 0.5 vz^2 ; out[3] = sum of rows[0..nrows) of

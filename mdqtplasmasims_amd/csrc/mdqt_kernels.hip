@@ -31,7 +31,7 @@ __device__ __forceinline__ const double* pos_base(const double* Rall, int g, int
 // ------------------------------------------------------------------------------------------
 constexpr int FT = 256;   // threads per block = rows per block = j tile
 
-template <int MODE>   // 0: force, 1: potential
+template <int MODE, int VARIANT>   // MODE 0: force, 1: potential; VARIANT 0: exact, 1: fast
 __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
     __shared__ double sx[FT], sy[FT], sz[FT];
     const int tid = threadIdx.x;
@@ -44,7 +44,8 @@ __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
         const double* p = pos_base(a.Rall, gi, a.S);
         rx = p[0]; ry = p[a.S]; rz = p[2 * a.S];
     }
-    const double L = a.L, lDeb = a.lDeb, Rcut = a.Rcut;
+    const double L = a.L, lDeb = a.lDeb, Rcut = a.Rcut, invlDeb = a.invlDeb;
+    const double T = a.micT, G = a.micGuard;
     double fx = 0., fy = 0., fz = 0.;
     const int j0 = seg * a.seglen;
     const int j1 = min(a.N, j0 + a.seglen);
@@ -63,18 +64,49 @@ __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
                 double dx = rx - sx[k];                    // SpeedUp:213-215
                 double dy = ry - sy[k];
                 double dz = rz - sz[k];
-                dx -= L * round(dx / L);                   // minimum image :218-220
-                dy -= L * round(dy / L);
-                dz -= L * round(dz / L);
-                const double dr = sqrt(dx * dx + dy * dy + dz * dz);   // :221
-                if (dr > 0 && dr < Rcut) {                 // :222
-                    if (MODE == 0) {
-                        const double ftotal = (1. / dr + 1. / lDeb) * exp(-dr / lDeb) / (dr * dr); // :224
-                        fx += dx * ftotal;                 // :225-230 (i's view)
-                        fy += dy * ftotal;
-                        fz += dz * ftotal;
-                    } else {
-                        fx += exp(-dr / lDeb) / (dr);      // :265
+                // minimum image dx -= L*round(dx/L) (:218-220), evaluated exactly without the
+                // division: for |dx/L| < 1.5, round(dx/L) is +1 iff dx >= T, -1 iff dx <= -T
+                if (fabs(dx) < G && fabs(dy) < G && fabs(dz) < G) {
+                    dx = (dx >= T) ? dx - L : ((dx <= -T) ? dx + L : dx);
+                    dy = (dy >= T) ? dy - L : ((dy <= -T) ? dy + L : dy);
+                    dz = (dz >= T) ? dz - L : ((dz <= -T) ? dz + L : dz);
+                } else {
+                    dx -= L * round(dx / L);
+                    dy -= L * round(dy / L);
+                    dz -= L * round(dz / L);
+                }
+                const double r2 = dx * dx + dy * dy + dz * dz;
+                if (VARIANT == 0) {
+                    const double dr = sqrt(r2);            // :221
+                    if (dr > 0 && dr < Rcut) {             // :222
+                        if (MODE == 0) {
+                            const double ftotal = (1. / dr + invlDeb) * exp(-dr / lDeb) / (dr * dr); // :224
+                            fx += dx * ftotal;             // :225-230 (i's view)
+                            fy += dy * ftotal;
+                            fz += dz * ftotal;
+                        } else {
+                            fx += exp(-dr / lDeb) / (dr);  // :265
+                        }
+                    }
+                } else {
+                    // same law in reciprocal form: 1/r from a refined v_rsq_f64, r = r2/r
+                    // (a few ulp per pair; the force gate is 1e-13 relative)
+                    if (r2 > 0) {
+                        double ri = __builtin_amdgcn_rsq(r2);
+                        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
+                        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
+                        const double dr = r2 * ri;
+                        if (dr < Rcut) {
+                            const double e = exp(-dr * invlDeb);
+                            if (MODE == 0) {
+                                const double ftotal = ((ri + invlDeb) * e) * (ri * ri);
+                                fx += dx * ftotal;
+                                fy += dy * ftotal;
+                                fz += dz * ftotal;
+                            } else {
+                                fx += e * ri;
+                            }
+                        }
                     }
                 }
             }
@@ -87,15 +119,30 @@ __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
     }
 }
 
+// Canonical sum of the nseg segment partials of one (row, component): eight interleaved
+// accumulators (segment s goes to s % 8, ascending), combined as ((a0+a1)+(a2+a3))+((a4+a5)+
+// (a6+a7)).  Fixed order => deterministic and identical wherever it is evaluated; the loads are
+// independent, so the dependent chain is nseg/8 adds instead of nseg.
+__device__ __forceinline__ double seg_sum(const double* __restrict__ p, size_t stride, int nseg) {
+    double a[8] = {0., 0., 0., 0., 0., 0., 0., 0.};
+    int s = 0;
+    for (; s + 8 <= nseg; s += 8) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] += p[(size_t)(s + q) * stride];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if (s + q < nseg) a[q] += p[(size_t)(s + q) * stride];
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
 __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restrict__ Fpart,
                                                          double* __restrict__ F, int nseg,
                                                          int nrows, int S, int ncomp) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int c = blockIdx.y;
     if (i >= nrows || c >= ncomp) return;
-    double acc = Fpart[(size_t)c * S + i];
-    for (int s = 1; s < nseg; ++s) acc += Fpart[((size_t)s * 3 + c) * S + i];
-    F[(size_t)c * S + i] = acc;
+    F[(size_t)c * S + i] = seg_sum(Fpart + (size_t)c * S + i, (size_t)3 * S, nseg);
 }
 
 static int seg_blocks(int nrows) { return (nrows + FT - 1) / FT; }
@@ -103,14 +150,16 @@ static int seg_blocks(int nrows) { return (nrows + FT - 1) / FT; }
 hipError_t launch_forces(const ForceArgs& a, hipStream_t s) {
     if (a.nrows <= 0) return hipSuccess;
     dim3 grid(seg_blocks(a.nrows), a.nseg);
-    hipLaunchKernelGGL(k_pairs<0>, grid, dim3(FT), 0, s, a);
+    if (a.variant == 1) hipLaunchKernelGGL((k_pairs<0, 1>), grid, dim3(FT), 0, s, a);
+    else hipLaunchKernelGGL((k_pairs<0, 0>), grid, dim3(FT), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s) {
     if (a.nrows <= 0) return hipSuccess;
     dim3 grid(seg_blocks(a.nrows), a.nseg);
-    hipLaunchKernelGGL(k_pairs<1>, grid, dim3(FT), 0, s, a);
+    if (a.variant == 1) hipLaunchKernelGGL((k_pairs<1, 1>), grid, dim3(FT), 0, s, a);
+    else hipLaunchKernelGGL((k_pairs<1, 0>), grid, dim3(FT), 0, s, a);
     return hipGetLastError();
 }
 
@@ -329,7 +378,15 @@ __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
     const int S = a.S;
     double x = a.R[i], y = a.R[S + i], z = a.R[2 * S + i];
     double vx = a.V[i], vy = a.V[S + i], vz = a.V[2 * S + i];
-    const double fx = a.F[i], fy = a.F[S + i], fz = a.F[2 * S + i];
+    double fx, fy, fz;
+    if (a.nseg > 1) {        // forces() left segment partials: canonical sum (seg_sum)
+        fx = seg_sum(a.Fpart + i, (size_t)3 * S, a.nseg);
+        fy = seg_sum(a.Fpart + S + i, (size_t)3 * S, a.nseg);
+        fz = seg_sum(a.Fpart + 2 * S + i, (size_t)3 * S, a.nseg);
+        a.F[i] = fx; a.F[S + i] = fy; a.F[2 * S + i] = fz;
+    } else {
+        fx = a.F[i]; fy = a.F[S + i]; fz = a.F[2 * S + i];
+    }
     double tPart = a.tPart[i];
     cxd w[NS];
     if (a.do_qt) {
@@ -380,9 +437,209 @@ __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
     }
 }
 
-hipError_t launch_substeps(const SubstepArgs& a, hipStream_t s) {
+// ------------------------------------------------------------------------------------------
+// Kernel 2b: the same substeps with one ion per 16-lane group, lane k holding state k
+// (4 ions per wave64).  For small N (C2: 3573 ions = 56 waves thread-per-ion, 894 waves
+// here) this fills the chip; the sparse matvec row k needs y at up to three other states,
+// fetched with ds_bpermute inside the group.  Every floating-point operation is the one
+// k_substeps performs, in the same order (cross-lane moves are exact), so the two kernels
+// are bit-identical — tests/test_gpu_parity.py checks it.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double gat(double v, int src) {
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ cxd gatc(cxd v, int src) { return {gat(v.re, src), gat(v.im, src)}; }
+
+__global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const LaneTab* __restrict__ tab) {
+    const int lane = threadIdx.x & 63;
+    const int k = lane & 15;                          // state index (valid when < 12)
+    const int g0 = lane & ~15;                        // first lane of this ion's group
+    const int iraw = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const bool store = iraw < a.n;
+    const int i = store ? iraw : a.n - 1;             // idle groups shadow the last ion
+    const bool st = k < NS;
+    const QTConst& qc = a.qc;
+    const int S = a.S;
+    // per-lane row structure of M and kick weights
+    const int srcA = g0 + tab->colA[k], srcB = g0 + tab->colB[k], srcC = g0 + tab->colC[k];
+    const int order = tab->order[k], hasB = tab->hasB[k], hasC = tab->hasC[k];
+    const int dynB = tab->dynB[k], dynC = tab->dynC[k];
+    const cxd cA = {tab->cAre[k], tab->cAim[k]};
+    cxd cB = {tab->cBre[k], tab->cBim[k]}, cC = {tab->cCre[k], tab->cCim[k]};
+    const double dynScale = tab->dynScale[k];
+    const double gA = tab->gA[k], gB = tab->gB[k], dPk = tab->dP[k], hdk = tab->hd[k];
+    // ion state (replicated over the group) and this lane's amplitude
+    double x = a.R[i], y = a.R[S + i], z = a.R[2 * S + i];
+    double vx = a.V[i], vy = a.V[S + i], vz = a.V[2 * S + i];
+    double fx, fy, fz;
+    if (a.nseg > 1) {        // lanes 0..2 sum component k of the segment partials, then share
+        double fk = 0.;
+        if (k < 3) {
+            fk = seg_sum(a.Fpart + (size_t)k * S + i, (size_t)3 * S, a.nseg);
+            if (store) a.F[(size_t)k * S + i] = fk;
+        }
+        fx = gat(fk, g0 + 0); fy = gat(fk, g0 + 1); fz = gat(fk, g0 + 2);
+    } else {
+        fx = a.F[i]; fy = a.F[S + i]; fz = a.F[2 * S + i];
+    }
+    double tPart = a.tPart[i];
+    cxd w = {0., 0.};
+    if (a.do_qt && st) w = {a.psi[(size_t)(2 * k) * S + i], a.psi[(size_t)(2 * k + 1) * S + i]};
+    const double L = a.L;
+    const double dt = qc.dtQ;
+    const double DT = 0.5 * dt;
+    const uint64_t gid = a.gid0 + (uint64_t)i;
+    for (int s = 0; s < a.nsub; ++s) {
+        if (a.do_step) {                              // step(), as in k_substeps
+            const bool moving = a.t[s] > 0;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                if (moving) {
+                    x += DT * vx; y += DT * vy; z += DT * vz;
+                } else {
+                    x += DT * vx + DT * DT * fx;
+                    y += DT * vy + DT * DT * fy;
+                    z += DT * vz + DT * DT * fz;
+                }
+                if (x < 0) x += L;
+                if (x > L) x -= L;
+                if (y < 0) y += L;
+                if (y > L) y -= L;
+                if (z < 0) z += L;
+                if (z > L) z -= L;
+                if (half == 0) { vx += dt * fx; vy += dt * fy; vz += dt * fz; }
+            }
+        }
+        if (!a.do_qt) continue;
+        // ---- qstep() for this ion (SpeedUp:478-712), state k on this lane ----
+        const double eD = a.expDet[s];
+        const double velQuant = vx * qc.pv2q;
+        tPart += qc.dtQ;
+        const double Tk = (w.re * dPk) * w.re + (w.im * dPk) * w.im;
+        const double dp = qc.h * (((gat(Tk, g0 + 2) + gat(Tk, g0 + 3)) + gat(Tk, g0 + 4)) + gat(Tk, g0 + 5));
+        double u1, u2;
+        philox_pair(qc, gid, a.q0 + (uint64_t)s, 0, u1, u2);
+        const cxd wA = gatc(w, srcA), wB = gatc(w, srcB);
+        double kick;
+        if (u1 > dp) {
+            // optical kick from the pre-step density matrix (:490-503)
+            const double kA = rho_im(w, wA) * gA, kB = rho_im(w, wB) * gB;
+            const double sum1 = ((gat(kA, g0 + 1) + gat(kA, g0 + 0)) - gat(kB, g0 + 1)) - gat(kB, g0 + 0);
+            const double sum2 = ((((((gat(kB, g0 + 8) + gat(kB, g0 + 9)) + gat(kA, g0 + 10)) + gat(kA, g0 + 11)) -
+                                  gat(kA, g0 + 6)) - gat(kA, g0 + 7)) - gat(kA, g0 + 8)) - gat(kA, g0 + 9);
+            kick = qc.kickS * sum1 * qc.dtQ * qc.gamToE + qc.kickD * sum2 * qc.dtQ * qc.gamToE;
+            // this lane's row of M = I - i h H (:506-526)
+            const double vq = velQuant + eD;
+            const double ER = -qc.det - velQuant - eD;
+            const double EL = -qc.det + velQuant + eD;
+            const double E67 = (-qc.det + qc.detDP + (1 - qc.kRat) * (velQuant + eD));
+            const double E1011 = (-qc.det + qc.detDP + (qc.kRat - 1) * (velQuant + eD));
+            const double E89 = (-qc.det + qc.detDP - velQuant - eD - qc.kRat * (velQuant + eD));
+            const double E = (k < 2) ? 0. : (k < 4) ? ER : (k < 6) ? EL : (k < 8) ? E67 : (k < 10) ? E89 : E1011;
+            const double h = qc.h;
+            const cxd Md = {(k >= 2 && k < 6) ? 1. + h * hdk : 1., -(h * E)};
+            const double phi = 2. * vq * (1 + qc.kRat) * tPart * qc.gamToE;
+            double sn, cs;
+            sincos(phi, &sn, &cs);
+            const double as = dynScale * sn, ac = dynScale * cs;
+            if (dynB) cB = {-(h * as), h * ac};       // M85 / M94
+            if (dynC) cC = {h * as, h * ac};          // M58 / M49
+            cxd yv = w, acc = {0., 0.};
+            cxd yA = wA, yB = wB;
+#pragma unroll
+            for (int stg = 0; stg < 4; ++stg) {
+                double dpy = dp;
+                if (stg > 0) {
+                    const double Ty = (yv.re * dPk) * yv.re + (yv.im * dPk) * yv.im;
+                    dpy = qc.h * (((gat(Ty, g0 + 2) + gat(Ty, g0 + 3)) + gat(Ty, g0 + 4)) + gat(Ty, g0 + 5));
+                    yA = gatc(yv, srcA);
+                    yB = gatc(yv, srcB);
+                }
+                const cxd yC = gatc(yv, srcC);
+                const double pref = 1 / sqrt(1 - dpy);
+                const cxd tA = cmul(cA, yA), tB = cmul(cB, yB), tC = cmul(cC, yC), tD = cmul(Md, yv);
+                // ascending-column row sum (order patterns of LaneTab)
+                const cxd second = (order == 3) ? tB : tD;
+                const cxd third = (order == 3) ? tD : tB;
+                cxd ws = cadd(tA, second);
+                if (hasB) ws = cadd(ws, third);
+                if (hasC) ws = cadd(ws, tC);
+                const double step = (stg == 2) ? h : qc.dtHalf;
+                const cxd kk = {qc.invh * (pref * ws.re - yv.re), qc.invh * (pref * ws.im - yv.im)};
+                if (stg == 0) {
+                    acc = kk;
+                } else if (stg < 3) {
+                    acc = {acc.re + 3. * kk.re, acc.im + 3. * kk.im};
+                } else {
+                    const cxd sum = {acc.re + kk.re, acc.im + kk.im};
+                    w = {w.re + h * (sum.re / 8), w.im + h * (sum.im / 8)};
+                }
+                if (stg < 3) yv = {w.re + step * kk.re, w.im + step * kk.im};
+            }
+        } else {                                      // quantum jump (:573-703)
+            tPart = 0;
+            const double nk = w.re * w.re + w.im * w.im;
+            const double n3 = gat(nk, g0 + 2), n4 = gat(nk, g0 + 3), n5 = gat(nk, g0 + 4), n6 = gat(nk, g0 + 5);
+            const double tot = n3 + n4 + n5 + n6;
+            const double prob3 = n3 / tot, prob4 = n4 / tot, prob5 = n5 / tot;
+            const double rand2 = u2;
+            double randDOrS, randDir, rand3, dummy;
+            philox_pair(qc, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
+            philox_pair(qc, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
+            (void)dummy;
+            const bool sDecay = !(randDOrS < qc.pD);
+            if (!sDecay) kick = (randDir < 0.5) ? qc.vKickDP : -qc.vKickDP;
+            else kick = (randDir < 0.5) ? qc.vKick : -qc.vKick;
+            int target;
+            if (rand2 < prob3) {
+                if (sDecay) target = 1;
+                else target = (rand3 < qc.thD[0][0]) ? 11 : (rand3 < qc.thD[0][1]) ? 10 : 9;
+            } else if (rand2 < prob3 + prob4) {
+                if (sDecay) target = (rand3 < qc.thS3) ? 0 : 1;
+                else target = (rand3 < qc.thD[1][0]) ? 10 : (rand3 < qc.thD[1][1]) ? 9 : 8;
+            } else if (rand2 < prob3 + prob4 + prob5) {
+                if (sDecay) target = (rand3 < qc.thS4) ? 1 : 0;
+                else target = (rand3 < qc.thD[2][0]) ? 9 : (rand3 < qc.thD[2][1]) ? 8 : 7;
+            } else {
+                if (sDecay) target = 0;
+                else target = (rand3 < qc.thD[3][0]) ? 8 : (rand3 < qc.thD[3][1]) ? 7 : 6;
+            }
+            w = {k == target ? 1. : 0., 0.};
+        }
+        if (qc.renorm) {                              // :706-712
+            const double nk = w.re * w.re + w.im * w.im;
+            const double popS = gat(nk, g0 + 0) + gat(nk, g0 + 1);
+            double popP = gat(nk, g0 + 2);
+#pragma unroll
+            for (int q = 3; q < 6; ++q) popP = popP + gat(nk, g0 + q);
+            double popD = gat(nk, g0 + 6);
+#pragma unroll
+            for (int q = 7; q < 12; ++q) popD = popD + gat(nk, g0 + q);
+            const double nrm = sqrt(popS + popP + popD);
+            w = {w.re / nrm, w.im / nrm};
+        }
+        vx = vx + kick;
+    }
+    if (store) {
+        if (k == 0) {
+            a.R[i] = x; a.R[S + i] = y; a.R[2 * S + i] = z;
+            a.V[i] = vx; a.V[S + i] = vy; a.V[2 * S + i] = vz;
+            if (a.do_qt) a.tPart[i] = tPart;
+        }
+        if (a.do_qt && st) {
+            a.psi[(size_t)(2 * k) * S + i] = w.re;
+            a.psi[(size_t)(2 * k + 1) * S + i] = w.im;
+        }
+    }
+}
+
+hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, hipStream_t s) {
     if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_substeps, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
+    if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes, dim3((a.n + 15) / 16), dim3(256), 0, s, a, tab);
+    else hipLaunchKernelGGL(k_substeps, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

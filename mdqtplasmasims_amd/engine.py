@@ -61,24 +61,39 @@ def slab(N: int, world: int, rank: int):
     return lo.value, hi.value, S.value
 
 
-def forces_raw(R, L: float, lDeb: float, nseg: int = 0, device: int = -1):
+def forces_raw(R, L: float, lDeb: float, nseg: int = 0, device: int = -1, variant: int = 1):
     """Yukawa forces of positions R[3][N] in a periodic box L (kernel 1, stateless)."""
     R = np.ascontiguousarray(R, dtype=np.float64)
     N = R.shape[1]
     F = np.zeros((3, N))
-    check(lib().mdqt_forces_raw(N, float(L), float(lDeb), dptr(R), N, dptr(F), int(nseg), int(device)),
+    check(lib().mdqt_forces_raw(N, float(L), float(lDeb), dptr(R), N, dptr(F), int(nseg), int(device),
+                                int(variant)),
           "forces_raw")
     return F
 
 
-def potentials_raw(R, L: float, lDeb: float, nseg: int = 0, device: int = -1):
+def potentials_raw(R, L: float, lDeb: float, nseg: int = 0, device: int = -1, variant: int = 1):
     """U[i] = sum_{j != i} exp(-r/lDeb)/r inside L/2 (kernel 1 potential mode, stateless)."""
     R = np.ascontiguousarray(R, dtype=np.float64)
     N = R.shape[1]
     U = np.zeros(N)
-    check(lib().mdqt_potentials_raw(N, float(L), float(lDeb), dptr(R), N, dptr(U), int(nseg), int(device)),
+    check(lib().mdqt_potentials_raw(N, float(L), float(lDeb), dptr(R), N, dptr(U), int(nseg), int(device),
+                                    int(variant)),
           "potentials_raw")
     return U
+
+
+def comm_unique_id() -> bytes:
+    """a fresh RCCL unique id (rank 0 makes it; the launcher broadcasts it)"""
+    buf = C.create_string_buffer(128)
+    check(lib().mdqt_comm_unique_id(buf, 128), "comm_unique_id")
+    return buf.raw
+
+
+def comm_init_local(sims) -> None:
+    """join the contexts of one process into an in-process group (tests on one GPU)"""
+    arr = (C.c_void_p * len(sims))(*[s.h.value for s in sims])
+    check(lib().mdqt_comm_init_local(arr, len(sims)), "comm_init_local")
 
 
 class Simulation:
@@ -221,6 +236,9 @@ class Simulation:
     def run(self):
         check(lib().mdqt_run(self.h), "run")
 
+    def set_option(self, name: str, value: int):
+        check(lib().mdqt_set_option(self.h, name.encode(), int(value)), "set_option")
+
     # ---- streams / timing / sharding plumbing ----
     def set_stream(self, stream_handle: int | None):
         check(lib().mdqt_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None))
@@ -232,6 +250,22 @@ class Simulation:
         p = C.c_void_p(); S = C.c_int()
         check(lib().mdqt_positions_device(self.h, C.byref(p), C.byref(S)))
         return p.value, S.value
+
+    def slab_bounds(self):
+        lo, hi = C.c_int(), C.c_int()
+        check(lib().mdqt_slab_bounds(self.h, C.byref(lo), C.byref(hi)))
+        return lo.value, hi.value
+
+    def allgather_positions(self):
+        check(lib().mdqt_allgather_positions(self.h), "allgather_positions")
+
+    def allreduce_sum(self, buf):
+        buf = np.ascontiguousarray(buf, dtype=np.float64)
+        check(lib().mdqt_allreduce_sum(self.h, dptr(buf), buf.size), "allreduce_sum")
+        return buf
+
+    def comm_init(self, uid: bytes):
+        check(lib().mdqt_comm_init(self.h, uid, len(uid)), "comm_init")
 
     def enable_timing(self, on: bool = True):
         check(lib().mdqt_enable_timing(self.h, int(on)))

@@ -34,21 +34,23 @@ def rel(a, b):
 
 @pytest.mark.parametrize("case", [0, 1])
 @pytest.mark.parametrize("nseg", [1, 0, 7])
-def test_forces_match_reference_golden(eng, case, nseg):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_forces_match_reference_golden(eng, case, nseg, variant):
     from mdqtplasmasims_amd.engine import forces_raw
     g = np.load(GOLD)
     L, kappa = float(g["L"]), float(g["kappa"])
-    F = forces_raw(g[f"R{case}"], L, 1.0 / kappa, nseg=nseg)
+    F = forces_raw(g[f"R{case}"], L, 1.0 / kappa, nseg=nseg, variant=variant)
     A = g[f"A{case}"]
     assert rel(F, A) < 1e-13
     assert np.allclose(F, A, rtol=1e-11, atol=1e-12 * np.abs(A).max())
 
 
 @pytest.mark.parametrize("case", [0, 1])
-def test_potentials_match_reference_golden(eng, case):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_potentials_match_reference_golden(eng, case, variant):
     from mdqtplasmasims_amd.engine import potentials_raw
     g = np.load(GOLD)
-    U = potentials_raw(g[f"R{case}"], float(g["L"]), 1.0 / float(g["kappa"]))
+    U = potentials_raw(g[f"R{case}"], float(g["L"]), 1.0 / float(g["kappa"]), variant=variant)
     assert rel(U, g[f"U{case}"]) < 1e-13
 
 
@@ -58,9 +60,15 @@ def test_forces_match_oracle_bitwise_order(eng, orc):
     rng = np.random.default_rng(4)
     L = 12.794389
     R = rng.uniform(0, L, (3, 777))
-    F = forces_raw(R, L, 1.8257418583505538, nseg=1)
+    F = forces_raw(R, L, 1.8257418583505538, nseg=1, variant=0)
     O = orc.forces_raw(R, L, 1.8257418583505538)
     assert rel(F, O) < 1e-14
+    # boundary-straddling pairs: exercise the exact minimum-image thresholds at |dx| ~ L/2
+    R2 = R.copy()
+    R2[:, 1::2] = (R2[:, 0::2][:, :R2[:, 1::2].shape[1]] + L / 2) % L
+    F2 = forces_raw(R2, L, 1.8257418583505538, nseg=1, variant=0)
+    O2 = orc.forces_raw(R2, L, 1.8257418583505538)
+    assert rel(F2, O2) < 1e-14
 
 
 # ---------------------------------------------------------------------------------------------
@@ -192,6 +200,54 @@ def test_substeps_fusion_equals_single_substeps(eng):
     sc = c.get_state()
     for k in ("R", "V", "psi", "tPart"):
         assert np.array_equal(sa[k], sc[k]), k
+
+
+@pytest.mark.parametrize("N0,extra", [(500, {}), (3500, {}), (300, dict(Om=3.0, OmDP=2.0, reNormalizewvFns=1)),
+                                      (300, dict(fracOfSig=0.4, detuningDP=-0.5))])
+def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra):
+    """k_substeps_lanes (16 lanes per ion) performs exactly k_substeps' operations"""
+    sims = []
+    for mode in (1, 2):
+        s = eng.Simulation(N0=N0, seed=31, **extra).init()
+        s.set_option("substep_kernel", mode)
+        s.md_steps(3)
+        sims.append(s.get_state())
+    a, b = sims
+    jumped = (a["tPart"] < 3 * 0.002).sum()
+    for k in ("R", "V", "psi", "tPart"):
+        assert np.array_equal(a[k], b[k]), (k, jumped)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_local_group_bit_identical(eng, world):
+    """the sharded data path (slab layout [world][3][S], all-gather of positions, owner-computes
+    force rows, global-id RNG) run as an in-process rank group is bit-identical to world 1"""
+    from mdqtplasmasims_amd.engine import comm_init_local
+    kw = dict(N0=700, seed=9)
+    ref = eng.Simulation(**kw).init()
+    ref.md_steps(3)
+    rs = ref.get_state()
+    st = eng.Simulation(**kw).init().get_state()
+    sims = [eng.Simulation(world_size=world, rank=r, **kw) for r in range(world)]
+    for s in sims:
+        s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+    comm_init_local(sims)
+    for _ in range(3):
+        for s in sims:
+            s.allgather_positions()
+        for s in sims:
+            s.forces()
+        for s in sims:
+            s.substeps(25)
+    for s in sims:
+        lo, hi = s.slab_bounds()
+        a = s.get_state()
+        assert hi > lo
+        for k in ("R", "V"):
+            assert np.array_equal(a[k][:, lo:hi], rs[k][:, lo:hi]), k
+        for k in ("psi", "tPart"):
+            assert np.array_equal(a[k][lo:hi], rs[k][lo:hi]), k
+        assert a["t"] == rs["t"]
 
 
 # ---------------------------------------------------------------------------------------------

@@ -85,7 +85,12 @@ struct mdqt_ctx {
     LaneTab* dTab = nullptr;       // device copy (uploaded once at create)
     int substep_mode = 0;          // 0 auto, 1 thread-per-ion, 2 lane-per-state
     int force_variant = 1;         // 0 exact reference operations, 1 fast reciprocal form
-    bool f_pending = false;        // dFpart holds unreduced force partials (nseg > 1)
+    bool f_pending = false;        // dFpart holds unreduced force partials (pend_nseg > 1)
+    int pend_nseg = 1;             // partial count of the pending forces (segments or slots)
+    int scheme_opt = 0;            // force scheme: 0 auto, 1 rows (owner computes), 2 Newton-3 tiles
+    bool use_n3 = false;
+    int nslots = 0, npairs = 0, capPairs = 0;
+    int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel
     ncclComm_t comm = nullptr;     // RCCL communicator over the world_size ranks (sharded runs)
     double* dComm = nullptr;       // device staging for small all-reduces
     std::vector<mdqt_ctx*> local;  // in-process group (tests on one GPU): all-gather by D2D copies
@@ -289,11 +294,47 @@ static void choose_segments(mdqt_ctx* s) {
     if (nseg < 1) nseg = 1;
     s->seglen = N > 0 ? (N + nseg - 1) / nseg : 1;
     s->nseg = N > 0 ? (N + s->seglen - 1) / s->seglen : 1;
+    // Newton-3 tile pairs: one GPU, and the (ntiles+1) x 3 x S partial slots stay small
+    const bool n3_ok = s->p.world_size == 1 && N >= 128 && N <= 65536;
+    s->use_n3 = (s->scheme_opt == 2 && s->p.world_size == 1 && N >= 1) || (s->scheme_opt == 0 && n3_ok);
+    const int nt = (N + 63) / 64;
+    s->nslots = s->use_n3 ? nt + 1 : 0;
+    s->npairs = s->use_n3 ? nt * (nt + 1) / 2 : 0;
+}
+
+// partial-sum buffer (row segments or Newton-3 slots) and the tile-pair table
+static int ensure_aux(mdqt_ctx* s) {
+    const int need = std::max(std::max(s->nseg, s->nslots), 2);
+    if (need > s->capNseg) {
+        if (s->dFpart) HIPCHK(hipFree(s->dFpart));
+        s->dFpart = nullptr;
+        HIPCHK(hipMalloc(&s->dFpart, (size_t)s->capS * 3 * need * sizeof(double)));
+        s->capNseg = need;
+    }
+    if (s->use_n3 && s->npairs > 0) {
+        if (s->npairs > s->capPairs) {
+            if (s->dPairs) HIPCHK(hipFree(s->dPairs));
+            s->dPairs = nullptr;
+            HIPCHK(hipMalloc(&s->dPairs, (size_t)s->npairs * sizeof(int2)));
+            s->capPairs = s->npairs;
+        }
+        const int nt = s->nslots - 1;
+        std::vector<int2> h;
+        h.reserve(s->npairs);
+        for (int I = 0; I < nt; ++I)
+            for (int J = I; J < nt; ++J) h.push_back(make_int2(I, J));
+        HIPCHK(hipMemcpyAsync(s->dPairs, h.data(), h.size() * sizeof(int2), hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    return 0;
 }
 
 static void free_device(mdqt_ctx* s) {
     double** ps[] = {&s->dR, &s->dV, &s->dF, &s->dFpart, &s->dPsi, &s->dTp, &s->dScr, &s->dKde, &s->dUrow};
     for (double** q : ps) { if (*q) (void)hipFree(*q); *q = nullptr; }
+    if (s->dPairs) (void)hipFree(s->dPairs);
+    s->dPairs = nullptr;
+    s->capPairs = 0;
     s->capS = 0; s->capNseg = 0; s->kdeChunks = 0;
 }
 
@@ -305,22 +346,20 @@ static int resize(mdqt_ctx* s, int N) {
     s->N = N; s->lo = lo; s->hi = hi; s->nloc = hi - lo;
     choose_segments(s);
     const int W = s->p.world_size;
-    if (S != s->capS || s->nseg > s->capNseg) {
+    if (S != s->capS) {
         free_device(s);
         HIPCHK(hipSetDevice(s->dev));
         const size_t sz = (size_t)S * sizeof(double);
         HIPCHK(hipMalloc(&s->dR, sz * 3 * W));
         HIPCHK(hipMalloc(&s->dV, sz * 3));
         HIPCHK(hipMalloc(&s->dF, sz * 3));
-        const int nsegAlloc = s->nseg < 2 ? 2 : s->nseg;
-        HIPCHK(hipMalloc(&s->dFpart, sz * 3 * nsegAlloc));
         HIPCHK(hipMalloc(&s->dPsi, sz * 24));
         HIPCHK(hipMalloc(&s->dTp, sz));
         HIPCHK(hipMalloc(&s->dUrow, sz));
         HIPCHK(hipMalloc(&s->dScr, (64 + 3 * NBINS) * sizeof(double)));
         s->kdeChunks = 64;
         HIPCHK(hipMalloc(&s->dKde, (size_t)s->kdeChunks * 3 * NBINS * sizeof(double)));
-        s->capS = S; s->capNseg = nsegAlloc;
+        s->capS = S;
         HIPCHK(hipMemsetAsync(s->dR, 0, sz * 3 * W, s->stream));
         HIPCHK(hipMemsetAsync(s->dV, 0, sz * 3, s->stream));
         HIPCHK(hipMemsetAsync(s->dF, 0, sz * 3, s->stream));
@@ -328,6 +367,7 @@ static int resize(mdqt_ctx* s, int N) {
         HIPCHK(hipMemsetAsync(s->dTp, 0, sz, s->stream));
     }
     s->S = S;
+    if (ensure_aux(s)) return -1;
     s->Vholder.assign((size_t)NINTERVALV * 3 * (N > 0 ? N : 1), 0.);
     return 0;
 }
@@ -398,6 +438,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "decayRatioD5Halves")) return s->r;
     if (!strcmp(n, "kRat")) return s->kRat;
     if (!strcmp(n, "force_segments")) return s->nseg;
+    if (!strcmp(n, "force_scheme")) return s->use_n3 ? 2 : 1;
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
     return NAN;
@@ -604,7 +645,7 @@ static ForceArgs force_args(mdqt_ctx* s, double* out) {
 // fold pending force partials into F (consumers other than the substep kernels)
 static int settle_forces(mdqt_ctx* s) {
     if (!s->f_pending) return 0;
-    HIPCHK(launch_reduce_segments(s->dFpart, s->dF, s->nseg, s->nloc, s->S, 3, s->stream));
+    HIPCHK(launch_reduce_segments(s->dFpart, s->dF, s->pend_nseg, s->nloc, s->S, 3, s->stream));
     s->f_pending = false;
     return 0;
 }
@@ -626,11 +667,22 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
     if (s->nloc == 0) return 0;
     HIPCHK(hipSetDevice(s->dev));
     if (s->timing && mark(s, 0)) return -1;
-    if (s->nseg == 1) {
+    if (s->use_n3) {
+        N3Args a;
+        a.R = s->dR; a.P = s->dFpart; a.pairs = s->dPairs;
+        a.N = s->N; a.S = s->S; a.ntiles = s->nslots - 1; a.npairs = s->npairs;
+        ForceArgs c = force_args(s, nullptr);
+        a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
+        a.micGuard = c.micGuard;
+        HIPCHK(launch_forces_n3(a, s->force_variant, s->stream));
+        s->f_pending = true;       // slots summed by the next substep launch (or settle_forces)
+        s->pend_nseg = s->nslots;
+    } else if (s->nseg == 1) {
         HIPCHK(launch_forces(force_args(s, s->dF), s->stream));
     } else {
         HIPCHK(launch_forces(force_args(s, s->dFpart), s->stream));
         s->f_pending = true;       // summed by the next substep launch (or settle_forces)
+        s->pend_nseg = s->nseg;
     }
     if (s->timing && mark(s, 0)) return -1;
     return 0;
@@ -646,7 +698,7 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         memset(&a, 0, sizeof a);
         a.R = s->dR + (size_t)s->p.rank * 3 * s->S;
         a.V = s->dV; a.F = s->dF; a.psi = s->dPsi; a.tPart = s->dTp;
-        a.Fpart = s->dFpart; a.nseg = s->f_pending ? s->nseg : 1;
+        a.Fpart = s->dFpart; a.nseg = s->f_pending ? s->pend_nseg : 1;
         s->f_pending = false;
         a.n = s->nloc; a.S = s->S; a.gid0 = (uint64_t)s->lo;
         a.q0 = s->qidx;
@@ -700,6 +752,9 @@ static int pairs_raw(int mode, int N, double L, double lDeb, const double* R, si
     int lo, hi, S;
     if (mdqt_slab(N, 1, 0, &lo, &hi, &S)) return -1;
     mdqt_ctx tmp;                                   // only for choose_segments
+    memset(&tmp.p, 0, sizeof tmp.p);
+    tmp.p.world_size = 1;
+    tmp.scheme_opt = 1;
     tmp.N = N; tmp.p.force_segments = nseg_req;
     choose_segments(&tmp);
     const int nseg = tmp.nseg;
@@ -1053,6 +1108,14 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
 
 extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     if (!s || !name) return fail("mdqt_set_option: NULL argument");
+    if (!strcmp(name, "force_scheme")) {
+        if (value < 0 || value > 2) return fail("force_scheme must be 0 (auto), 1 (rows) or 2 (Newton-3 tiles)");
+        if (value == 2 && s->p.world_size != 1) return fail("force_scheme 2 needs world_size 1");
+        if (settle_forces(s)) return -1;
+        s->scheme_opt = value;
+        choose_segments(s);
+        return ensure_aux(s);
+    }
     if (!strcmp(name, "force_kernel")) {
         if (value < 0 || value > 1) return fail("force_kernel must be 0 (exact) or 1 (fast)");
         s->force_variant = value;

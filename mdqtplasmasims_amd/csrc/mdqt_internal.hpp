@@ -87,8 +87,21 @@ struct ForceArgs {
     int variant;        // 0 = exact (the reference's operations), 1 = fast (rsqrt/reciprocal form)
 };
 
+// Newton-3 tile-pair scheme (world_size 1, small/medium N): one wave per 64x64 tile pair
+// (I <= J), the J tile rotating through the lanes; partials go to slot J (rows of I) and slot
+// I (rows of J), the diagonal tile's two sides to slots I and ntiles.  F = canonical sum of
+// the ntiles + 1 slots (seg_sum), like the row scheme's segments.
+struct N3Args {
+    const double* R;    // [3][S] (world_size 1)
+    double* P;          // [ntiles + 1][3][S]
+    const int2* pairs;  // (I, J) of every wave
+    int N, S, ntiles, npairs;
+    double L, lDeb, Rcut, invlDeb, micT, micGuard;
+};
+
 // ---- launchers (mdqt_kernels.hip) ----
 hipError_t launch_forces(const ForceArgs& a, hipStream_t s);
+hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s);
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
                                   hipStream_t s);
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[seg][0][i]

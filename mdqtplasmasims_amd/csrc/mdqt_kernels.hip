@@ -147,6 +147,103 @@ __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restric
 
 static int seg_blocks(int nrows) { return (nrows + FT - 1) / FT; }
 
+// One pair's minimum image + Yukawa force magnitude (SpeedUp:213-224), as in k_pairs.
+// dx, dy, dz in: r_i - r_j; out: minimum-image separation.  Returns false outside 0<r<L/2.
+template <int VARIANT>
+__device__ __forceinline__ bool yukawa_ft(double& dx, double& dy, double& dz, const N3Args& a, double& ft) {
+    const double L = a.L, T = a.micT, G = a.micGuard;
+    if (fabs(dx) < G && fabs(dy) < G && fabs(dz) < G) {
+        dx = (dx >= T) ? dx - L : ((dx <= -T) ? dx + L : dx);
+        dy = (dy >= T) ? dy - L : ((dy <= -T) ? dy + L : dy);
+        dz = (dz >= T) ? dz - L : ((dz <= -T) ? dz + L : dz);
+    } else {
+        dx -= L * round(dx / L);
+        dy -= L * round(dy / L);
+        dz -= L * round(dz / L);
+    }
+    const double r2 = dx * dx + dy * dy + dz * dz;
+    if (VARIANT == 0) {
+        const double dr = sqrt(r2);
+        if (!(dr > 0 && dr < a.Rcut)) return false;
+        ft = (1. / dr + a.invlDeb) * exp(-dr / a.lDeb) / (dr * dr);
+        return true;
+    } else {
+        if (!(r2 > 0)) return false;
+        double ri = __builtin_amdgcn_rsq(r2);
+        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
+        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
+        const double dr = r2 * ri;
+        if (!(dr < a.Rcut)) return false;
+        ft = ((ri + a.invlDeb) * exp(-dr * a.invlDeb)) * (ri * ri);
+        return true;
+    }
+}
+
+__device__ __forceinline__ int gat_i(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ double gat_d(double v, int src) {
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+// Newton-3 tile pairs: wave w takes (I, J) = pairs[w]; lane l holds ion I*64+l and one ion of
+// tile J, which travels one lane per step together with its accumulated force.  Each pair of
+// the two tiles is evaluated once: f goes to i, -f to j (exact: the minimum image and r are
+// sign-symmetric, f(j,i) == -f(i,j) bit for bit).
+template <int VARIANT>
+__global__ __launch_bounds__(256) void k_pairs_n3(N3Args a) {
+    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int l = threadIdx.x & 63;
+    if (w >= a.npairs) return;                      // wave-uniform exit
+    const int2 IJ = a.pairs[w];
+    const int I = IJ.x, J = IJ.y;
+    const int S = a.S, N = a.N;
+    const double* X = a.R;
+    const double* Y = a.R + S;
+    const double* Z = a.R + 2 * S;
+    const int i = I * 64 + l;
+    const bool vi = i < N;
+    const double xi = vi ? X[i] : 0., yi = vi ? Y[i] : 0., zi = vi ? Z[i] : 0.;
+    int jx = J * 64 + l;
+    double xj = jx < N ? X[jx] : 0., yj = jx < N ? Y[jx] : 0., zj = jx < N ? Z[jx] : 0.;
+    double fxi = 0., fyi = 0., fzi = 0., fxj = 0., fyj = 0., fzj = 0.;
+    const int nxt = (l + 1) & 63;
+    const bool diag = (I == J);
+    const int nsteps = diag ? 32 : 64;
+    for (int s = 0; s < nsteps; ++s) {
+        if (diag) {                                 // diagonal: meet lane l+1 .. l+32 only
+            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
+            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
+        }
+        const bool on = vi && jx < N && (!diag || s < 31 || l < 32);
+        if (on) {
+            double dx = xi - xj, dy = yi - yj, dz = zi - zj, ft;
+            if (yukawa_ft<VARIANT>(dx, dy, dz, a, ft)) {
+                const double px = dx * ft, py = dy * ft, pz = dz * ft;
+                fxi += px; fyi += py; fzi += pz;
+                fxj -= px; fyj -= py; fzj -= pz;
+            }
+        }
+        if (!diag) {
+            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
+            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
+        }
+    }
+    const size_t slab3 = (size_t)3 * S;
+    double* Pi = a.P + (size_t)J * slab3;            // rows of I: slot J (I itself on the diagonal)
+    double* Pj = a.P + (size_t)(diag ? a.ntiles : I) * slab3;
+    if (i < S) { Pi[i] = fxi; Pi[S + i] = fyi; Pi[2 * S + i] = fzi; }
+    if (jx < S) { Pj[jx] = fxj; Pj[S + jx] = fyj; Pj[2 * S + jx] = fzj; }
+}
+
+hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s) {
+    if (a.npairs <= 0) return hipSuccess;
+    dim3 grid((a.npairs + 3) / 4);
+    if (variant == 1) hipLaunchKernelGGL(k_pairs_n3<1>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_pairs_n3<0>, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_forces(const ForceArgs& a, hipStream_t s) {
     if (a.nrows <= 0) return hipSuccess;
     dim3 grid(seg_blocks(a.nrows), a.nseg);

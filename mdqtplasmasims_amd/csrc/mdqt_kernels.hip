@@ -549,6 +549,27 @@ __device__ __forceinline__ double gat(double v, int src) {
 }
 __device__ __forceinline__ cxd gatc(cxd v, int src) { return {gat(v.re, src), gat(v.im, src)}; }
 
+// DPP moves inside a 16-lane row (one ion): row_shl:n (lane l reads lane l+n), row_shr:n
+// (lane l reads lane l-n), row_newbcast:n (every lane reads lane n of its row).  VALU-latency
+// cross-lane moves for the fixed-pattern sums; exact.
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+#define SHL(n) (0x100 + (n))
+#define SHR(n) (0x110 + (n))
+#define BCAST(n) (0x150 + (n))
+
+// ((T2 + T3) + T4) + T5 of the ion's lanes 2..5, in every lane of the row
+__device__ __forceinline__ double row_sum_p(double T) {
+    double a = T + dpp<SHL(1)>(T);
+    a = a + dpp<SHL(2)>(T);
+    a = a + dpp<SHL(3)>(T);
+    return dpp<BCAST(2)>(a);
+}
+
 __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const LaneTab* __restrict__ tab) {
     const int lane = threadIdx.x & 63;
     const int k = lane & 15;                          // state index (valid when < 12)
@@ -615,7 +636,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
         const double velQuant = vx * qc.pv2q;
         tPart += qc.dtQ;
         const double Tk = (w.re * dPk) * w.re + (w.im * dPk) * w.im;
-        const double dp = qc.h * (((gat(Tk, g0 + 2) + gat(Tk, g0 + 3)) + gat(Tk, g0 + 4)) + gat(Tk, g0 + 5));
+        const double dp = qc.h * row_sum_p(Tk);
         double u1, u2;
         philox_pair(qc, gid, a.q0 + (uint64_t)s, 0, u1, u2);
         const cxd wA = gatc(w, srcA), wB = gatc(w, srcB);
@@ -623,9 +644,12 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
         if (u1 > dp) {
             // optical kick from the pre-step density matrix (:490-503)
             const double kA = rho_im(w, wA) * gA, kB = rho_im(w, wB) * gB;
-            const double sum1 = ((gat(kA, g0 + 1) + gat(kA, g0 + 0)) - gat(kB, g0 + 1)) - gat(kB, g0 + 0);
-            const double sum2 = ((((((gat(kB, g0 + 8) + gat(kB, g0 + 9)) + gat(kA, g0 + 10)) + gat(kA, g0 + 11)) -
-                                  gat(kA, g0 + 6)) - gat(kA, g0 + 7)) - gat(kA, g0 + 8)) - gat(kA, g0 + 9);
+            // ((p23 g0 + p14 g2) - p25 g4) - p16 g5, evaluated at lane 0 (terms of lanes 0, 1)
+            const double sum1 = dpp<BCAST(0)>(((dpp<SHL(1)>(kA) + kA) - dpp<SHL(1)>(kB)) - kB);
+            // ((((((p96 g8 + p105 g11) + p114 g14) + p123 g17) - p76 g6) - p85 g9) - p94 g12) - p103 g15
+            // evaluated at lane 8 (terms of lanes 6..11)
+            const double sum2 = dpp<BCAST(8)>(((((((kB + dpp<SHL(1)>(kB)) + dpp<SHL(2)>(kA)) + dpp<SHL(3)>(kA)) -
+                                                 dpp<SHR(2)>(kA)) - dpp<SHR(1)>(kA)) - kA) - dpp<SHL(1)>(kA));
             kick = qc.kickS * sum1 * qc.dtQ * qc.gamToE + qc.kickD * sum2 * qc.dtQ * qc.gamToE;
             // this lane's row of M = I - i h H (:506-526)
             const double vq = velQuant + eD;
@@ -650,7 +674,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
                 double dpy = dp;
                 if (stg > 0) {
                     const double Ty = (yv.re * dPk) * yv.re + (yv.im * dPk) * yv.im;
-                    dpy = qc.h * (((gat(Ty, g0 + 2) + gat(Ty, g0 + 3)) + gat(Ty, g0 + 4)) + gat(Ty, g0 + 5));
+                    dpy = qc.h * row_sum_p(Ty);
                     yA = gatc(yv, srcA);
                     yB = gatc(yv, srcB);
                 }
@@ -678,7 +702,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
         } else {                                      // quantum jump (:573-703)
             tPart = 0;
             const double nk = w.re * w.re + w.im * w.im;
-            const double n3 = gat(nk, g0 + 2), n4 = gat(nk, g0 + 3), n5 = gat(nk, g0 + 4), n6 = gat(nk, g0 + 5);
+            const double n3 = dpp<BCAST(2)>(nk), n4 = dpp<BCAST(3)>(nk), n5 = dpp<BCAST(4)>(nk), n6 = dpp<BCAST(5)>(nk);
             const double tot = n3 + n4 + n5 + n6;
             const double prob3 = n3 / tot, prob4 = n4 / tot, prob5 = n5 / tot;
             const double rand2 = u2;

@@ -37,6 +37,7 @@ CONFIGS = {
     "c2": (dict(N0=3500), 1, "C2: N0=3500 full MDQT, detuning=-1, Om=1, density=2, fp64"),
     "c1": (dict(N0=500, Ge=0.1), 0, "C1: N0=500 Yukawa OCP MD-only, Ge=0.1"),
     "c3": (dict(N0=100000, Ge=1.0 / 12), 0, "C3: N0=100000 MD-only, kappa=0.5"),
+    "c4": (dict(N0=1000000, Ge=1.0 / 12), 0, "C4: N0=1000000 MD-only, kappa=0.5"),
     "c5": (dict(N0=250000, detuningDP=1.0), 1, "C5: N0=250000 full MDQT, detuningDP=+1"),
 }
 
@@ -49,16 +50,18 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--sharded-config", default="c5", choices=["none", "c3", "c5", "c4"])
+    ap.add_argument("--sharded-steps", type=int, default=3)
     return ap.parse_args()
 
 
-def cpu_baseline(params, qt, seconds):
+def cpu_baseline(params, qt, seconds, seed, job):
     """The oracle (CPU restatement, race-free OpenMP) on a bounded sample of the same workload."""
     from oracle import oracle as O
     if not os.path.exists(O.LIB_PATH):
         O.build()
     threads = max(1, min(16, os.cpu_count() or 1))
-    o = O.OracleSim(rng_mode=1, nthreads=threads, qt_enabled=qt, **params).init()
+    o = O.OracleSim(rng_mode=1, nthreads=threads, qt_enabled=qt, seed=seed, job=job, **params).init()
     ratio = int(o.const("plasmaToQuantumTimestepRatio"))
     o.md_steps(1)                                  # warm
     n, t0 = 0, time.perf_counter()
@@ -163,12 +166,54 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(params, qt, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(params, qt, args.cpu_seconds, 12345 + job, job)
+    sim.close()
+    # secondary line item: one large system sharded over all ranks (RCCL all-gather per MD step)
+    if args.sharded_config != "none":
+        sh = sharded_run(args.sharded_config, args.sharded_steps, rank, world, local, dist, barrier)
+        if rank == 0:
+            out["sharded"] = sh
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def sharded_run(cfg, steps, rank, world, local, dist, barrier):
+    """C5 (or C3/C4) as ONE system whose ions are sharded over the world: strong scaling."""
+    import torch
+    import mdqtplasmasims_amd as M
+    from mdqtplasmasims_amd.engine import comm_unique_id
+    params, qt, desc = CONFIGS[cfg]
+    sim = M.Simulation(device=local, world_size=world, rank=rank, seed=12346, job=1, qt_enabled=qt, **params)
+    if world > 1:
+        obj = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        sim.comm_init(obj[0])
+    t0 = time.perf_counter()
+    sim.init()                                     # collective: Epot0 over all slabs
+    t_init = time.perf_counter() - t0
+    ratio = int(sim.const("plasmaToQuantumTimestepRatio"))
+    sim.md_steps(1)
+    barrier()
+    t0 = time.perf_counter()
+    sim.md_steps(steps)
+    sim.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el = float(tt[0])
+    N = sim.N
     sim.close()
+    unit_steps = ratio if qt else 1
+    return {"workload": desc + ", one system sharded over all ranks (RCCL position all-gather)",
+            "N": N, "n_gpus": world, "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
+            "value": N * unit_steps * steps / el,
+            "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
+            "scaling": "strong", "init_s": t_init}
 
 
 if __name__ == "__main__":

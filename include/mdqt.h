@@ -50,9 +50,11 @@ typedef struct mdqt_params {
     int reNormalizewvFns; /* SpeedUp:74                                                       */
     /* ---- extensions ---- */
     int qt_enabled;       /* 1 = MDQT (reference); 0 = MD-only (qstep body skipped, t advances) */
-    int rng_mode;         /* 1 = Philox4x32-10 keyed (seed, job) x (global ion, qstep) — the
-                           * only mode the device path implements this round; 0 (drand48 in
-                           * reference order) is rejected with an error                         */
+    int rng_mode;         /* 1 = Philox4x32-10 keyed (seed, job) x (global ion, qstep): fast,
+                           *     reproducible, partition-invariant (default);
+                           * 0 = the reference's own drand48 stream in its consumption order
+                           *     (SpeedUp:486, :575-687; one stream, world_size 1): trajectory
+                           *     parity with the 1-thread reference, one launch per substep   */
     uint32_t seed;        /* srand48 seed for init (reference: time(NULL)+job, SpeedUp:1219)   */
     uint32_t job;         /* SpeedUp:1145 argv[1]                                               */
     int device;           /* HIP device ordinal (-1 = current device)                           */
@@ -82,6 +84,8 @@ double      mdqt_get_time(const mdqt_ctx* c);
 int         mdqt_set_time(mdqt_ctx* c, double t);
 uint64_t    mdqt_get_qstep_index(const mdqt_ctx* c);
 int         mdqt_set_qstep_index(mdqt_ctx* c, uint64_t q);
+/* rng_mode 0: the 48-bit drand48 state X after the draws consumed so far (glibc layout) */
+int         mdqt_get_drand48_state(mdqt_ctx* c, uint64_t* x);
 int         mdqt_get_counters(const mdqt_ctx* c, int* c0, unsigned* counter, double* Epot, double* Epot0);
 /* Whole-system state (all N ions; with world_size > 1 only this rank's slab of V/F/psi/tPart
  * is meaningful, R is the full gathered array). NULL pointers are skipped. */

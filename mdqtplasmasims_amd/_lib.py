@@ -44,6 +44,7 @@ SIGNATURES = [
     ("mdqt_set_time", C.c_int, [C.c_void_p, C.c_double]),
     ("mdqt_get_qstep_index", C.c_uint64, [C.c_void_p]),
     ("mdqt_set_qstep_index", C.c_int, [C.c_void_p, C.c_uint64]),
+    ("mdqt_get_drand48_state", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("mdqt_get_counters", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint), _dp, _dp]),
     ("mdqt_set_state", C.c_int, [C.c_void_p, C.c_int, _dp, _dp, C.c_size_t, _dp, _dp, C.c_double]),
     ("mdqt_get_state", C.c_int, [C.c_void_p, _dp, _dp, _dp, C.c_size_t, _dp, _dp, _dp]),

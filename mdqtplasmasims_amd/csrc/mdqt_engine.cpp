@@ -91,6 +91,9 @@ struct mdqt_ctx {
     bool use_n3 = false;
     int nslots = 0, npairs = 0, capPairs = 0;
     int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel
+    // rng_mode 0: the reference's drand48 stream, consumed in ion order on the device
+    unsigned long long* dX48 = nullptr;   // [1] stream state + [48] jA + [48] jC
+    double* dU = nullptr;                 // [5][S] uniforms of the current substep
     ncclComm_t comm = nullptr;     // RCCL communicator over the world_size ranks (sharded runs)
     double* dComm = nullptr;       // device staging for small all-reduces
     std::vector<mdqt_ctx*> local;  // in-process group (tests on one GPU): all-gather by D2D copies
@@ -330,7 +333,7 @@ static int ensure_aux(mdqt_ctx* s) {
 }
 
 static void free_device(mdqt_ctx* s) {
-    double** ps[] = {&s->dR, &s->dV, &s->dF, &s->dFpart, &s->dPsi, &s->dTp, &s->dScr, &s->dKde, &s->dUrow};
+    double** ps[] = {&s->dR, &s->dV, &s->dF, &s->dFpart, &s->dPsi, &s->dTp, &s->dScr, &s->dKde, &s->dUrow, &s->dU};
     for (double** q : ps) { if (*q) (void)hipFree(*q); *q = nullptr; }
     if (s->dPairs) (void)hipFree(s->dPairs);
     s->dPairs = nullptr;
@@ -356,6 +359,7 @@ static int resize(mdqt_ctx* s, int N) {
         HIPCHK(hipMalloc(&s->dPsi, sz * 24));
         HIPCHK(hipMalloc(&s->dTp, sz));
         HIPCHK(hipMalloc(&s->dUrow, sz));
+        if (s->p.rng_mode == 0) HIPCHK(hipMalloc(&s->dU, sz * 5));
         HIPCHK(hipMalloc(&s->dScr, (64 + 3 * NBINS) * sizeof(double)));
         s->kdeChunks = 64;
         HIPCHK(hipMalloc(&s->dKde, (size_t)s->kdeChunks * 3 * NBINS * sizeof(double)));
@@ -375,8 +379,10 @@ static int resize(mdqt_ctx* s, int N) {
 extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
     if (!p || !out) return fail("mdqt_create: NULL argument");
     *out = nullptr;
-    if (p->rng_mode != 1)
-        return fail("rng_mode %d not implemented on the device path (only 1 = Philox)", p->rng_mode);
+    if (p->rng_mode != 0 && p->rng_mode != 1)
+        return fail("rng_mode must be 0 (drand48, reference order) or 1 (Philox)");
+    if (p->rng_mode == 0 && p->world_size != 1)
+        return fail("rng_mode 0 (one sequential drand48 stream) needs world_size 1");
     if (p->world_size < 1 || p->rank < 0 || p->rank >= p->world_size) return fail("bad world_size/rank");
     if (p->N0 < 1) return fail("N0 must be >= 1");
     if (p->sampleFreq < 1) return fail("sampleFreq must be >= 1");
@@ -399,6 +405,21 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
     s->stream = s->own;
     if (hipMalloc(&s->dTab, sizeof(LaneTab)) != hipSuccess) { mdqt_destroy(s); return fail("hipMalloc lane table"); }
     build_constants(s);
+    if (s->p.rng_mode == 0) {
+        unsigned long long h[97];
+        h[0] = srand48_state(s->p.seed);
+        unsigned long long A = 0x5DEECE66Dull, Cc = 0xBull;
+        for (int b = 0; b < 48; ++b) {            // 2^b steps of X' = A X + C (mod 2^48)
+            h[1 + b] = A; h[49 + b] = Cc;
+            Cc = (A * Cc + Cc) & 0xFFFFFFFFFFFFull;
+            A = (A * A) & 0xFFFFFFFFFFFFull;
+        }
+        if (hipMalloc(&s->dX48, sizeof h) != hipSuccess ||
+            hipMemcpy(s->dX48, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
+            mdqt_destroy(s);
+            return fail("drand48 state upload failed");
+        }
+    }
     if (hipMemcpy(s->dTab, &s->tab, sizeof(LaneTab), hipMemcpyHostToDevice) != hipSuccess) {
         mdqt_destroy(s);
         return fail("upload of the lane table failed");
@@ -419,6 +440,7 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     free_device(s);
     if (s->dTab) (void)hipFree(s->dTab);
     if (s->dComm) (void)hipFree(s->dComm);
+    if (s->dX48) (void)hipFree(s->dX48);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     for (auto& pool : s->evpool)
         for (hipEvent_t ev : pool) (void)hipEventDestroy(ev);
@@ -601,6 +623,10 @@ extern "C" int mdqt_init(mdqt_ctx* s) {
     for (int i = 0; i < N; ++i) { R[i] = X[i]; R[(size_t)N + i] = Y[i]; R[(size_t)2 * N + i] = Z[i]; }
     if (resize(s, N)) return -1;
     if (upload(s, R.data(), V.data(), N, psi.data(), tp.data())) return -1;
+    if (s->dX48) {                                   // the qstep draws continue this stream
+        unsigned long long x = s->x48;
+        HIPCHK(hipMemcpy(s->dX48, &x, sizeof x, hipMemcpyHostToDevice));
+    }
     double e;
     if (mdqt_epotential(s, &e)) return -1;                                           // :345-347
     s->Epot0 = s->Epot;
@@ -692,8 +718,9 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
 static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int advance_t) {
     HIPCHK(hipSetDevice(s->dev));
     const int do_qt = do_qt_flag && s->p.qt_enabled;
+    const bool d48 = do_qt && s->p.rng_mode == 0;
     while (n > 0) {
-        const int m = n < MAXSUB ? n : MAXSUB;
+        const int m = d48 ? 1 : (n < MAXSUB ? n : MAXSUB);   // drand48: the stream orders ions per substep
         SubstepArgs a;
         memset(&a, 0, sizeof a);
         a.R = s->dR + (size_t)s->p.rank * 3 * s->S;
@@ -710,6 +737,14 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             a.t[k] = t;
             a.expDet[k] = expDetuning_of(&s->p, t);
             if (advance_t) t += s->dtQ;                    // qstep: t += dtQuant (:716)
+        }
+        if (d48 && s->nloc > 0) {
+            D48Args r;
+            r.psi = s->dPsi; r.n = s->nloc; r.S = s->S;
+            r.state = s->dX48; r.jA = s->dX48 + 1; r.jC = s->dX48 + 49;
+            r.U = s->dU; r.qc = s->qc;
+            HIPCHK(launch_d48_resolve(r, s->stream));
+            a.U = s->dU;
         }
         if (s->timing && mark(s, 1)) return -1;
         HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->stream));
@@ -1258,5 +1293,16 @@ extern "C" int mdqt_slab_bounds(const mdqt_ctx* s, int* lo, int* hi) {
 
 extern "C" int mdqt_set_counters(mdqt_ctx* s, int c0, unsigned counter, double Epot, double Epot0) {
     s->c0 = c0; s->counter = counter; s->Epot = Epot; s->Epot0 = Epot0;
+    return 0;
+}
+
+extern "C" int mdqt_get_drand48_state(mdqt_ctx* s, uint64_t* x) {
+    if (!s || !x) return fail("mdqt_get_drand48_state: bad arguments");
+    if (!s->dX48) { *x = s->x48; return 0; }
+    unsigned long long h = 0;
+    HIPCHK(hipSetDevice(s->dev));
+    HIPCHK(hipMemcpyAsync(&h, s->dX48, sizeof h, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    *x = h;
     return 0;
 }

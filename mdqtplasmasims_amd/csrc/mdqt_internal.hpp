@@ -68,6 +68,8 @@ struct SubstepArgs {
     uint64_t gid0;      // global id of local ion 0
     uint64_t q0;        // qstep index of the first substep
     int nsub, do_step, do_qt;
+    const double* U;    // rng_mode 0 (drand48 reference order): uniforms [5][S] of this substep
+                        // (nsub == 1), from k_d48_resolve; nullptr = Philox stream
     double L;
     double t[MAXSUB];       // global time at each substep (t before qstep advances it)
     double expDet[MAXSUB];  // expDetuning(t) (:447)
@@ -98,6 +100,20 @@ struct N3Args {
     int N, S, ntiles, npairs;
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
 };
+
+// drand48 in the reference's order (SpeedUp:486, :575-687: ions in index order, 1 draw per
+// ion, 4-5 for a quantum jump): one workgroup assigns every ion its uniforms from the single
+// stream, by LCG jump-ahead from the stream state, restarting after each (rare) jump.
+struct D48Args {
+    const double* psi;         // [24][S]
+    int n, S;
+    unsigned long long* state; // device: drand48 X before this substep's first draw; advanced
+    const unsigned long long* jA;   // [48] multiplier of 2^b steps
+    const unsigned long long* jC;   // [48] increment of 2^b steps
+    double* U;                 // out: [5][S]
+    QTConst qc;
+};
+hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s);
 
 // ---- launchers (mdqt_kernels.hip) ----
 hipError_t launch_forces(const ForceArgs& a, hipStream_t s);

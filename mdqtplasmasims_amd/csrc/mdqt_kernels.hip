@@ -304,6 +304,116 @@ __device__ __forceinline__ void philox_pair(const QTConst& qc, uint64_t ion, uin
     ub = u53(o[2], o[3]);
 }
 
+// uniforms 2p, 2p+1 of local ion i at substep (gid, q): the precomputed drand48 reference-order
+// values when U is given (rng_mode 0), else the Philox stream
+__device__ __forceinline__ void draw_pair(const QTConst& qc, const double* U, int S, int i, uint64_t gid,
+                                          uint64_t q, int p, double& ua, double& ub) {
+    if (U) {
+        ua = U[(size_t)(2 * p) * S + i];
+        ub = (2 * p + 1 < 5) ? U[(size_t)(2 * p + 1) * S + i] : 0.;
+    } else {
+        philox_pair(qc, gid, q, p, ua, ub);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// drand48 in the reference's consumption order (SpeedUp:486, :575-687).  X' = a X + c mod 2^48;
+// 2^b steps compose to (jA[b], jC[b]).  One workgroup walks the ions in chunks of 1024: every
+// ion of the chunk takes its u1 at (index + draws already shifted by earlier jumps); the first
+// ion that jumps (u1 <= dp) takes 4 or 5 draws, which shifts everybody after it, and the walk
+// restarts behind it.  Jumps are rare (dp ~ 1e-3), so a substep costs ~N/1024 + #jumps passes.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long lcg_adv(unsigned long long x, unsigned long long k,
+                                                      const unsigned long long* jA,
+                                                      const unsigned long long* jC) {
+    for (int b = 0; k; ++b, k >>= 1)
+        if (k & 1ull) x = (jA[b] * x + jC[b]) & 0xFFFFFFFFFFFFull;
+    return x;
+}
+
+__global__ __launch_bounds__(1024) void k_d48_resolve(D48Args a) {
+    __shared__ unsigned long long sA[48], sC[48];
+    __shared__ int s_first[16];
+    __shared__ int s_min, s_extra;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid < 48) { sA[tid] = a.jA[tid]; sC[tid] = a.jC[tid]; }
+    __syncthreads();
+    const QTConst& qc = a.qc;
+    const int S = a.S, n = a.n;
+    const unsigned long long X0 = *a.state;
+    unsigned long long off = 0;
+    int pos = 0;
+    while (pos < n) {
+        const int i = pos + tid;
+        bool jmp = false;
+        if (i < n) {
+            const unsigned long long x = lcg_adv(X0, (unsigned long long)i + off + 1, sA, sC);
+            const double u1 = ldexp((double)x, -48);
+            double T[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double re = a.psi[(size_t)(2 * (q + 2)) * S + i], im = a.psi[(size_t)(2 * (q + 2) + 1) * S + i];
+                T[q] = (re * qc.dP[q]) * re + (im * qc.dP[q]) * im;
+            }
+            const double dp = qc.h * (((T[0] + T[1]) + T[2]) + T[3]);     // exactly dp_of / row_sum_p
+            jmp = !(u1 > dp);
+            a.U[i] = u1;
+        }
+        const unsigned long long b = __ballot(jmp);
+        if (lane == 0) s_first[wv] = b ? wv * 64 + __ffsll((long long)b) - 1 : 0x7fffffff;
+        __syncthreads();
+        if (tid == 0) {
+            int m = 0x7fffffff;
+            for (int w = 0; w < 16; ++w) m = min(m, s_first[w]);
+            s_min = m;
+            s_extra = 0;
+        }
+        __syncthreads();
+        const int m = s_min;
+        if (m == 0x7fffffff) {
+            pos += 1024;
+            __syncthreads();
+            continue;
+        }
+        if (tid == m) {                               // the jumping ion: draws 2..4 (or 2..5)
+            const unsigned long long k0 = (unsigned long long)i + off;
+            const double rand2 = ldexp((double)lcg_adv(X0, k0 + 2, sA, sC), -48);
+            const double randDOrS = ldexp((double)lcg_adv(X0, k0 + 3, sA, sC), -48);
+            const double randDir = ldexp((double)lcg_adv(X0, k0 + 4, sA, sC), -48);
+            double nrm[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double re = a.psi[(size_t)(2 * (q + 2)) * S + i], im = a.psi[(size_t)(2 * (q + 2) + 1) * S + i];
+                nrm[q] = re * re + im * im;
+            }
+            const double tot = nrm[0] + nrm[1] + nrm[2] + nrm[3];
+            const double prob3 = nrm[0] / tot, prob4 = nrm[1] / tot, prob5 = nrm[2] / tot;
+            const bool sDecay = !(randDOrS < qc.pD);
+            bool need3;
+            if (rand2 < prob3) need3 = !sDecay;
+            else if (rand2 < prob3 + prob4) need3 = true;
+            else if (rand2 < prob3 + prob4 + prob5) need3 = true;
+            else need3 = !sDecay;
+            const double rand3 = need3 ? ldexp((double)lcg_adv(X0, k0 + 5, sA, sC), -48) : 0.;
+            a.U[(size_t)S + i] = rand2;
+            a.U[(size_t)2 * S + i] = randDOrS;
+            a.U[(size_t)3 * S + i] = randDir;
+            a.U[(size_t)4 * S + i] = rand3;
+            s_extra = need3 ? 4 : 3;
+        }
+        __syncthreads();
+        off += (unsigned long long)s_extra;
+        pos += m + 1;
+        __syncthreads();
+    }
+    if (tid == 0) *a.state = lcg_adv(X0, (unsigned long long)n + off, sA, sC);
+}
+
+hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_d48_resolve, dim3(1), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------
 // Kernel 2: fused integrator + quantum-trajectory substeps, one thread per ion, the whole
 // state (R, V, F, psi, tPart) held in registers across the nsub substeps of one launch
@@ -352,12 +462,13 @@ __device__ __forceinline__ double rho_im(cxd a, cxd b) {   // Im(a * conj(b)), S
 
 // One ion through qstep() (SpeedUp:478-712).  Returns the velocity kick.
 __device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double vx,
-                                            double& tPart, cxd* w, uint64_t gid, uint64_t q) {
+                                            double& tPart, cxd* w, uint64_t gid, uint64_t q,
+                                            const double* U, int S, int i) {
     const double velQuant = vx * qc.pv2q;                                  // :481-482
     tPart += qc.dtQ;                                                        // :483
     const double dp = dp_of(qc, w);                                         // :484-485
     double u1, u2;
-    philox_pair(qc, gid, q, 0, u1, u2);                                     // :486
+    draw_pair(qc, U, S, i, gid, q, 0, u1, u2);                              // :486
     double kick;
     if (u1 > dp) {                                                          // :487
         const double p23 = rho_im(w[1], w[2]), p14 = rho_im(w[0], w[3]);
@@ -432,8 +543,8 @@ __device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double
         const double tot = n3 + n4 + n5 + n6;
         const double prob3 = n3 / tot, prob4 = n4 / tot, prob5 = n5 / tot;
         double randDOrS, randDir, rand3, dummy;
-        philox_pair(qc, gid, q, 1, randDOrS, randDir);
-        philox_pair(qc, gid, q, 2, rand3, dummy);
+        draw_pair(qc, U, S, i, gid, q, 1, randDOrS, randDir);
+        draw_pair(qc, U, S, i, gid, q, 2, rand3, dummy);
         (void)dummy;
         const bool sDecay = !(randDOrS < qc.pD);
         if (!sDecay) kick = (randDir < 0.5) ? qc.vKickDP : -qc.vKickDP;
@@ -518,7 +629,7 @@ __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
             }
         }
         if (a.do_qt) {
-            const double kick = qstep_ion(a.qc, a.expDet[s], vx, tPart, w, gid, a.q0 + (uint64_t)s);
+            const double kick = qstep_ion(a.qc, a.expDet[s], vx, tPart, w, gid, a.q0 + (uint64_t)s, a.U, S, i);
             vx = vx + kick;                                      // :705
         }
     }
@@ -638,7 +749,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
         const double Tk = (w.re * dPk) * w.re + (w.im * dPk) * w.im;
         const double dp = qc.h * row_sum_p(Tk);
         double u1, u2;
-        philox_pair(qc, gid, a.q0 + (uint64_t)s, 0, u1, u2);
+        draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 0, u1, u2);
         const cxd wA = gatc(w, srcA), wB = gatc(w, srcB);
         double kick;
         if (u1 > dp) {
@@ -707,8 +818,8 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
             const double prob3 = n3 / tot, prob4 = n4 / tot, prob5 = n5 / tot;
             const double rand2 = u2;
             double randDOrS, randDir, rand3, dummy;
-            philox_pair(qc, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
-            philox_pair(qc, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
+            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
+            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
             (void)dummy;
             const bool sDecay = !(randDOrS < qc.pD);
             if (!sDecay) kick = (randDir < 0.5) ? qc.vKickDP : -qc.vKickDP;

@@ -147,6 +147,12 @@ class Simulation:
     def qstep_index(self, q: int):
         check(lib().mdqt_set_qstep_index(self.h, int(q)))
 
+    @property
+    def drand48_state(self) -> int:
+        x = C.c_uint64()
+        check(lib().mdqt_get_drand48_state(self.h, C.byref(x)))
+        return x.value
+
     def counters(self):
         c0 = C.c_int(); cnt = C.c_uint(); e = C.c_double(); e0 = C.c_double()
         check(lib().mdqt_get_counters(self.h, C.byref(c0), C.byref(cnt), C.byref(e), C.byref(e0)))

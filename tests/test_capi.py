@@ -101,10 +101,13 @@ def test_create_fails_loudly_without_gpu(L):
         Simulation(N0=100)
 
 
-def test_drand48_tape_mode_is_rejected_not_faked(L):
+def test_bad_rng_configurations_are_rejected(L):
     from mdqtplasmasims_amd import MdqtError, Simulation
-    with pytest.raises(MdqtError):
-        Simulation(N0=100, rng_mode=0)
+    with pytest.raises(MdqtError, match="rng_mode must be"):
+        Simulation(N0=100, rng_mode=5)
+    # one sequential drand48 stream cannot be sharded
+    with pytest.raises(MdqtError, match="needs world_size 1"):
+        Simulation(N0=100, rng_mode=0, world_size=2, rank=0)
 
 
 def test_cli_usage(L):

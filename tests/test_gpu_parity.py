@@ -239,6 +239,24 @@ def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra):
         assert np.array_equal(a[k], b[k]), (k, jumped)
 
 
+@pytest.mark.parametrize("N0,extra", [(300, {}), (500, dict(Om=3.0, OmDP=2.0)), (3500, {})])
+def test_drand48_reference_order_matches_oracle(eng, orc, N0, extra):
+    """rng_mode 0: the reference's own drand48 stream consumed in its order (1 draw per ion,
+    4-5 per quantum jump) — same jumps, same stream position, same trajectory as the oracle's
+    reference-order restatement"""
+    kw = dict(N0=N0, seed=12346, rng_mode=0, **extra)
+    s = eng.Simulation(**kw).init()
+    o = orc.OracleSim(**kw).init()
+    assert s.drand48_state == orc.lib().orc_get_drand48_state(o.h)
+    s.md_steps(4); o.md_steps(4)
+    a, b = s.get_state(), o.get_state()
+    assert s.drand48_state == orc.lib().orc_get_drand48_state(o.h)    # same number of draws
+    assert np.array_equal(a["tPart"] == 0, b["tPart"] == 0) or np.array_equal(a["tPart"] < 1e-3, b["tPart"] < 1e-3)
+    assert np.abs(a["psi"] - b["psi"]).max() < 1e-9
+    assert np.abs(a["V"] - b["V"]).max() < 1e-10
+    assert np.abs(a["R"] - b["R"]).max() < 1e-10
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_local_group_bit_identical(eng, world):
     """the sharded data path (slab layout [world][3][S], all-gather of positions, owner-computes

@@ -1256,8 +1256,10 @@ extern "C" int mdqt_allgather_positions(mdqt_ctx* s) {
         HIPCHK(hipStreamSynchronize(s->stream));
         for (mdqt_ctx* q : s->local) {
             if (q == s) continue;
-            HIPCHK(hipMemcpyPeer(q->dR + (size_t)s->p.rank * cnt, q->dev, s->dR + (size_t)s->p.rank * cnt,
-                                 s->dev, cnt * sizeof(double)));
+            // on the PEER's stream: ordered before the peer's next force launch (a plain
+            // hipMemcpyPeer is asynchronous for device-to-device copies and races with it)
+            HIPCHK(hipMemcpyPeerAsync(q->dR + (size_t)s->p.rank * cnt, q->dev, s->dR + (size_t)s->p.rank * cnt,
+                                      s->dev, cnt * sizeof(double), q->stream));
         }
         return 0;
     }

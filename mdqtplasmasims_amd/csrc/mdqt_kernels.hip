@@ -31,6 +31,31 @@ __device__ __forceinline__ const double* pos_base(const double* Rall, int g, int
 // ------------------------------------------------------------------------------------------
 constexpr int FT = 256;   // threads per block = rows per block = j tile
 
+// e^x for the fast pair variant.  x = -r/lDeb lies in [-L/(2 lDeb), 0] (no overflow, no
+// subnormal results for any box the reference runs), so the libm special-case paths are not
+// needed: Cody-Waite reduction x = n ln2 + r, |r| <= ln2/2, then the degree-13 Taylor
+// polynomial (truncation < 5e-18 relative) in FMA Horner form and an exponent shift.  ~1 ulp.
+__device__ __forceinline__ double exp_neg(double x) {
+    const double n = __builtin_rint(x * 1.4426950408889634);
+    double r = fma(-n, 0x1.62e42fefa39efp-1, x);
+    r = fma(-n, 0x1.abc9e3b39803fp-56, r);
+    double p = 1.6059043836821613e-10;               // 1/13!
+    p = fma(p, r, 2.08767569878681e-09);             // 1/12!
+    p = fma(p, r, 2.505210838544172e-08);            // 1/11!
+    p = fma(p, r, 2.755731922398589e-07);            // 1/10!
+    p = fma(p, r, 2.7557319223985893e-06);           // 1/9!
+    p = fma(p, r, 2.48015873015873e-05);             // 1/8!
+    p = fma(p, r, 0.0001984126984126984);            // 1/7!
+    p = fma(p, r, 0.001388888888888889);             // 1/6!
+    p = fma(p, r, 0.008333333333333333);             // 1/5!
+    p = fma(p, r, 0.041666666666666664);             // 1/4!
+    p = fma(p, r, 0.16666666666666666);              // 1/3!
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)n);
+}
+
 template <int MODE, int VARIANT>   // MODE 0: force, 1: potential; VARIANT 0: exact, 1: fast
 __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
     __shared__ double sx[FT], sy[FT], sz[FT];
@@ -75,8 +100,8 @@ __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
                     dy -= L * round(dy / L);
                     dz -= L * round(dz / L);
                 }
-                const double r2 = dx * dx + dy * dy + dz * dz;
                 if (VARIANT == 0) {
+                    const double r2 = dx * dx + dy * dy + dz * dz;
                     const double dr = sqrt(r2);            // :221
                     if (dr > 0 && dr < Rcut) {             // :222
                         if (MODE == 0) {
@@ -89,22 +114,24 @@ __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
                         }
                     }
                 } else {
-                    // same law in reciprocal form: 1/r from a refined v_rsq_f64, r = r2/r
-                    // (a few ulp per pair; the force gate is 1e-13 relative)
+                    // same law in reciprocal form: 1/r from a refined v_rsq_f64, r = r2/r,
+                    // exp_neg, FMA contraction (a few ulp per pair; force gate 1e-13 relative)
+                    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
                     if (r2 > 0) {
                         double ri = __builtin_amdgcn_rsq(r2);
-                        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
-                        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
+                        const double hr = 0.5 * r2;
+                        ri = ri * fma(-hr * ri, ri, 1.5);
+                        ri = ri * fma(-hr * ri, ri, 1.5);
                         const double dr = r2 * ri;
                         if (dr < Rcut) {
-                            const double e = exp(-dr * invlDeb);
+                            const double e = exp_neg(-dr * invlDeb);
                             if (MODE == 0) {
                                 const double ftotal = ((ri + invlDeb) * e) * (ri * ri);
-                                fx += dx * ftotal;
-                                fy += dy * ftotal;
-                                fz += dz * ftotal;
+                                fx = fma(dx, ftotal, fx);
+                                fy = fma(dy, ftotal, fy);
+                                fz = fma(dz, ftotal, fz);
                             } else {
-                                fx += e * ri;
+                                fx = fma(e, ri, fx);
                             }
                         }
                     }
@@ -161,20 +188,22 @@ __device__ __forceinline__ bool yukawa_ft(double& dx, double& dy, double& dz, co
         dy -= L * round(dy / L);
         dz -= L * round(dz / L);
     }
-    const double r2 = dx * dx + dy * dy + dz * dz;
     if (VARIANT == 0) {
+        const double r2 = dx * dx + dy * dy + dz * dz;
         const double dr = sqrt(r2);
         if (!(dr > 0 && dr < a.Rcut)) return false;
         ft = (1. / dr + a.invlDeb) * exp(-dr / a.lDeb) / (dr * dr);
         return true;
     } else {
+        const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
         if (!(r2 > 0)) return false;
         double ri = __builtin_amdgcn_rsq(r2);
-        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
-        ri = ri * (1.5 - (0.5 * r2) * (ri * ri));
+        const double hr = 0.5 * r2;
+        ri = ri * fma(-hr * ri, ri, 1.5);
+        ri = ri * fma(-hr * ri, ri, 1.5);
         const double dr = r2 * ri;
         if (!(dr < a.Rcut)) return false;
-        ft = ((ri + a.invlDeb) * exp(-dr * a.invlDeb)) * (ri * ri);
+        ft = ((ri + a.invlDeb) * exp_neg(-dr * a.invlDeb)) * (ri * ri);
         return true;
     }
 }

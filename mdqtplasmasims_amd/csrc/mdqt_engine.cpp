@@ -93,6 +93,8 @@ struct mdqt_ctx {
     int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel
     // rng_mode 0: the reference's drand48 stream, consumed in ion order on the device
     unsigned long long* dX48 = nullptr;   // [1] stream state + [48] jA + [48] jC
+    int* dFlags = nullptr;         // [0] set by the substep kernels when a position leaves [-L/8, 9L/8]
+    bool guard = false;            // host view: range-check every pair (see ForceArgs::guard)
     double* dU = nullptr;                 // [5][S] uniforms of the current substep
     ncclComm_t comm = nullptr;     // RCCL communicator over the world_size ranks (sharded runs)
     double* dComm = nullptr;       // device staging for small all-reduces
@@ -116,6 +118,23 @@ struct mdqt_ctx {
 };
 
 static int settle_forces(mdqt_ctx* s);
+
+// The substep kernels raise dFlags[0] if a position leaves [-L/8, 9L/8] (an ion moving more than
+// L/8 in half a substep: not a physical run).  Checked at every host synchronisation point;
+// from then on every pair is range-checked, and the call reports the event as an error.
+static int check_range_flag(mdqt_ctx* s) {
+    int f = 0;
+    if (hipMemcpyAsync(&f, s->dFlags, sizeof f, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+        hipStreamSynchronize(s->stream) != hipSuccess)
+        return fail("reading the position-range flag failed");
+    if (f && !s->guard) {
+        s->guard = true;
+        return fail("positions left [-L/8, 9L/8] during the run (ion displacement > L/8 per half "
+                    "substep); pair range checks are now on, but forces since the last sync used "
+                    "the in-box minimum image");
+    }
+    return 0;
+}
 
 // ---------------------------------------------------------------------------------------------
 // parameters and constants
@@ -404,6 +423,14 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
     }
     s->stream = s->own;
     if (hipMalloc(&s->dTab, sizeof(LaneTab)) != hipSuccess) { mdqt_destroy(s); return fail("hipMalloc lane table"); }
+    {
+        const int f[2] = {0, 1};
+        if (hipMalloc(&s->dFlags, sizeof f) != hipSuccess ||
+            hipMemcpy(s->dFlags, f, sizeof f, hipMemcpyHostToDevice) != hipSuccess) {
+            mdqt_destroy(s);
+            return fail("hipMalloc flags");
+        }
+    }
     build_constants(s);
     if (s->p.rng_mode == 0) {
         unsigned long long h[97];
@@ -441,6 +468,7 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     if (s->dTab) (void)hipFree(s->dTab);
     if (s->dComm) (void)hipFree(s->dComm);
     if (s->dX48) (void)hipFree(s->dX48);
+    if (s->dFlags) (void)hipFree(s->dFlags);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     for (auto& pool : s->evpool)
         for (hipEvent_t ev : pool) (void)hipEventDestroy(ev);
@@ -481,6 +509,15 @@ static int upload(mdqt_ctx* s, const double* R, const double* V, size_t ld, cons
             for (int c = 0; c < 3; ++c) h[(size_t)w * 3 * S + (size_t)c * S + l] = R[(size_t)c * ld + g];
         }
         HIPCHK(hipMemcpyAsync(s->dR, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+        int oor = 0;                                     // positions outside [-L/8, 9L/8]?
+        const double plo = -0.125 * s->L, phi = 1.125 * s->L;
+        for (size_t k = 0; k < (size_t)3 * N && !oor; ++k) {
+            const double x = R[(k / N) * ld + k % N];
+            if (!(x >= plo && x <= phi)) oor = 1;
+        }
+        s->guard = oor != 0;
+        const int zero = 0;
+        HIPCHK(hipMemcpyAsync(s->dFlags, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
     }
     const int lo = s->lo, n = s->nloc;
@@ -535,6 +572,7 @@ extern "C" int mdqt_get_state(mdqt_ctx* s, double* R, double* V, double* F, size
     const int N = s->N, S = s->S, W = s->p.world_size, lo = s->lo, n = s->nloc;
     if (ld < (size_t)N) return fail("ld < N");
     HIPCHK(hipSetDevice(s->dev));
+    if (check_range_flag(s)) return -1;
     if (F && settle_forces(s)) return -1;
     if (R) {
         std::vector<double> h((size_t)3 * S * W);
@@ -665,6 +703,7 @@ static ForceArgs force_args(mdqt_ctx* s, double* out) {
     a.row_lo = s->lo; a.nrows = s->nloc;
     a.nseg = s->nseg; a.seglen = s->seglen;
     fill_pair_consts(a, s->L, s->lDeb, s->force_variant);
+    a.guard = s->guard ? 1 : 0;
     return a;
 }
 
@@ -700,6 +739,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         ForceArgs c = force_args(s, nullptr);
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
         a.micGuard = c.micGuard;
+        a.guard = c.guard;
         HIPCHK(launch_forces_n3(a, s->force_variant, s->stream));
         s->f_pending = true;       // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots;
@@ -726,6 +766,7 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         a.R = s->dR + (size_t)s->p.rank * 3 * s->S;
         a.V = s->dV; a.F = s->dF; a.psi = s->dPsi; a.tPart = s->dTp;
         a.Fpart = s->dFpart; a.nseg = s->f_pending ? s->pend_nseg : 1;
+        a.oor = s->dFlags;
         s->f_pending = false;
         a.n = s->nloc; a.S = s->S; a.gid0 = (uint64_t)s->lo;
         a.q0 = s->qidx;
@@ -769,6 +810,7 @@ extern "C" int mdqt_substeps(mdqt_ctx* s, int n) {
 extern "C" int mdqt_md_steps(mdqt_ctx* s, int n) {
     if (!s) return fail("NULL context");
     for (int k = 0; k < n; ++k) {
+        if (k > 0 && k % 64 == 0 && check_range_flag(s)) return -1;
         if (mdqt_allgather_positions(s)) return -1;     // sharded: other slabs' R
         if (mdqt_forces(s)) return -1;
         s->c0++;
@@ -803,10 +845,16 @@ static int pairs_raw(int mode, int N, double L, double lDeb, const double* R, si
     HIPCHK(hipMalloc(&dP, (size_t)3 * S * nseg * sizeof(double)));
     HIPCHK(hipMalloc(&dO, (size_t)3 * S * sizeof(double)));
     HIPCHK(hipMemcpyAsync(dR, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    int oor = 0;
+    for (size_t k = 0; k < (size_t)3 * N && !oor; ++k) {
+        const double x = R[(k / N) * ld + k % N];
+        if (!(x >= -0.125 * L && x <= 1.125 * L)) oor = 1;
+    }
     ForceArgs a;
     a.Rall = dR; a.Fpart = dP; a.N = N; a.S = S; a.row_lo = 0; a.nrows = N;
     a.nseg = nseg; a.seglen = tmp.seglen;
     fill_pair_consts(a, L, lDeb, variant);
+    a.guard = oor;
     HIPCHK(mode == 0 ? launch_forces(a, st) : launch_potential_rows(a, st));
     HIPCHK(launch_reduce_segments(dP, dO, nseg, N, S, mode == 0 ? 3 : 1, st));
     HIPCHK(hipMemcpyAsync(h.data(), dO, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1172,7 +1220,7 @@ extern "C" void* mdqt_get_stream(mdqt_ctx* s) { return (void*)s->stream; }
 extern "C" int mdqt_synchronize(mdqt_ctx* s) {
     HIPCHK(hipSetDevice(s->dev));
     HIPCHK(hipStreamSynchronize(s->stream));
-    return 0;
+    return check_range_flag(s);
 }
 extern "C" int mdqt_positions_device(mdqt_ctx* s, void** dptr, int* S) {
     if (dptr) *dptr = (void*)s->dR;

@@ -1,0 +1,297 @@
+// gfx950 force kernels: forces() (SpeedUp:192-236) and the pair potential of Epotential()
+// (SpeedUp:244-281).
+//
+//   k_pairs<MODE, VARIANT>   owner-computes rows, LDS-staged j tiles, j split in segments
+//   k_pairs_n3<VARIANT>      Newton-3 over 64x64 tile pairs (one GPU, N <= 65536)
+//   k_reduce_segments        canonical sum of the partials when a caller asks for F
+//
+// VARIANT 0 keeps the reference's operations (sqrt, the three divisions, libm exp) without
+// contraction; VARIANT 1 (default) is the reciprocal form with a range-specialised exp and
+// FMA contraction — a few ulp per pair, inside the 1e-13 force gate.  Both evaluate the minimum
+// image exactly without dividing (see PairC / mic below).
+#include "mdqt_internal.hpp"
+
+#include <math.h>
+
+namespace mdqt {
+
+struct PairC {
+    double L, T, G, Rcut, lDeb, invlDeb;
+};
+
+__device__ __forceinline__ const double* pos_base(const double* Rall, int g, int S) {
+    const int w = g / S;
+    return Rall + (size_t)w * 3 * S + (g - w * S);
+}
+
+// e^x for x = -r/lDeb in [-L/(2 lDeb), 0] (no overflow, no subnormal results for any box the
+// reference runs): Cody-Waite x = n ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial
+// (truncation < 5e-18 relative) in FMA Horner form, exponent shift.  <= 1 ulp vs glibc.
+__device__ __forceinline__ double exp_neg(double x) {
+    const double n = __builtin_rint(x * 1.4426950408889634);
+    double r = fma(-n, 0x1.62e42fefa39efp-1, x);
+    r = fma(-n, 0x1.abc9e3b39803fp-56, r);
+    double p = 1.6059043836821613e-10;               // 1/13!
+    p = fma(p, r, 2.08767569878681e-09);
+    p = fma(p, r, 2.505210838544172e-08);
+    p = fma(p, r, 2.755731922398589e-07);
+    p = fma(p, r, 2.7557319223985893e-06);
+    p = fma(p, r, 2.48015873015873e-05);
+    p = fma(p, r, 0.0001984126984126984);
+    p = fma(p, r, 0.001388888888888889);
+    p = fma(p, r, 0.008333333333333333);
+    p = fma(p, r, 0.041666666666666664);
+    p = fma(p, r, 0.16666666666666666);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)n);
+}
+
+// Minimum image dx -= L*round(dx/L) (SpeedUp:218-220), exactly, without the division: for
+// |dx/L| < 1.5, round(dx/L) is +1 iff dx >= T and -1 iff dx <= -T, T the smallest double with
+// fl(T/L) >= 0.5 (host nextafter search), and dx - copysign(L, dx) is bit-identical to dx - L
+// resp. dx + L.  GUARD: positions may have left [-L/8, 9L/8] (set_state input), so take the
+// division form for separations beyond G = 1.25 L.
+template <bool GUARD>
+__device__ __forceinline__ void mic(double& dx, double& dy, double& dz, const PairC& c) {
+    if (GUARD && !(fabs(dx) < c.G && fabs(dy) < c.G && fabs(dz) < c.G)) {
+        dx -= c.L * round(dx / c.L);
+        dy -= c.L * round(dy / c.L);
+        dz -= c.L * round(dz / c.L);
+        return;
+    }
+    dx = (fabs(dx) >= c.T) ? dx - copysign(c.L, dx) : dx;
+    dy = (fabs(dy) >= c.T) ? dy - copysign(c.L, dy) : dy;
+    dz = (fabs(dz) >= c.T) ? dz - copysign(c.L, dz) : dz;
+}
+
+// Force factor ft of one minimum-image separation (F_i += d * ft), 0 unless 0 < r < L/2
+// (:221-224).  Branch-free: out-of-range values are discarded by the final select.
+template <int VARIANT>
+__device__ __forceinline__ double pair_ft(double dx, double dy, double dz, const PairC& c) {
+    if (VARIANT == 0) {
+        const double r2 = dx * dx + dy * dy + dz * dz;
+        const double dr = sqrt(r2);
+        const double ft = (1. / dr + c.invlDeb) * exp(-dr / c.lDeb) / (dr * dr);   // :224
+        return (dr > 0 && dr < c.Rcut) ? ft : 0.;
+    } else {
+        const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+        double ri = __builtin_amdgcn_rsq(r2);
+        const double hr = 0.5 * r2;
+        ri = ri * fma(-hr * ri, ri, 1.5);
+        ri = ri * fma(-hr * ri, ri, 1.5);
+        const double dr = r2 * ri;
+        const double ft = ((ri + c.invlDeb) * exp_neg(-dr * c.invlDeb)) * (ri * ri);
+        return (r2 > 0 && dr < c.Rcut) ? ft : 0.;
+    }
+}
+
+// Pair potential exp(-r/lDeb)/r (:265), 0 unless 0 < r < L/2
+template <int VARIANT>
+__device__ __forceinline__ double pair_u(double dx, double dy, double dz, const PairC& c) {
+    if (VARIANT == 0) {
+        const double dr = sqrt(dx * dx + dy * dy + dz * dz);
+        const double u = exp(-dr / c.lDeb) / (dr);
+        return (dr > 0 && dr < c.Rcut) ? u : 0.;
+    } else {
+        const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+        double ri = __builtin_amdgcn_rsq(r2);
+        const double hr = 0.5 * r2;
+        ri = ri * fma(-hr * ri, ri, 1.5);
+        ri = ri * fma(-hr * ri, ri, 1.5);
+        const double dr = r2 * ri;
+        const double u = exp_neg(-dr * c.invlDeb) * ri;
+        return (r2 > 0 && dr < c.Rcut) ? u : 0.;
+    }
+}
+
+template <int VARIANT>
+__device__ __forceinline__ void accum(double& f, double d, double ft) {
+    if (VARIANT == 0) f += d * ft;        // the reference's F[i] += dx*ftotal (:225-230)
+    else f = fma(d, ft, f);
+}
+
+// ------------------------------------------------------------------------------------------
+// rows: owner computes row i over the j of its segment in ASCENDING j (the single-thread
+// reference's F_i is exactly that sum; the self pair has r = 0 and is dropped
+// by the 0 < r test like the reference's coincident pairs)
+// ------------------------------------------------------------------------------------------
+constexpr int FT = 256;
+
+template <int MODE, int VARIANT, bool GUARD>
+__device__ __forceinline__ void rows_body(const ForceArgs& a, const PairC& c, double* sx, double* sy,
+                                          double* sz) {
+    const int tid = threadIdx.x;
+    const int li = blockIdx.x * FT + tid;
+    const int seg = blockIdx.y;
+    const bool active = li < a.nrows;
+    const int gi = a.row_lo + li;
+    double rx = 0., ry = 0., rz = 0.;
+    if (active) {
+        const double* p = pos_base(a.Rall, gi, a.S);
+        rx = p[0]; ry = p[a.S]; rz = p[2 * a.S];
+    }
+    double fx = 0., fy = 0., fz = 0.;
+    const int j0 = seg * a.seglen;
+    const int j1 = min(a.N, j0 + a.seglen);
+    for (int jt = j0; jt < j1; jt += FT) {
+        const int jl = jt + tid;
+        __syncthreads();
+        if (jl < j1) {
+            const double* p = pos_base(a.Rall, jl, a.S);
+            sx[tid] = p[0]; sy[tid] = p[a.S]; sz[tid] = p[2 * a.S];
+        }
+        __syncthreads();
+        const int nj = min(FT, j1 - jt);
+        if (active) {
+#pragma unroll 2
+            for (int k = 0; k < nj; ++k) {
+                double dx = rx - sx[k], dy = ry - sy[k], dz = rz - sz[k];   // :213-215
+                mic<GUARD>(dx, dy, dz, c);
+                if (MODE == 0) {
+                    const double ft = pair_ft<VARIANT>(dx, dy, dz, c);
+                    accum<VARIANT>(fx, dx, ft);
+                    accum<VARIANT>(fy, dy, ft);
+                    accum<VARIANT>(fz, dz, ft);
+                } else {
+                    const double u = pair_u<VARIANT>(dx, dy, dz, c);
+                    if (VARIANT == 0) fx += u;
+                    else fx += u;
+                }
+            }
+        }
+    }
+    if (active) {
+        double* o = a.Fpart + (size_t)seg * 3 * a.S;
+        o[li] = fx;
+        if (MODE == 0) { o[a.S + li] = fy; o[2 * a.S + li] = fz; }
+    }
+}
+
+template <int MODE, int VARIANT, bool GUARD>
+__global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
+    __shared__ double sx[FT], sy[FT], sz[FT];
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb};
+    rows_body<MODE, VARIANT, GUARD>(a, c, sx, sy, sz);
+}
+
+__global__ __launch_bounds__(256) void k_reduce_segments(const double* __restrict__ Fpart,
+                                                         double* __restrict__ F, int nseg,
+                                                         int nrows, int S, int ncomp) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= nrows || c >= ncomp) return;
+    F[(size_t)c * S + i] = seg_sum(Fpart + (size_t)c * S + i, (size_t)3 * S, nseg);
+}
+
+// ------------------------------------------------------------------------------------------
+// Newton-3 tile pairs: wave w takes (I, J) = pairs[w]; lane l holds ion I*64+l and one ion of
+// tile J, which travels one lane per step together with its accumulated force.  Each pair of
+// the two tiles is evaluated once: f goes to i, -f to j (exact: the minimum image and r are
+// sign-symmetric, so f(j,i) == -f(i,j) bit for bit).  Deterministic slots, no atomics.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int gat_i(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ double gat_d(double v, int src) {
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+template <int VARIANT, bool GUARD>
+__device__ __forceinline__ void n3_body(const N3Args& a, const PairC& c) {
+    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int l = threadIdx.x & 63;
+    const int2 IJ = a.pairs[w];
+    const int I = IJ.x, J = IJ.y;
+    const int S = a.S, N = a.N;
+    const double* X = a.R;
+    const double* Y = a.R + S;
+    const double* Z = a.R + 2 * S;
+    const int i = I * 64 + l;
+    const bool vi = i < N;
+    const double xi = vi ? X[i] : 0., yi = vi ? Y[i] : 0., zi = vi ? Z[i] : 0.;
+    int jx = J * 64 + l;
+    double xj = jx < N ? X[jx] : 0., yj = jx < N ? Y[jx] : 0., zj = jx < N ? Z[jx] : 0.;
+    double fxi = 0., fyi = 0., fzi = 0., fxj = 0., fyj = 0., fzj = 0.;
+    const int nxt = (l + 1) & 63;
+    const bool diag = (I == J);
+    const int nsteps = diag ? 32 : 64;
+    for (int s = 0; s < nsteps; ++s) {
+        if (diag) {                                 // diagonal: meet lanes l+1 .. l+32 only
+            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
+            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
+        }
+        const bool on = vi && jx < N && (!diag || s < 31 || l < 32);
+        double dx = xi - xj, dy = yi - yj, dz = zi - zj;
+        mic<GUARD>(dx, dy, dz, c);
+        double ft = pair_ft<VARIANT>(dx, dy, dz, c);
+        ft = on ? ft : 0.;
+        const double px = dx * ft, py = dy * ft, pz = dz * ft;
+        fxi += px; fyi += py; fzi += pz;
+        fxj -= px; fyj -= py; fzj -= pz;
+        if (!diag) {
+            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
+            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
+        }
+    }
+    const size_t slab3 = (size_t)3 * S;
+    double* Pi = a.P + (size_t)J * slab3;            // rows of I: slot J (I itself on the diagonal)
+    double* Pj = a.P + (size_t)(diag ? a.ntiles : I) * slab3;
+    if (i < S) { Pi[i] = fxi; Pi[S + i] = fyi; Pi[2 * S + i] = fzi; }
+    if (jx < S) { Pj[jx] = fxj; Pj[S + jx] = fyj; Pj[2 * S + jx] = fzj; }
+}
+
+template <int VARIANT, bool GUARD>
+__global__ __launch_bounds__(256) void k_pairs_n3(N3Args a) {
+    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (w >= a.npairs) return;                      // wave-uniform exit
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb};
+    n3_body<VARIANT, GUARD>(a, c);
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+static int seg_blocks(int nrows) { return (nrows + FT - 1) / FT; }
+
+template <int MODE>
+static hipError_t launch_rows(const ForceArgs& a, hipStream_t s) {
+    if (a.nrows <= 0) return hipSuccess;
+    dim3 grid(seg_blocks(a.nrows), a.nseg);
+    if (a.variant == 1) {
+        if (a.guard) hipLaunchKernelGGL((k_pairs<MODE, 1, true>), grid, dim3(FT), 0, s, a);
+        else hipLaunchKernelGGL((k_pairs<MODE, 1, false>), grid, dim3(FT), 0, s, a);
+    } else {
+        if (a.guard) hipLaunchKernelGGL((k_pairs<MODE, 0, true>), grid, dim3(FT), 0, s, a);
+        else hipLaunchKernelGGL((k_pairs<MODE, 0, false>), grid, dim3(FT), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_forces(const ForceArgs& a, hipStream_t s) { return launch_rows<0>(a, s); }
+hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s) { return launch_rows<1>(a, s); }
+
+hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
+                                  hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    if (ncomp < 1 || ncomp > 3) return hipErrorInvalidValue;
+    dim3 grid((nrows + 255) / 256, ncomp);
+    hipLaunchKernelGGL(k_reduce_segments, grid, dim3(256), 0, s, Fpart, F, nseg, nrows, S, ncomp);
+    return hipGetLastError();
+}
+
+hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s) {
+    if (a.npairs <= 0) return hipSuccess;
+    dim3 grid((a.npairs + 3) / 4);
+    if (variant == 1) {
+        if (a.guard) hipLaunchKernelGGL((k_pairs_n3<1, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_pairs_n3<1, false>), grid, dim3(256), 0, s, a);
+    } else {
+        if (a.guard) hipLaunchKernelGGL((k_pairs_n3<0, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_pairs_n3<0, false>), grid, dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mdqt

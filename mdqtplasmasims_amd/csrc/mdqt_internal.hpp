@@ -70,6 +70,7 @@ struct SubstepArgs {
     int nsub, do_step, do_qt;
     const double* U;    // rng_mode 0 (drand48 reference order): uniforms [5][S] of this substep
                         // (nsub == 1), from k_d48_resolve; nullptr = Philox stream
+    int* oor;           // set to 1 if a final position leaves [-L/8, 9L/8] (see ForceArgs::oor)
     double L;
     double t[MAXSUB];       // global time at each substep (t before qstep advances it)
     double expDet[MAXSUB];  // expDetuning(t) (:447)
@@ -87,7 +88,25 @@ struct ForceArgs {
     double micT;        // smallest d with fl(d/L) >= 0.5: round(dx/L) = [dx >= micT] - [dx <= -micT]
     double micGuard;    // |dx| below this is inside the threshold rule's validity (|dx/L| < 1.5)
     int variant;        // 0 = exact (the reference's operations), 1 = fast (rsqrt/reciprocal form)
+    int guard;          // positions may have left [-L/8, 9L/8] (set_state input or a device
+                        // report): range-check every pair, far separations take the division form
 };
+
+// Canonical sum of nseg partials p[0], p[stride], ... : eight interleaved accumulators
+// (partial s goes to s % 8, ascending) combined as ((a0+a1)+(a2+a3))+((a4+a5)+(a6+a7)).  One
+// fixed order wherever it is evaluated (deterministic); independent loads, short chains.
+__device__ __forceinline__ double seg_sum(const double* __restrict__ p, size_t stride, int nseg) {
+    double a[8] = {0., 0., 0., 0., 0., 0., 0., 0.};
+    int s = 0;
+    for (; s + 8 <= nseg; s += 8) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] += p[(size_t)(s + q) * stride];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if (s + q < nseg) a[q] += p[(size_t)(s + q) * stride];
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
 
 // Newton-3 tile-pair scheme (world_size 1, small/medium N): one wave per 64x64 tile pair
 // (I <= J), the J tile rotating through the lanes; partials go to slot J (rows of I) and slot
@@ -99,6 +118,7 @@ struct N3Args {
     const int2* pairs;  // (I, J) of every wave
     int N, S, ntiles, npairs;
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
+    int guard;          // as ForceArgs::guard
 };
 
 // drand48 in the reference's order (SpeedUp:486, :575-687: ions in index order, 1 draw per

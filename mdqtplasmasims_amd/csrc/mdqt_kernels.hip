@@ -1,8 +1,8 @@
-// gfx950 kernels of the MDQT hot path.
+// gfx950 kernels of the MDQT hot path (the force kernels are in mdqt_forces.hip).
 //
-//   k_pairs<FORCE>      Yukawa all-pairs force, forces() SpeedUp:192-236
-//   k_pairs<POTENTIAL>  pair potential rows,    Epotential() SpeedUp:244-281
 //   k_substeps          n x (step(); qstep()) fused per ion, SpeedUp:356-430 + :438-717
+//   k_substeps_lanes    the same, one ion per 16-lane group (lane = quantum state)
+//   k_d48_resolve       drand48 in the reference's consumption order (rng_mode 0)
 //   k_sum_vx / k_energy_sums / k_kde*   observables of output(), SpeedUp:917-1032
 //
 // Built with -ffp-contract=off and without fast-math: every floating-point expression keeps
@@ -13,290 +13,6 @@
 #include <math.h>
 
 namespace mdqt {
-
-// ------------------------------------------------------------------------------------------
-// position addressing: gathered array [world][3][S]; global ion g lives in slab g / S
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ const double* pos_base(const double* Rall, int g, int S) {
-    const int w = g / S;
-    return Rall + (size_t)w * 3 * S + (g - w * S);
-}
-
-// ------------------------------------------------------------------------------------------
-// Kernel 1: all-pairs Yukawa force / potential, owner-computes rows, LDS-staged j tiles.
-// Row i of the owned slab accumulates f(i, j) over its j segment in ASCENDING j — in the
-// single-thread reference F_i is exactly that ascending sum, so with one
-// segment the result matches the reference order; with nseg > 1 the segment partials are
-// summed in ascending segment order by k_reduce_segments (deterministic).
-// ------------------------------------------------------------------------------------------
-constexpr int FT = 256;   // threads per block = rows per block = j tile
-
-// e^x for the fast pair variant.  x = -r/lDeb lies in [-L/(2 lDeb), 0] (no overflow, no
-// subnormal results for any box the reference runs), so the libm special-case paths are not
-// needed: Cody-Waite reduction x = n ln2 + r, |r| <= ln2/2, then the degree-13 Taylor
-// polynomial (truncation < 5e-18 relative) in FMA Horner form and an exponent shift.  ~1 ulp.
-__device__ __forceinline__ double exp_neg(double x) {
-    const double n = __builtin_rint(x * 1.4426950408889634);
-    double r = fma(-n, 0x1.62e42fefa39efp-1, x);
-    r = fma(-n, 0x1.abc9e3b39803fp-56, r);
-    double p = 1.6059043836821613e-10;               // 1/13!
-    p = fma(p, r, 2.08767569878681e-09);             // 1/12!
-    p = fma(p, r, 2.505210838544172e-08);            // 1/11!
-    p = fma(p, r, 2.755731922398589e-07);            // 1/10!
-    p = fma(p, r, 2.7557319223985893e-06);           // 1/9!
-    p = fma(p, r, 2.48015873015873e-05);             // 1/8!
-    p = fma(p, r, 0.0001984126984126984);            // 1/7!
-    p = fma(p, r, 0.001388888888888889);             // 1/6!
-    p = fma(p, r, 0.008333333333333333);             // 1/5!
-    p = fma(p, r, 0.041666666666666664);             // 1/4!
-    p = fma(p, r, 0.16666666666666666);              // 1/3!
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    return ldexp(p, (int)n);
-}
-
-template <int MODE, int VARIANT>   // MODE 0: force, 1: potential; VARIANT 0: exact, 1: fast
-__global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
-    __shared__ double sx[FT], sy[FT], sz[FT];
-    const int tid = threadIdx.x;
-    const int li = blockIdx.x * FT + tid;
-    const int seg = blockIdx.y;
-    const bool active = li < a.nrows;
-    const int gi = a.row_lo + li;
-    double rx = 0., ry = 0., rz = 0.;
-    if (active) {
-        const double* p = pos_base(a.Rall, gi, a.S);
-        rx = p[0]; ry = p[a.S]; rz = p[2 * a.S];
-    }
-    const double L = a.L, lDeb = a.lDeb, Rcut = a.Rcut, invlDeb = a.invlDeb;
-    const double T = a.micT, G = a.micGuard;
-    double fx = 0., fy = 0., fz = 0.;
-    const int j0 = seg * a.seglen;
-    const int j1 = min(a.N, j0 + a.seglen);
-    for (int jt = j0; jt < j1; jt += FT) {
-        const int jl = jt + tid;
-        __syncthreads();
-        if (jl < j1) {
-            const double* p = pos_base(a.Rall, jl, a.S);
-            sx[tid] = p[0]; sy[tid] = p[a.S]; sz[tid] = p[2 * a.S];
-        }
-        __syncthreads();
-        const int nj = min(FT, j1 - jt);
-        if (active) {
-            for (int k = 0; k < nj; ++k) {
-                if (jt + k == gi) continue;
-                double dx = rx - sx[k];                    // SpeedUp:213-215
-                double dy = ry - sy[k];
-                double dz = rz - sz[k];
-                // minimum image dx -= L*round(dx/L) (:218-220), evaluated exactly without the
-                // division: for |dx/L| < 1.5, round(dx/L) is +1 iff dx >= T, -1 iff dx <= -T
-                if (fabs(dx) < G && fabs(dy) < G && fabs(dz) < G) {
-                    dx = (dx >= T) ? dx - L : ((dx <= -T) ? dx + L : dx);
-                    dy = (dy >= T) ? dy - L : ((dy <= -T) ? dy + L : dy);
-                    dz = (dz >= T) ? dz - L : ((dz <= -T) ? dz + L : dz);
-                } else {
-                    dx -= L * round(dx / L);
-                    dy -= L * round(dy / L);
-                    dz -= L * round(dz / L);
-                }
-                if (VARIANT == 0) {
-                    const double r2 = dx * dx + dy * dy + dz * dz;
-                    const double dr = sqrt(r2);            // :221
-                    if (dr > 0 && dr < Rcut) {             // :222
-                        if (MODE == 0) {
-                            const double ftotal = (1. / dr + invlDeb) * exp(-dr / lDeb) / (dr * dr); // :224
-                            fx += dx * ftotal;             // :225-230 (i's view)
-                            fy += dy * ftotal;
-                            fz += dz * ftotal;
-                        } else {
-                            fx += exp(-dr / lDeb) / (dr);  // :265
-                        }
-                    }
-                } else {
-                    // same law in reciprocal form: 1/r from a refined v_rsq_f64, r = r2/r,
-                    // exp_neg, FMA contraction (a few ulp per pair; force gate 1e-13 relative)
-                    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
-                    if (r2 > 0) {
-                        double ri = __builtin_amdgcn_rsq(r2);
-                        const double hr = 0.5 * r2;
-                        ri = ri * fma(-hr * ri, ri, 1.5);
-                        ri = ri * fma(-hr * ri, ri, 1.5);
-                        const double dr = r2 * ri;
-                        if (dr < Rcut) {
-                            const double e = exp_neg(-dr * invlDeb);
-                            if (MODE == 0) {
-                                const double ftotal = ((ri + invlDeb) * e) * (ri * ri);
-                                fx = fma(dx, ftotal, fx);
-                                fy = fma(dy, ftotal, fy);
-                                fz = fma(dz, ftotal, fz);
-                            } else {
-                                fx = fma(e, ri, fx);
-                            }
-                        }
-                    }
-                }
-            }
-        }
-    }
-    if (active) {
-        double* o = a.Fpart + (size_t)seg * 3 * a.S;
-        o[li] = fx;
-        if (MODE == 0) { o[a.S + li] = fy; o[2 * a.S + li] = fz; }
-    }
-}
-
-// Canonical sum of the nseg segment partials of one (row, component): eight interleaved
-// accumulators (segment s goes to s % 8, ascending), combined as ((a0+a1)+(a2+a3))+((a4+a5)+
-// (a6+a7)).  Fixed order => deterministic and identical wherever it is evaluated; the loads are
-// independent, so the dependent chain is nseg/8 adds instead of nseg.
-__device__ __forceinline__ double seg_sum(const double* __restrict__ p, size_t stride, int nseg) {
-    double a[8] = {0., 0., 0., 0., 0., 0., 0., 0.};
-    int s = 0;
-    for (; s + 8 <= nseg; s += 8) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a[q] += p[(size_t)(s + q) * stride];
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-        if (s + q < nseg) a[q] += p[(size_t)(s + q) * stride];
-    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-}
-
-__global__ __launch_bounds__(256) void k_reduce_segments(const double* __restrict__ Fpart,
-                                                         double* __restrict__ F, int nseg,
-                                                         int nrows, int S, int ncomp) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int c = blockIdx.y;
-    if (i >= nrows || c >= ncomp) return;
-    F[(size_t)c * S + i] = seg_sum(Fpart + (size_t)c * S + i, (size_t)3 * S, nseg);
-}
-
-static int seg_blocks(int nrows) { return (nrows + FT - 1) / FT; }
-
-// One pair's minimum image + Yukawa force magnitude (SpeedUp:213-224), as in k_pairs.
-// dx, dy, dz in: r_i - r_j; out: minimum-image separation.  Returns false outside 0<r<L/2.
-template <int VARIANT>
-__device__ __forceinline__ bool yukawa_ft(double& dx, double& dy, double& dz, const N3Args& a, double& ft) {
-    const double L = a.L, T = a.micT, G = a.micGuard;
-    if (fabs(dx) < G && fabs(dy) < G && fabs(dz) < G) {
-        dx = (dx >= T) ? dx - L : ((dx <= -T) ? dx + L : dx);
-        dy = (dy >= T) ? dy - L : ((dy <= -T) ? dy + L : dy);
-        dz = (dz >= T) ? dz - L : ((dz <= -T) ? dz + L : dz);
-    } else {
-        dx -= L * round(dx / L);
-        dy -= L * round(dy / L);
-        dz -= L * round(dz / L);
-    }
-    if (VARIANT == 0) {
-        const double r2 = dx * dx + dy * dy + dz * dz;
-        const double dr = sqrt(r2);
-        if (!(dr > 0 && dr < a.Rcut)) return false;
-        ft = (1. / dr + a.invlDeb) * exp(-dr / a.lDeb) / (dr * dr);
-        return true;
-    } else {
-        const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
-        if (!(r2 > 0)) return false;
-        double ri = __builtin_amdgcn_rsq(r2);
-        const double hr = 0.5 * r2;
-        ri = ri * fma(-hr * ri, ri, 1.5);
-        ri = ri * fma(-hr * ri, ri, 1.5);
-        const double dr = r2 * ri;
-        if (!(dr < a.Rcut)) return false;
-        ft = ((ri + a.invlDeb) * exp_neg(-dr * a.invlDeb)) * (ri * ri);
-        return true;
-    }
-}
-
-__device__ __forceinline__ int gat_i(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
-__device__ __forceinline__ double gat_d(double v, int src) {
-    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
-    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
-    return __hiloint2double(hi, lo);
-}
-
-// Newton-3 tile pairs: wave w takes (I, J) = pairs[w]; lane l holds ion I*64+l and one ion of
-// tile J, which travels one lane per step together with its accumulated force.  Each pair of
-// the two tiles is evaluated once: f goes to i, -f to j (exact: the minimum image and r are
-// sign-symmetric, f(j,i) == -f(i,j) bit for bit).
-template <int VARIANT>
-__global__ __launch_bounds__(256) void k_pairs_n3(N3Args a) {
-    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int l = threadIdx.x & 63;
-    if (w >= a.npairs) return;                      // wave-uniform exit
-    const int2 IJ = a.pairs[w];
-    const int I = IJ.x, J = IJ.y;
-    const int S = a.S, N = a.N;
-    const double* X = a.R;
-    const double* Y = a.R + S;
-    const double* Z = a.R + 2 * S;
-    const int i = I * 64 + l;
-    const bool vi = i < N;
-    const double xi = vi ? X[i] : 0., yi = vi ? Y[i] : 0., zi = vi ? Z[i] : 0.;
-    int jx = J * 64 + l;
-    double xj = jx < N ? X[jx] : 0., yj = jx < N ? Y[jx] : 0., zj = jx < N ? Z[jx] : 0.;
-    double fxi = 0., fyi = 0., fzi = 0., fxj = 0., fyj = 0., fzj = 0.;
-    const int nxt = (l + 1) & 63;
-    const bool diag = (I == J);
-    const int nsteps = diag ? 32 : 64;
-    for (int s = 0; s < nsteps; ++s) {
-        if (diag) {                                 // diagonal: meet lane l+1 .. l+32 only
-            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
-            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
-        }
-        const bool on = vi && jx < N && (!diag || s < 31 || l < 32);
-        if (on) {
-            double dx = xi - xj, dy = yi - yj, dz = zi - zj, ft;
-            if (yukawa_ft<VARIANT>(dx, dy, dz, a, ft)) {
-                const double px = dx * ft, py = dy * ft, pz = dz * ft;
-                fxi += px; fyi += py; fzi += pz;
-                fxj -= px; fyj -= py; fzj -= pz;
-            }
-        }
-        if (!diag) {
-            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
-            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
-        }
-    }
-    const size_t slab3 = (size_t)3 * S;
-    double* Pi = a.P + (size_t)J * slab3;            // rows of I: slot J (I itself on the diagonal)
-    double* Pj = a.P + (size_t)(diag ? a.ntiles : I) * slab3;
-    if (i < S) { Pi[i] = fxi; Pi[S + i] = fyi; Pi[2 * S + i] = fzi; }
-    if (jx < S) { Pj[jx] = fxj; Pj[S + jx] = fyj; Pj[2 * S + jx] = fzj; }
-}
-
-hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s) {
-    if (a.npairs <= 0) return hipSuccess;
-    dim3 grid((a.npairs + 3) / 4);
-    if (variant == 1) hipLaunchKernelGGL(k_pairs_n3<1>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_pairs_n3<0>, grid, dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_forces(const ForceArgs& a, hipStream_t s) {
-    if (a.nrows <= 0) return hipSuccess;
-    dim3 grid(seg_blocks(a.nrows), a.nseg);
-    if (a.variant == 1) hipLaunchKernelGGL((k_pairs<0, 1>), grid, dim3(FT), 0, s, a);
-    else hipLaunchKernelGGL((k_pairs<0, 0>), grid, dim3(FT), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s) {
-    if (a.nrows <= 0) return hipSuccess;
-    dim3 grid(seg_blocks(a.nrows), a.nseg);
-    if (a.variant == 1) hipLaunchKernelGGL((k_pairs<1, 1>), grid, dim3(FT), 0, s, a);
-    else hipLaunchKernelGGL((k_pairs<1, 0>), grid, dim3(FT), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
-                                  hipStream_t s) {
-    if (nrows <= 0) return hipSuccess;
-    if (ncomp < 1 || ncomp > 3) return hipErrorInvalidValue;
-    dim3 grid((nrows + 255) / 256, ncomp);
-    hipLaunchKernelGGL(k_reduce_segments, grid, dim3(256), 0, s, Fpart, F, nseg, nrows, S, ncomp);
-    return hipGetLastError();
-}
 
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. SC'11): the counter-based stream keyed by (seed, job) with
@@ -663,6 +379,10 @@ __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
         }
     }
     a.R[i] = x; a.R[S + i] = y; a.R[2 * S + i] = z;
+    {
+        const double lo = -0.125 * L, hi = 1.125 * L;
+        if (!(x >= lo && x <= hi && y >= lo && y <= hi && z >= lo && z <= hi)) *a.oor = 1;
+    }
     a.V[i] = vx; a.V[S + i] = vy; a.V[2 * S + i] = vz;
     if (a.do_qt) {
         a.tPart[i] = tPart;
@@ -886,6 +606,8 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
     if (store) {
         if (k == 0) {
             a.R[i] = x; a.R[S + i] = y; a.R[2 * S + i] = z;
+            const double lo = -0.125 * L, hi = 1.125 * L;
+            if (!(x >= lo && x <= hi && y >= lo && y <= hi && z >= lo && z <= hi)) *a.oor = 1;
             a.V[i] = vx; a.V[S + i] = vy; a.V[2 * S + i] = vz;
             if (a.do_qt) a.tPart[i] = tPart;
         }

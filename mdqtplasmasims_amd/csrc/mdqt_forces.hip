@@ -191,11 +191,10 @@ __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restric
 // the two tiles is evaluated once: f goes to i, -f to j (exact: the minimum image and r are
 // sign-symmetric, so f(j,i) == -f(i,j) bit for bit).  Deterministic slots, no atomics.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int gat_i(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
-__device__ __forceinline__ double gat_d(double v, int src) {
-    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
-    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
-    return __hiloint2double(hi, lo);
+// rotate a value by one lane across the whole wave64 (DPP wave_rol:1, VALU latency)
+__device__ __forceinline__ int rot_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x134, 0xF, 0xF, false); }
+__device__ __forceinline__ double rot_d(double v) {
+    return __hiloint2double(rot_i(__double2hiint(v)), rot_i(__double2loint(v)));
 }
 
 template <int VARIANT, bool GUARD>
@@ -203,7 +202,9 @@ __device__ __forceinline__ void n3_body(const N3Args& a, const PairC& c) {
     const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;
     const int l = threadIdx.x & 63;
     const int2 IJ = a.pairs[w];
-    const int I = IJ.x, J = IJ.y;
+    const int I = IJ.x;
+    const int J = a.split == 2 ? (IJ.y >> 1) : IJ.y;
+    const int half = a.split == 2 ? (IJ.y & 1) : 0;  // split 2: an off-diagonal pair in two waves
     const int S = a.S, N = a.N;
     const double* X = a.R;
     const double* Y = a.R + S;
@@ -211,16 +212,17 @@ __device__ __forceinline__ void n3_body(const N3Args& a, const PairC& c) {
     const int i = I * 64 + l;
     const bool vi = i < N;
     const double xi = vi ? X[i] : 0., yi = vi ? Y[i] : 0., zi = vi ? Z[i] : 0.;
-    int jx = J * 64 + l;
+    // the second half of a split pair starts half a turn in: the two halves then meet the
+    // complementary lane offsets whichever way the rotation runs
+    int jx = J * 64 + ((l + 32 * half) & 63);
     double xj = jx < N ? X[jx] : 0., yj = jx < N ? Y[jx] : 0., zj = jx < N ? Z[jx] : 0.;
     double fxi = 0., fyi = 0., fzi = 0., fxj = 0., fyj = 0., fzj = 0.;
-    const int nxt = (l + 1) & 63;
     const bool diag = (I == J);
-    const int nsteps = diag ? 32 : 64;
+    const int nsteps = diag ? 32 : 64 / a.split;
     for (int s = 0; s < nsteps; ++s) {
-        if (diag) {                                 // diagonal: meet lanes l+1 .. l+32 only
-            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
-            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
+        if (diag) {                                 // diagonal: lane distances 1 .. 32 only
+            xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
+            fxj = rot_d(fxj); fyj = rot_d(fyj); fzj = rot_d(fzj);
         }
         const bool on = vi && jx < N && (!diag || s < 31 || l < 32);
         double dx = xi - xj, dy = yi - yj, dz = zi - zj;
@@ -231,13 +233,18 @@ __device__ __forceinline__ void n3_body(const N3Args& a, const PairC& c) {
         fxi += px; fyi += py; fzi += pz;
         fxj -= px; fyj -= py; fzj -= pz;
         if (!diag) {
-            xj = gat_d(xj, nxt); yj = gat_d(yj, nxt); zj = gat_d(zj, nxt); jx = gat_i(jx, nxt);
-            fxj = gat_d(fxj, nxt); fyj = gat_d(fyj, nxt); fzj = gat_d(fzj, nxt);
+            xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
+            fxj = rot_d(fxj); fyj = rot_d(fyj); fzj = rot_d(fzj);
         }
     }
+    // slots: split 1: rows of I -> J (I on the diagonal), rows of J -> I (ntiles on the diagonal)
+    //        split 2: rows of I -> 2J+half, rows of J -> 2I+half (diagonal: 2I and 2I+1)
     const size_t slab3 = (size_t)3 * S;
-    double* Pi = a.P + (size_t)J * slab3;            // rows of I: slot J (I itself on the diagonal)
-    double* Pj = a.P + (size_t)(diag ? a.ntiles : I) * slab3;
+    int si, sj;
+    if (a.split == 2) { si = 2 * J + half; sj = diag ? 2 * I + 1 : 2 * I + half; }
+    else { si = J; sj = diag ? a.ntiles : I; }
+    double* Pi = a.P + (size_t)si * slab3;
+    double* Pj = a.P + (size_t)sj * slab3;
     if (i < S) { Pi[i] = fxi; Pi[S + i] = fyi; Pi[2 * S + i] = fzi; }
     if (jx < S) { Pj[jx] = fxj; Pj[S + jx] = fyj; Pj[2 * S + jx] = fzj; }
 }

@@ -115,8 +115,9 @@ __device__ __forceinline__ double seg_sum(const double* __restrict__ p, size_t s
 struct N3Args {
     const double* R;    // [3][S] (world_size 1)
     double* P;          // [ntiles + 1][3][S]
-    const int2* pairs;  // (I, J) of every wave
+    const int2* pairs;  // (I, J) of every wave; split 2: (I, 2J + half) for off-diagonal pairs
     int N, S, ntiles, npairs;
+    int split;          // 1 or 2 waves per off-diagonal tile pair (2: small N, load balance)
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;          // as ForceArgs::guard
 };

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restric
 // sign-symmetric, so f(j,i) == -f(i,j) bit for bit).  Deterministic slots, no atomics.
 // ------------------------------------------------------------------------------------------
 // rotate a value by one lane across the whole wave64 (DPP wave_rol:1, VALU latency)
-__device__ __forceinline__ int rot_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x134, 0xF, 0xF, false); }
+__device__ __forceinline__ int rot_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x134, 0xF, 0xF, true); }
 __device__ __forceinline__ double rot_d(double v) {
     return __hiloint2double(rot_i(__double2hiint(v)), rot_i(__double2loint(v)));
 }
@@ -219,11 +219,10 @@ __device__ __forceinline__ void n3_body(const N3Args& a, const PairC& c) {
     double fxi = 0., fyi = 0., fzi = 0., fxj = 0., fyj = 0., fzj = 0.;
     const bool diag = (I == J);
     const int nsteps = diag ? 32 : 64 / a.split;
+    if (diag) {                                     // diagonal: lane distances 1 .. 32 only
+        xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
+    }
     for (int s = 0; s < nsteps; ++s) {
-        if (diag) {                                 // diagonal: lane distances 1 .. 32 only
-            xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
-            fxj = rot_d(fxj); fyj = rot_d(fyj); fzj = rot_d(fzj);
-        }
         const bool on = vi && jx < N && (!diag || s < 31 || l < 32);
         double dx = xi - xj, dy = yi - yj, dz = zi - zj;
         mic<GUARD>(dx, dy, dz, c);
@@ -232,10 +231,8 @@ __device__ __forceinline__ void n3_body(const N3Args& a, const PairC& c) {
         const double px = dx * ft, py = dy * ft, pz = dz * ft;
         fxi += px; fyi += py; fzi += pz;
         fxj -= px; fyj -= py; fzj -= pz;
-        if (!diag) {
-            xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
-            fxj = rot_d(fxj); fyj = rot_d(fyj); fzj = rot_d(fzj);
-        }
+        xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
+        fxj = rot_d(fxj); fyj = rot_d(fyj); fzj = rot_d(fzj);
     }
     // slots: split 1: rows of I -> J (I on the diagonal), rows of J -> I (ntiles on the diagonal)
     //        split 2: rows of I -> 2J+half, rows of J -> 2I+half (diagonal: 2I and 2I+1)

@@ -414,8 +414,8 @@ __device__ __forceinline__ cxd gatc(cxd v, int src) { return {gat(v.re, src), ga
 // cross-lane moves for the fixed-pattern sums; exact.
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 #define SHL(n) (0x100 + (n))

@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sharded-config", default="c5", choices=["none", "c3", "c5", "c4"])
     ap.add_argument("--sharded-steps", type=int, default=3)
+    ap.add_argument("--timing-period", type=int, default=8,
+                    help="bracket every k-th kernel launch of the timed region with HIP events")
     return ap.parse_args()
 
 
@@ -104,7 +106,7 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
-    sim.enable_timing(True)
+    sim.enable_timing(args.timing_period)
     t0 = time.perf_counter()
     sim.md_steps(args.steps)
     sim.synchronize()

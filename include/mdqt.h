@@ -160,10 +160,11 @@ int         mdqt_allreduce_sum(mdqt_ctx* c, double* host_buf, size_t n);
  * reference's EkinX/Y/Z terms about vxAvg, [4] = sum over owned i of the full-row pair
  * potential, Pvel partial [3][2001] before normalisation.  Used by the sharded driver. */
 int         mdqt_partial_observables(mdqt_ctx* c, double vxAvg, double out5[5], double* Pvel_partial);
-/* kernel timing: while enabled, every force launch (incl. its segment reduction) and every
- * fused-substep launch is bracketed by HIP events on the context stream; totals() syncs,
- * returns the summed device time (ms) and launch counts since the last call, and resets. */
-int         mdqt_enable_timing(mdqt_ctx* c, int on);
+/* kernel timing: with period k > 0, every k-th force launch and every k-th fused-substep
+ * launch is bracketed by HIP events on the context stream (k = 1: all; 0: off); totals()
+ * syncs, returns the summed device time (ms) and bracketed-launch counts since the last
+ * call, and resets. */
+int         mdqt_enable_timing(mdqt_ctx* c, int period);
 int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
                                     int* nsub);
 

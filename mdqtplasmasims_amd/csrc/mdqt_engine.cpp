@@ -113,6 +113,7 @@ struct mdqt_ctx {
     // per-launch HIP events of the hot kernels (kind 0 = force, 1 = substeps), recorded on
     // the launch stream while timing is on; summed by mdqt_kernel_time_totals
     bool timing = false;
+    unsigned tperiod = 1, tcount[2] = {0, 0};   // bracket every tperiod-th launch of each kind
     std::vector<hipEvent_t> evpool[2];
     int evused[2] = {0, 0};
 };
@@ -739,7 +740,8 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
     if (!s) return fail("NULL context");
     if (s->nloc == 0) return 0;
     HIPCHK(hipSetDevice(s->dev));
-    if (s->timing && mark(s, 0)) return -1;
+    const bool tm = s->timing && (s->tcount[0]++ % s->tperiod == 0);
+    if (tm && mark(s, 0)) return -1;
     if (s->use_n3) {
         N3Args a;
         a.R = s->dR; a.P = s->dFpart; a.pairs = s->dPairs;
@@ -758,7 +760,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         s->f_pending = true;       // summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nseg;
     }
-    if (s->timing && mark(s, 0)) return -1;
+    if (tm && mark(s, 0)) return -1;
     return 0;
 }
 
@@ -795,9 +797,10 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             HIPCHK(launch_d48_resolve(r, s->stream));
             a.U = s->dU;
         }
-        if (s->timing && mark(s, 1)) return -1;
+        const bool tm = s->timing && (s->tcount[1]++ % s->tperiod == 0);
+        if (tm && mark(s, 1)) return -1;
         HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->stream));
-        if (s->timing && mark(s, 1)) return -1;
+        if (tm && mark(s, 1)) return -1;
         if (advance_t) {
             s->t = t;
             s->qidx += (uint64_t)m;
@@ -1236,7 +1239,9 @@ extern "C" int mdqt_positions_device(mdqt_ctx* s, void** dptr, int* S) {
     return 0;
 }
 extern "C" int mdqt_enable_timing(mdqt_ctx* s, int on) {
-    s->timing = on != 0;
+    s->timing = on > 0;
+    s->tperiod = on > 0 ? (unsigned)on : 1u;
+    s->tcount[0] = s->tcount[1] = 0;
     s->evused[0] = s->evused[1] = 0;
     return 0;
 }

@@ -273,8 +273,9 @@ class Simulation:
     def comm_init(self, uid: bytes):
         check(lib().mdqt_comm_init(self.h, uid, len(uid)), "comm_init")
 
-    def enable_timing(self, on: bool = True):
-        check(lib().mdqt_enable_timing(self.h, int(on)))
+    def enable_timing(self, period: int = 1):
+        """bracket every `period`-th hot-kernel launch with HIP events (0/False: off)"""
+        check(lib().mdqt_enable_timing(self.h, int(period)))
 
     def kernel_time_totals(self):
         """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""

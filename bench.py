@@ -57,6 +57,22 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r01_c2_pmc.json")):
+    """HBM bytes per launch of the kernel from the committed rocprofv3 --pmc summary of the same
+    C2 workload (FETCH_SIZE and WRITE_SIZE in separate passes, kB -> B; no gfx950 x2 read
+    correction: the kernel's loads are 8 B/lane, outside the guide's calibrated 16 B/lane case)."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except OSError:
+        return None
+    for k, v in d.items():
+        short = k.split("(")[0].replace("void ", "").replace("mdqt::", "")
+        if short.startswith(kernel_prefix) and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            return (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
+    return None
+
+
 def cpu_baseline(params, qt, seconds, seed, job):
     """The oracle (CPU restatement, race-free OpenMP) on a bounded sample of the same workload."""
     from oracle import oracle as O
@@ -134,8 +150,8 @@ def main():
             ach = bytes_launch / s_avg / 1e9
             flops = F_Q_PER_QSTEP * N * nsub_per_launch
             roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                    "kernel": "k_substeps (fused 25 x step+qstep)",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("k_substeps"),
+                    "kernel": "k_substeps_lanes (fused 25 x step+qstep)" if N < 98304 else "k_substeps",
                     "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
                     "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS}
         else:

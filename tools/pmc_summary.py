@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Per-kernel averages of rocprofv3 --pmc counters (one rocpd database per pass).
+
+    python tools/pmc_summary.py gpurun_out/pmc_fetch/run_results.db gpurun_out/pmc_write/run_results.db ...
+
+Counter values are summed over the rows of one dispatch (per-SE / per-XCD instances), then
+averaged over the dispatches of each kernel.  Prints JSON {kernel: {counter: mean, "dispatches": n}}.
+"""
+import collections
+import json
+import sqlite3
+import sys
+
+
+def load(db):
+    c = sqlite3.connect(db)
+    per = collections.defaultdict(float)   # (kernel, dispatch, counter) -> value
+    for k, d, n, v in c.execute("select kernel_name, dispatch_id, counter_name, value from counters_collection"):
+        per[(k, d, n)] += v
+    return per
+
+
+def main(dbs):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for db in dbs:
+        for (k, d, n), v in load(db).items():
+            agg[k][n].append(v)
+    out = {}
+    for k, cs in agg.items():
+        out[k] = {n: sum(v) / len(v) for n, v in cs.items()}
+        out[k]["dispatches"] = max(len(v) for v in cs.values())
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

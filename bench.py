@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sharded-config", default="c5", choices=["none", "c3", "c5", "c4"])
     ap.add_argument("--sharded-steps", type=int, default=3)
+    ap.add_argument("--qt-math", type=int, default=0, choices=[0, 1],
+                    help="0: the reference's exact QT operations, 1: FMA-contracted (option qt_math)")
     ap.add_argument("--timing-period", type=int, default=8,
                     help="bracket every k-th kernel launch of the timed region with HIP events")
     return ap.parse_args()
@@ -110,6 +112,7 @@ def main():
     params, qt, desc = CONFIGS[args.config]
     job = rank + 1
     sim = M.Simulation(device=local, seed=12345 + job, job=job, qt_enabled=qt, **params).init()
+    sim.set_option("qt_math", args.qt_math)
     N = sim.N
     ratio = int(sim.const("plasmaToQuantumTimestepRatio"))
     sim.md_steps(args.warmup)

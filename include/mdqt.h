@@ -131,7 +131,10 @@ int         mdqt_run(mdqt_ctx* c);                           /* main() time loop
 /* ---- tuning knobs (results are bit-identical across every setting) ----
  *   "substep_kernel": 0 = auto, 1 = thread per ion, 2 = 16-lane group per ion
  *   "force_kernel":   1 = fast reciprocal form (default), 0 = the reference's exact operations
- *                     (the two differ by a few ulp per pair; both meet the 1e-13 force gate) */
+ *                     (the two differ by a few ulp per pair; both meet the 1e-13 force gate)
+ *   "force_scheme":   0 = auto, 1 = owner-computes rows, 2 = Newton-3 tile pairs (one GPU)
+ *   "qt_math":        0 = the reference's exact operations (default), 1 = FMA-contracted with a
+ *                     refined rsq for 1/sqrt(1-dp) (a few ulp per substep; 1e-12 qstep gate) */
 int         mdqt_set_option(mdqt_ctx* c, const char* name, int value);
 
 /* ---- streams, timing, multi-GPU plumbing ---- */

@@ -85,6 +85,7 @@ struct mdqt_ctx {
     LaneTab* dTab = nullptr;       // device copy (uploaded once at create)
     int substep_mode = 0;          // 0 auto, 1 thread-per-ion, 2 lane-per-state
     int force_variant = 1;         // 0 exact reference operations, 1 fast reciprocal form
+    int qt_math = 0;               // 0 exact reference operations, 1 FMA-contracted (option "qt_math")
     bool f_pending = false;        // dFpart holds unreduced force partials (pend_nseg > 1)
     int pend_nseg = 1;             // partial count of the pending forces (segments or slots)
     int scheme_opt = 0;            // force scheme: 0 auto, 1 rows (owner computes), 2 Newton-3 tiles
@@ -793,13 +794,13 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             D48Args r;
             r.psi = s->dPsi; r.n = s->nloc; r.S = s->S;
             r.state = s->dX48; r.jA = s->dX48 + 1; r.jC = s->dX48 + 49;
-            r.U = s->dU; r.qc = s->qc;
+            r.U = s->dU; r.qc = s->qc; r.fast = s->qt_math;
             HIPCHK(launch_d48_resolve(r, s->stream));
             a.U = s->dU;
         }
         const bool tm = s->timing && (s->tcount[1]++ % s->tperiod == 0);
         if (tm && mark(s, 1)) return -1;
-        HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->stream));
+        HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream));
         if (tm && mark(s, 1)) return -1;
         if (advance_t) {
             s->t = t;
@@ -1209,6 +1210,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         s->scheme_opt = value;
         choose_segments(s);
         return ensure_aux(s);
+    }
+    if (!strcmp(name, "qt_math")) {
+        if (value < 0 || value > 1) return fail("qt_math must be 0 (exact) or 1 (FMA-contracted)");
+        s->qt_math = value;
+        return 0;
     }
     if (!strcmp(name, "force_kernel")) {
         if (value < 0 || value > 1) return fail("force_kernel must be 0 (exact) or 1 (fast)");

@@ -132,6 +132,7 @@ struct D48Args {
     const unsigned long long* jA;   // [48] multiplier of 2^b steps
     const unsigned long long* jC;   // [48] increment of 2^b steps
     double* U;                 // out: [5][S]
+    int fast;                  // qt_math of the substep kernel (dp must be bit-identical)
     QTConst qc;
 };
 hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s);
@@ -145,7 +146,8 @@ hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[
 // mode: 0 = auto (lane-per-state below kLaneKernelMaxIons ions, thread-per-ion above),
 //       1 = thread-per-ion, 2 = lane-per-state.  Both are bit-identical.
 constexpr int kLaneKernelMaxIons = 98304;
-hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, hipStream_t s);
+// fast: qt_math 1 (FMA contraction, refined rsq) instead of the reference's exact operations
+hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s);
 // deterministic sums: out[0] = sum vx; needs scratch >= 1024 doubles
 hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s);
 // out[0..2] = sum 0.5 (vx-avg)^2, 0.5 vy^2, 0.5 vz^2 ; out[3] = sum of rows[0..nrows) of

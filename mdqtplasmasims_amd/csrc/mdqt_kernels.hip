@@ -98,7 +98,9 @@ __global__ __launch_bounds__(1024) void k_d48_resolve(D48Args a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double re = a.psi[(size_t)(2 * (q + 2)) * S + i], im = a.psi[(size_t)(2 * (q + 2) + 1) * S + i];
-                T[q] = (re * qc.dP[q]) * re + (im * qc.dP[q]) * im;
+                // exactly decay_term<F> of the substep kernels (same jump decisions)
+                T[q] = a.fast ? fma(re * qc.dP[q], re, (im * qc.dP[q]) * im)
+                              : (re * qc.dP[q]) * re + (im * qc.dP[q]) * im;
             }
             const double dp = qc.h * (((T[0] + T[1]) + T[2]) + T[3]);     // exactly dp_of / row_sum_p
             jmp = !(u1 > dp);
@@ -171,12 +173,49 @@ __device__ __forceinline__ cxd cmul(cxd a, cxd b) {   // std::complex<double> op
 }
 __device__ __forceinline__ cxd cadd(cxd a, cxd b) { return {a.re + b.re, a.im + b.im}; }
 
+// The two QT arithmetic modes (option "qt_math"): F = false keeps the reference's operations
+// without contraction (bit-identical to the oracle up to sin/cos ulps); F = true contracts into
+// FMAs and takes 1/sqrt(1 - dp) from a refined v_rsq_f64 (a few ulp per operation).
+template <bool F>
+__device__ __forceinline__ cxd cmulT(cxd a, cxd b) {
+    if (F) return {fma(a.re, b.re, -(a.im * b.im)), fma(a.re, b.im, a.im * b.re)};
+    return cmul(a, b);
+}
+template <bool F>
+__device__ __forceinline__ double decay_term(cxd y, double d) {   // (re d) re + (im d) im
+    if (F) return fma(y.re * d, y.re, (y.im * d) * y.im);
+    return (y.re * d) * y.re + (y.im * d) * y.im;
+}
+template <bool F>
+__device__ __forceinline__ double inv_sqrt_1m(double dp) {        // 1 / sqrt(1 - dp) (:532)
+    if (F) {
+        const double x = 1 - dp;
+        double r = __builtin_amdgcn_rsq(x);
+        const double hx = 0.5 * x;
+        r = r * fma(-hx * r, r, 1.5);
+        r = r * fma(-hx * r, r, 1.5);
+        return r;
+    }
+    return 1 / sqrt(1 - dp);
+}
+template <bool F>
+__device__ __forceinline__ double axpy(double a, double x, double y) {   // y + a x
+    if (F) return fma(a, x, y);
+    return y + a * x;
+}
+template <bool F>
+__device__ __forceinline__ double kstage(double invh, double pref, double ws, double y) {
+    if (F) return invh * fma(pref, ws, -y);                         // invh (pref ws - y)
+    return invh * (pref * ws - y);
+}
+
 // Re(h * y^H D y) with D = decayMatrix (diagonal, P levels only): SpeedUp:484-485, :530-531
+template <bool F>
 __device__ __forceinline__ double dp_of(const QTConst& qc, const cxd* y) {
-    double v = (y[2].re * qc.dP[0]) * y[2].re + (y[2].im * qc.dP[0]) * y[2].im;
-    v = v + ((y[3].re * qc.dP[1]) * y[3].re + (y[3].im * qc.dP[1]) * y[3].im);
-    v = v + ((y[4].re * qc.dP[2]) * y[4].re + (y[4].im * qc.dP[2]) * y[4].im);
-    v = v + ((y[5].re * qc.dP[3]) * y[5].re + (y[5].im * qc.dP[3]) * y[5].im);
+    double v = decay_term<F>(y[2], qc.dP[0]);
+    v = v + decay_term<F>(y[3], qc.dP[1]);
+    v = v + decay_term<F>(y[4], qc.dP[2]);
+    v = v + decay_term<F>(y[5], qc.dP[3]);
     return qc.h * v;
 }
 
@@ -184,21 +223,24 @@ __device__ __forceinline__ double dp_of(const QTConst& qc, const cxd* y) {
 
 // out = M y, M sparse (App. A); terms summed in ascending column order as the dense
 // Armadillo product (exact zero terms dropped: they cannot change a non-zero sum).
+template <bool F>
 __device__ __forceinline__ void matvec(const QTConst& qc, const cxd* Md, const cxd& M49,
                                        const cxd& M58, const cxd& M85, const cxd& M94,
                                        const cxd* y, cxd* o) {
-    o[0] = cadd(cadd(cmul(Md[0], y[0]), cmul(MS(0), y[3])), cmul(MS(1), y[5]));
-    o[1] = cadd(cadd(cmul(Md[1], y[1]), cmul(MS(2), y[2])), cmul(MS(3), y[4]));
-    o[2] = cadd(cadd(cadd(cmul(MS(4), y[1]), cmul(Md[2], y[2])), cmul(MS(5), y[9])), cmul(MS(6), y[11]));
-    o[3] = cadd(cadd(cadd(cmul(MS(7), y[0]), cmul(Md[3], y[3])), cmul(MS(8), y[8])), cmul(MS(9), y[10]));
-    o[4] = cadd(cadd(cadd(cmul(MS(10), y[1]), cmul(Md[4], y[4])), cmul(MS(11), y[7])), cmul(M49, y[9]));
-    o[5] = cadd(cadd(cadd(cmul(MS(12), y[0]), cmul(Md[5], y[5])), cmul(MS(13), y[6])), cmul(M58, y[8]));
-    o[6] = cadd(cmul(MS(14), y[5]), cmul(Md[6], y[6]));
-    o[7] = cadd(cmul(MS(15), y[4]), cmul(Md[7], y[7]));
-    o[8] = cadd(cadd(cmul(MS(16), y[3]), cmul(M85, y[5])), cmul(Md[8], y[8]));
-    o[9] = cadd(cadd(cmul(MS(17), y[2]), cmul(M94, y[4])), cmul(Md[9], y[9]));
-    o[10] = cadd(cmul(MS(18), y[3]), cmul(Md[10], y[10]));
-    o[11] = cadd(cmul(MS(19), y[2]), cmul(Md[11], y[11]));
+#define CM cmulT<F>
+    o[0] = cadd(cadd(CM(Md[0], y[0]), CM(MS(0), y[3])), CM(MS(1), y[5]));
+    o[1] = cadd(cadd(CM(Md[1], y[1]), CM(MS(2), y[2])), CM(MS(3), y[4]));
+    o[2] = cadd(cadd(cadd(CM(MS(4), y[1]), CM(Md[2], y[2])), CM(MS(5), y[9])), CM(MS(6), y[11]));
+    o[3] = cadd(cadd(cadd(CM(MS(7), y[0]), CM(Md[3], y[3])), CM(MS(8), y[8])), CM(MS(9), y[10]));
+    o[4] = cadd(cadd(cadd(CM(MS(10), y[1]), CM(Md[4], y[4])), CM(MS(11), y[7])), CM(M49, y[9]));
+    o[5] = cadd(cadd(cadd(CM(MS(12), y[0]), CM(Md[5], y[5])), CM(MS(13), y[6])), CM(M58, y[8]));
+    o[6] = cadd(CM(MS(14), y[5]), CM(Md[6], y[6]));
+    o[7] = cadd(CM(MS(15), y[4]), CM(Md[7], y[7]));
+    o[8] = cadd(cadd(CM(MS(16), y[3]), CM(M85, y[5])), CM(Md[8], y[8]));
+    o[9] = cadd(cadd(CM(MS(17), y[2]), CM(M94, y[4])), CM(Md[9], y[9]));
+    o[10] = cadd(CM(MS(18), y[3]), CM(Md[10], y[10]));
+    o[11] = cadd(CM(MS(19), y[2]), CM(Md[11], y[11]));
+#undef CM
 }
 
 __device__ __forceinline__ double rho_im(cxd a, cxd b) {   // Im(a * conj(b)), SpeedUp:490-502
@@ -206,12 +248,13 @@ __device__ __forceinline__ double rho_im(cxd a, cxd b) {   // Im(a * conj(b)), S
 }
 
 // One ion through qstep() (SpeedUp:478-712).  Returns the velocity kick.
+template <bool F>
 __device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double vx,
                                             double& tPart, cxd* w, uint64_t gid, uint64_t q,
                                             const double* U, int S, int i) {
     const double velQuant = vx * qc.pv2q;                                  // :481-482
     tPart += qc.dtQ;                                                        // :483
-    const double dp = dp_of(qc, w);                                         // :484-485
+    const double dp = dp_of<F>(qc, w);                                      // :484-485
     double u1, u2;
     draw_pair(qc, U, S, i, gid, q, 0, u1, u2);                              // :486
     double kick;
@@ -261,21 +304,21 @@ __device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double
         for (int k = 0; k < NS; ++k) y[k] = w[k];
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
-            const double pref = 1 / sqrt(1 - (st == 0 ? dp : dp_of(qc, y)));
-            matvec(qc, Md, M49, M58, M85, M94, y, ws);
+            const double pref = inv_sqrt_1m<F>(st == 0 ? dp : dp_of<F>(qc, y));
+            matvec<F>(qc, Md, M49, M58, M85, M94, y, ws);
             const double step = (st == 2) ? h : qc.dtHalf;
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
-                const cxd kk = {qc.invh * (pref * ws[k].re - y[k].re), qc.invh * (pref * ws[k].im - y[k].im)};
+                const cxd kk = {kstage<F>(qc.invh, pref, ws[k].re, y[k].re), kstage<F>(qc.invh, pref, ws[k].im, y[k].im)};
                 if (st == 0) {
                     acc[k] = kk;
                 } else if (st < 3) {
-                    acc[k] = {acc[k].re + 3. * kk.re, acc[k].im + 3. * kk.im};
+                    acc[k] = {axpy<F>(3., kk.re, acc[k].re), axpy<F>(3., kk.im, acc[k].im)};
                 } else {
                     const cxd sum = {acc[k].re + kk.re, acc[k].im + kk.im};
-                    w[k] = {w[k].re + h * (sum.re / 8), w[k].im + h * (sum.im / 8)};
+                    w[k] = {axpy<F>(h, sum.re / 8, w[k].re), axpy<F>(h, sum.im / 8, w[k].im)};
                 }
-                if (st < 3) y[k] = {w[k].re + step * kk.re, w[k].im + step * kk.im};
+                if (st < 3) y[k] = {axpy<F>(step, kk.re, w[k].re), axpy<F>(step, kk.im, w[k].im)};
             }
         }
     } else {                                                                // :573-703
@@ -325,6 +368,7 @@ __device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double
     return kick;
 }
 
+template <bool F>
 __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
@@ -374,7 +418,7 @@ __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
             }
         }
         if (a.do_qt) {
-            const double kick = qstep_ion(a.qc, a.expDet[s], vx, tPart, w, gid, a.q0 + (uint64_t)s, a.U, S, i);
+            const double kick = qstep_ion<F>(a.qc, a.expDet[s], vx, tPart, w, gid, a.q0 + (uint64_t)s, a.U, S, i);
             vx = vx + kick;                                      // :705
         }
     }
@@ -430,6 +474,7 @@ __device__ __forceinline__ double row_sum_p(double T) {
     return dpp<BCAST(2)>(a);
 }
 
+template <bool F>
 __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const LaneTab* __restrict__ tab) {
     const int lane = threadIdx.x & 63;
     const int k = lane & 15;                          // state index (valid when < 12)
@@ -495,7 +540,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
         const double eD = a.expDet[s];
         const double velQuant = vx * qc.pv2q;
         tPart += qc.dtQ;
-        const double Tk = (w.re * dPk) * w.re + (w.im * dPk) * w.im;
+        const double Tk = decay_term<F>(w, dPk);
         const double dp = qc.h * row_sum_p(Tk);
         double u1, u2;
         draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 0, u1, u2);
@@ -533,14 +578,14 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
             for (int stg = 0; stg < 4; ++stg) {
                 double dpy = dp;
                 if (stg > 0) {
-                    const double Ty = (yv.re * dPk) * yv.re + (yv.im * dPk) * yv.im;
+                    const double Ty = decay_term<F>(yv, dPk);
                     dpy = qc.h * row_sum_p(Ty);
                     yA = gatc(yv, srcA);
                     yB = gatc(yv, srcB);
                 }
                 const cxd yC = gatc(yv, srcC);
-                const double pref = 1 / sqrt(1 - dpy);
-                const cxd tA = cmul(cA, yA), tB = cmul(cB, yB), tC = cmul(cC, yC), tD = cmul(Md, yv);
+                const double pref = inv_sqrt_1m<F>(dpy);
+                const cxd tA = cmulT<F>(cA, yA), tB = cmulT<F>(cB, yB), tC = cmulT<F>(cC, yC), tD = cmulT<F>(Md, yv);
                 // ascending-column row sum (order patterns of LaneTab)
                 const cxd second = (order == 3) ? tB : tD;
                 const cxd third = (order == 3) ? tD : tB;
@@ -548,16 +593,16 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
                 if (hasB) ws = cadd(ws, third);
                 if (hasC) ws = cadd(ws, tC);
                 const double step = (stg == 2) ? h : qc.dtHalf;
-                const cxd kk = {qc.invh * (pref * ws.re - yv.re), qc.invh * (pref * ws.im - yv.im)};
+                const cxd kk = {kstage<F>(qc.invh, pref, ws.re, yv.re), kstage<F>(qc.invh, pref, ws.im, yv.im)};
                 if (stg == 0) {
                     acc = kk;
                 } else if (stg < 3) {
-                    acc = {acc.re + 3. * kk.re, acc.im + 3. * kk.im};
+                    acc = {axpy<F>(3., kk.re, acc.re), axpy<F>(3., kk.im, acc.im)};
                 } else {
                     const cxd sum = {acc.re + kk.re, acc.im + kk.im};
-                    w = {w.re + h * (sum.re / 8), w.im + h * (sum.im / 8)};
+                    w = {axpy<F>(h, sum.re / 8, w.re), axpy<F>(h, sum.im / 8, w.im)};
                 }
-                if (stg < 3) yv = {w.re + step * kk.re, w.im + step * kk.im};
+                if (stg < 3) yv = {axpy<F>(step, kk.re, w.re), axpy<F>(step, kk.im, w.im)};
             }
         } else {                                      // quantum jump (:573-703)
             tPart = 0;
@@ -618,11 +663,17 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
     }
 }
 
-hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, hipStream_t s) {
+hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s) {
     if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
-    if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes, dim3((a.n + 15) / 16), dim3(256), 0, s, a, tab);
-    else hipLaunchKernelGGL(k_substeps, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256);
+    if (fast) {
+        if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes<true>, gl, dim3(256), 0, s, a, tab);
+        else hipLaunchKernelGGL(k_substeps<true>, gt, dim3(256), 0, s, a);
+    } else {
+        if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes<false>, gl, dim3(256), 0, s, a, tab);
+        else hipLaunchKernelGGL(k_substeps<false>, gt, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -147,10 +147,12 @@ def _evolved_state(orc, N0=300, seed=21, nmd=4):
     return o
 
 
-def test_qstep_matches_oracle(eng, orc):
+@pytest.mark.parametrize("qt_math", [0, 1])
+def test_qstep_matches_oracle(eng, orc, qt_math):
     o = _evolved_state(orc)
     st = o.get_state()
     s = eng.Simulation(N0=300, seed=21, rng_mode=1)
+    s.set_option("qt_math", qt_math)
     s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
     s.set_forces(st["F"])
     s.qstep_index = o.qstep_index
@@ -188,10 +190,11 @@ def test_qstep_jump_branch_exercised(eng, orc):
     assert np.abs(a["V"] - b["V"]).max() < 1e-12
 
 
-@pytest.mark.parametrize("qt", [1, 0])
-def test_md_steps_short_horizon(eng, orc, qt):
+@pytest.mark.parametrize("qt,qt_math", [(1, 0), (1, 1), (0, 0)])
+def test_md_steps_short_horizon(eng, orc, qt, qt_math):
     kw = dict(N0=500, seed=77, rng_mode=1, qt_enabled=qt)
     s = eng.Simulation(**kw).init()
+    s.set_option("qt_math", qt_math)
     o = orc.OracleSim(nthreads=8, **kw).init()
     s.md_steps(3); o.md_steps(3)
     a, b = s.get_state(), o.get_state()
@@ -225,12 +228,14 @@ def test_substeps_fusion_equals_single_substeps(eng):
 
 @pytest.mark.parametrize("N0,extra", [(500, {}), (3500, {}), (300, dict(Om=3.0, OmDP=2.0, reNormalizewvFns=1)),
                                       (300, dict(fracOfSig=0.4, detuningDP=-0.5))])
-def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra):
+@pytest.mark.parametrize("qt_math", [0, 1])
+def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra, qt_math):
     """k_substeps_lanes (16 lanes per ion) performs exactly k_substeps' operations"""
     sims = []
     for mode in (1, 2):
         s = eng.Simulation(N0=N0, seed=31, **extra).init()
         s.set_option("substep_kernel", mode)
+        s.set_option("qt_math", qt_math)
         s.md_steps(3)
         sims.append(s.get_state())
     a, b = sims

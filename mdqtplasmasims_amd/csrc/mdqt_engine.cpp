@@ -85,7 +85,7 @@ struct mdqt_ctx {
     LaneTab* dTab = nullptr;       // device copy (uploaded once at create)
     int substep_mode = 0;          // 0 auto, 1 thread-per-ion, 2 lane-per-state
     int force_variant = 1;         // 0 exact reference operations, 1 fast reciprocal form
-    int qt_math = 0;               // 0 exact reference operations, 1 FMA-contracted (option "qt_math")
+    int qt_math = 1;               // 0 exact reference operations, 1 FMA-contracted (option "qt_math")
     bool f_pending = false;        // dFpart holds unreduced force partials (pend_nseg > 1)
     int pend_nseg = 1;             // partial count of the pending forces (segments or slots)
     int scheme_opt = 0;            // force scheme: 0 auto, 1 rows (owner computes), 2 Newton-3 tiles

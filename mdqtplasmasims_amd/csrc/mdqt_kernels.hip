@@ -514,6 +514,18 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
     const double dt = qc.dtQ;
     const double DT = 0.5 * dt;
     const uint64_t gid = a.gid0 + (uint64_t)i;
+    // Philox draws u1, u2 of all substeps of the launch up front, lane k taking substeps k and
+    // k + 16 (the per-substep chain then only reads LDS; jump draws stay on demand)
+    __shared__ double su[16][MAXSUB][2];
+    if (a.do_qt && !a.U) {
+        for (int s = k; s < a.nsub; s += 16) {
+            double p, q;
+            philox_pair(qc, gid, a.q0 + (uint64_t)s, 0, p, q);
+            su[threadIdx.x >> 4][s][0] = p;
+            su[threadIdx.x >> 4][s][1] = q;
+        }
+    }
+    __syncthreads();
     for (int s = 0; s < a.nsub; ++s) {
         if (a.do_step) {                              // step(), as in k_substeps
             const bool moving = a.t[s] > 0;
@@ -543,7 +555,13 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
         const double Tk = decay_term<F>(w, dPk);
         const double dp = qc.h * row_sum_p(Tk);
         double u1, u2;
-        draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 0, u1, u2);
+        if (a.U) {
+            u1 = a.U[i];
+            u2 = a.U[(size_t)S + i];
+        } else {
+            u1 = su[threadIdx.x >> 4][s][0];
+            u2 = su[threadIdx.x >> 4][s][1];
+        }
         const cxd wA = gatc(w, srcA), wB = gatc(w, srcB);
         double kick;
         if (u1 > dp) {

@@ -251,6 +251,7 @@ def test_drand48_reference_order_matches_oracle(eng, orc, N0, extra):
     reference-order restatement"""
     kw = dict(N0=N0, seed=12346, rng_mode=0, **extra)
     s = eng.Simulation(**kw).init()
+    s.set_option("qt_math", 0)                  # the reference's exact operations
     o = orc.OracleSim(**kw).init()
     assert s.drand48_state == orc.lib().orc_get_drand48_state(o.h)
     s.md_steps(4); o.md_steps(4)

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libmdqt.so")
+# MDQT_LIB: an alternative build of the same library (kernel A/B experiments, tools/expt.sh)
+LIB_PATH = os.environ.get("MDQT_LIB") or os.path.join(HERE, "lib", "libmdqt.so")
 CLI_PATH = os.path.join(HERE, "bin", "mdqt")
 
 _dp = C.POINTER(C.c_double)

@@ -209,6 +209,54 @@ __device__ __forceinline__ double kstage(double invh, double pref, double ws, do
     return invh * (pref * ws - y);
 }
 
+// 1 / sqrt(x) (F) or the reference's division by sqrt(x): the renormalisation of :706-712
+template <bool F>
+__device__ __forceinline__ cxd renorm_div(cxd w, double sumsq) {
+    if (F) {
+        double r = __builtin_amdgcn_rsq(sumsq);
+        const double hx = 0.5 * sumsq;
+        r = r * fma(-hx * r, r, 1.5);
+        r = r * fma(-hx * r, r, 1.5);
+        return {w.re * r, w.im * r};
+    }
+    const double nrm = sqrt(sumsq);
+    return {w.re / nrm, w.im / nrm};
+}
+
+// sin and cos of the time-dependent coupling phase (:508).  F = false: the math library's
+// sincos.  F = true: Cody-Waite reduction by pi/2 (three-part constant, FMA) and the classic
+// minimax kernels on [-pi/4, pi/4] (fdlibm's __kernel_sin/__kernel_cos coefficients, < 1 ulp),
+// about a third of the library's instruction count; |x| >= 2^20 takes the library path.
+#ifndef MDQT_FAST_SINCOS
+#define MDQT_FAST_SINCOS 1
+#endif
+template <bool F>
+__device__ __forceinline__ void sincos_q(double x, double& sn, double& cs) {
+    if (!F || !MDQT_FAST_SINCOS || !(fabs(x) < 1048576.)) {
+        sincos(x, &sn, &cs);
+        return;
+    }
+    const double n = rint(x * 0.63661977236758134308);           // 2/pi
+    double r = fma(-n, 1.57079632679489655800e+00, x);            // pi/2 = P1 + P2 + P3
+    r = fma(-n, 6.12323399573676603587e-17, r);
+    r = fma(-n, -1.49738490485916983014e-33, r);
+    const double z = r * r;
+    const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                         2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                          8.33333333332248946124e-03);
+    const double sr = fma(r * z, fma(z, ps, -1.66666666666666324348e-01), r);
+    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                 -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                                  -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+    const double hz = 0.5 * z;
+    const double wc = 1.0 - hz;
+    const double cr = wc + (((1.0 - wc) - hz) + z * pc);
+    const int q = (int)n & 3;
+    const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+    sn = (q & 2) ? -s0 : s0;
+    cs = ((q + 1) & 2) ? -c0 : c0;
+}
+
 // Re(h * y^H D y) with D = decayMatrix (diagonal, P levels only): SpeedUp:484-485, :530-531
 template <bool F>
 __device__ __forceinline__ double dp_of(const QTConst& qc, const cxd* y) {
@@ -278,7 +326,7 @@ __device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double
         const double E89 = (-qc.det + qc.detDP - velQuant - eD - qc.kRat * (velQuant + eD));
         const double phi = 2. * vq * (1 + qc.kRat) * tPart * qc.gamToE;   // :508
         double sn, cs;
-        sincos(phi, &sn, &cs);
+        sincos_q<F>(phi, sn, cs);
         const double h = qc.h;
         cxd Md[NS];
         Md[0] = {1., -(h * 0.)};
@@ -361,9 +409,9 @@ __device__ __forceinline__ double qstep_ion(const QTConst& qc, double eD, double
         for (int k = 2; k < 6; ++k) popP = popP + (w[k].re * w[k].re + w[k].im * w[k].im);
 #pragma unroll
         for (int k = 6; k < 12; ++k) popD = popD + (w[k].re * w[k].re + w[k].im * w[k].im);
-        const double nrm = sqrt(popS + popP + popD);
+        const double tot = popS + popP + popD;
 #pragma unroll
-        for (int k = 0; k < NS; ++k) w[k] = {w[k].re / nrm, w[k].im / nrm};
+        for (int k = 0; k < NS; ++k) w[k] = renorm_div<F>(w[k], tot);
     }
     return kick;
 }
@@ -456,6 +504,18 @@ __device__ __forceinline__ cxd gatc(cxd v, int src) { return {gat(v.re, src), ga
 // DPP moves inside a 16-lane row (one ion): row_shl:n (lane l reads lane l+n), row_shr:n
 // (lane l reads lane l-n), row_newbcast:n (every lane reads lane n of its row).  VALU-latency
 // cross-lane moves for the fixed-pattern sums; exact.
+// Row gathers of the sparse matvec through LDS (one ds_write_b128 + three ds_read_b128 per
+// exchange) instead of twelve ds_bpermute_b32; the 16-lane group lives in one wave, whose LDS
+// operations execute in order, so a wave-scope fence is the only synchronisation needed.
+#ifndef MDQT_GATHER_LDS
+#define MDQT_GATHER_LDS 1
+#endif
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
@@ -486,7 +546,9 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
     const QTConst& qc = a.qc;
     const int S = a.S;
     // per-lane row structure of M and kick weights
+#if !MDQT_GATHER_LDS
     const int srcA = g0 + tab->colA[k], srcB = g0 + tab->colB[k], srcC = g0 + tab->colC[k];
+#endif
     const int order = tab->order[k], hasB = tab->hasB[k], hasC = tab->hasC[k];
     const int dynB = tab->dynB[k], dynC = tab->dynC[k];
     const cxd cA = {tab->cAre[k], tab->cAim[k]};
@@ -526,6 +588,22 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
         }
     }
     __syncthreads();
+#if MDQT_GATHER_LDS
+    __shared__ double2 xg[256];
+    const int ldsA = (threadIdx.x & ~15) + tab->colA[k], ldsB = (threadIdx.x & ~15) + tab->colB[k],
+              ldsC = (threadIdx.x & ~15) + tab->colC[k];
+    auto exchange = [&](cxd v, cxd& A, cxd& B, cxd& C) {
+        wave_sync();
+        xg[threadIdx.x] = make_double2(v.re, v.im);
+        wave_sync();
+        const double2 ta = xg[ldsA], tb = xg[ldsB], tc = xg[ldsC];
+        A = {ta.x, ta.y}; B = {tb.x, tb.y}; C = {tc.x, tc.y};
+    };
+#else
+    auto exchange = [&](cxd v, cxd& A, cxd& B, cxd& C) {
+        A = gatc(v, srcA); B = gatc(v, srcB); C = gatc(v, srcC);
+    };
+#endif
     for (int s = 0; s < a.nsub; ++s) {
         if (a.do_step) {                              // step(), as in k_substeps
             const bool moving = a.t[s] > 0;
@@ -562,7 +640,8 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
             u1 = su[threadIdx.x >> 4][s][0];
             u2 = su[threadIdx.x >> 4][s][1];
         }
-        const cxd wA = gatc(w, srcA), wB = gatc(w, srcB);
+        cxd wA, wB, wC;
+        exchange(w, wA, wB, wC);
         double kick;
         if (u1 > dp) {
             // optical kick from the pre-step density matrix (:490-503)
@@ -586,22 +665,20 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
             const cxd Md = {(k >= 2 && k < 6) ? 1. + h * hdk : 1., -(h * E)};
             const double phi = 2. * vq * (1 + qc.kRat) * tPart * qc.gamToE;
             double sn, cs;
-            sincos(phi, &sn, &cs);
+            sincos_q<F>(phi, sn, cs);
             const double as = dynScale * sn, ac = dynScale * cs;
             if (dynB) cB = {-(h * as), h * ac};       // M85 / M94
             if (dynC) cC = {h * as, h * ac};          // M58 / M49
             cxd yv = w, acc = {0., 0.};
-            cxd yA = wA, yB = wB;
+            cxd yA = wA, yB = wB, yC = wC;
 #pragma unroll
             for (int stg = 0; stg < 4; ++stg) {
                 double dpy = dp;
                 if (stg > 0) {
                     const double Ty = decay_term<F>(yv, dPk);
                     dpy = qc.h * row_sum_p(Ty);
-                    yA = gatc(yv, srcA);
-                    yB = gatc(yv, srcB);
+                    exchange(yv, yA, yB, yC);
                 }
-                const cxd yC = gatc(yv, srcC);
                 const double pref = inv_sqrt_1m<F>(dpy);
                 const cxd tA = cmulT<F>(cA, yA), tB = cmulT<F>(cB, yB), tC = cmulT<F>(cC, yC), tD = cmulT<F>(Md, yv);
                 // ascending-column row sum (order patterns of LaneTab)
@@ -653,16 +730,15 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
             w = {k == target ? 1. : 0., 0.};
         }
         if (qc.renorm) {                              // :706-712
+            // (popS + popP) + popD with popS = n0 + n1, popP = ((n2 + n3) + n4) + n5,
+            // popD = ((((n6 + n7) + n8) + n9) + n10) + n11: row shifts build the three partial
+            // chains at lanes 0, 2 and 6 at once, broadcasts combine them (k_substeps' order)
             const double nk = w.re * w.re + w.im * w.im;
-            const double popS = gat(nk, g0 + 0) + gat(nk, g0 + 1);
-            double popP = gat(nk, g0 + 2);
-#pragma unroll
-            for (int q = 3; q < 6; ++q) popP = popP + gat(nk, g0 + q);
-            double popD = gat(nk, g0 + 6);
-#pragma unroll
-            for (int q = 7; q < 12; ++q) popD = popD + gat(nk, g0 + q);
-            const double nrm = sqrt(popS + popP + popD);
-            w = {w.re / nrm, w.im / nrm};
+            const double c1 = nk + dpp<SHL(1)>(nk);
+            const double c3 = (c1 + dpp<SHL(2)>(nk)) + dpp<SHL(3)>(nk);
+            const double c5 = (c3 + dpp<SHL(4)>(nk)) + dpp<SHL(5)>(nk);
+            const double tot = (dpp<BCAST(0)>(c1) + dpp<BCAST(2)>(c3)) + dpp<BCAST(6)>(c5);
+            w = renorm_div<F>(w, tot);
         }
         vx = vx + kick;
     }

@@ -52,8 +52,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sharded-config", default="c5", choices=["none", "c3", "c5", "c4"])
     ap.add_argument("--sharded-steps", type=int, default=3)
-    ap.add_argument("--qt-math", type=int, default=1, choices=[0, 1],
-                    help="0: the reference's exact QT operations, 1: FMA-contracted (option qt_math)")
+    ap.add_argument("--qt-math", type=int, default=2, choices=[0, 1, 2],
+                    help="0: the reference's exact QT operations, 1: FMA-contracted, 2: reassociated "
+                         "(option qt_math, the library default)")
     ap.add_argument("--timing-period", type=int, default=8,
                     help="bracket every k-th kernel launch of the timed region with HIP events")
     return ap.parse_args()

@@ -128,13 +128,16 @@ int         mdqt_write_conditions(mdqt_ctx* c, int c0);      /* writeConditions,
 int         mdqt_read_conditions(mdqt_ctx* c, int c0);       /* readConditions,  :785-916       */
 int         mdqt_run(mdqt_ctx* c);                           /* main() time loop, :1139-1383    */
 
-/* ---- tuning knobs (results are bit-identical across every setting) ----
+/* ---- tuning knobs ----
  *   "substep_kernel": 0 = auto, 1 = thread per ion, 2 = 16-lane group per ion
  *   "force_kernel":   1 = fast reciprocal form (default), 0 = the reference's exact operations
  *                     (the two differ by a few ulp per pair; both meet the 1e-13 force gate)
  *   "force_scheme":   0 = auto, 1 = owner-computes rows, 2 = Newton-3 tile pairs (one GPU)
- *   "qt_math":        0 = the reference's exact operations (default), 1 = FMA-contracted with a
- *                     refined rsq for 1/sqrt(1-dp) (a few ulp per substep; 1e-12 qstep gate) */
+ *   "qt_math":        0 = the reference's exact operations, 1 = FMA-contracted with a refined
+ *                     rsq for 1/sqrt(1-dp), 2 = reassociated (default: fixed FMA chains per row
+ *                     of M, folded constants; ~3x fewer instructions per substep).  1 and 2
+ *                     differ from 0 by rounding only (1e-12 qstep gate); substep_kernel settings
+ *                     are bit-identical to each other within one qt_math mode */
 int         mdqt_set_option(mdqt_ctx* c, const char* name, int value);
 
 /* ---- streams, timing, multi-GPU plumbing ---- */

@@ -83,9 +83,11 @@ struct mdqt_ctx {
     int kdeChunks = 0;
     LaneTab tab;                   // lane-per-state QT kernel tables (host copy)
     LaneTab* dTab = nullptr;       // device copy (uploaded once at create)
+    FastTab ftab;                  // qt_math 2 row tables (host copy)
+    FastTab* dFTab = nullptr;      // device copy
     int substep_mode = 0;          // 0 auto, 1 thread-per-ion, 2 lane-per-state
     int force_variant = 1;         // 0 exact reference operations, 1 fast reciprocal form
-    int qt_math = 1;               // 0 exact reference operations, 1 FMA-contracted (option "qt_math")
+    int qt_math = 2;               // 0 exact reference operations, 1 FMA-contracted, 2 reassociated (option "qt_math")
     bool f_pending = false;        // dFpart holds unreduced force partials (pend_nseg > 1)
     int pend_nseg = 1;             // partial count of the pending forces (segments or slots)
     int scheme_opt = 0;            // force scheme: 0 auto, 1 rows (owner computes), 2 Newton-3 tiles
@@ -278,6 +280,50 @@ static void build_constants(mdqt_ctx* s) {
     t.gA[1] = gs[0]; t.gA[0] = gs[2]; t.gB[1] = gs[4]; t.gB[0] = gs[5];
     t.gB[8] = gs[8]; t.gB[9] = gs[11]; t.gA[10] = gs[14]; t.gA[11] = gs[17];
     t.gA[6] = gs[6]; t.gA[7] = gs[9]; t.gA[8] = gs[12]; t.gA[9] = gs[15];
+    // qt_math 2 tables (mdqt_qtfast.hip): slots of kFastCol, constants folded
+    FastTab& f = s->ftab;
+    memset(&f, 0, sizeof f);
+    const double h = q.h;
+    for (int k = 0; k < 16; ++k)
+        for (int j = 0; j < 3; ++j) f.col[j][k] = k < NS ? kFastCol[k][j] : k;
+    for (int k = 0; k < NS; ++k) {
+        for (int j = 0; j < 3; ++j) {
+            const int c = kFastCol[k][j];
+            if (c == k) continue;                  // unused slot
+            const int e = static_idx(k, c);
+            if (e >= 0) { f.cre[j][k] = q.Mre[e]; f.cim[j][k] = q.Mim[e]; }
+        }
+        const bool P = k >= 2 && k < 6;
+        f.mre[k] = P ? 1. + h * q.hdP[k - 2] : 1.;
+        f.hdp[k] = P ? h * q.dP[k - 2] : 0.;
+        // E_k = e0 + e1 u (:506-510); Im M_kk = -h E_k
+        double e0 = 0., e1 = 0.;
+        if (k >= 2) e0 = (k < 6) ? -q.det : -q.det + q.detDP;
+        if (k == 2 || k == 3) e1 = -1.;
+        else if (k == 4 || k == 5) e1 = 1.;
+        else if (k == 6 || k == 7) e1 = 1. - q.kRat;
+        else if (k == 8 || k == 9) e1 = -(1. + q.kRat);
+        else if (k >= 10) e1 = q.kRat - 1.;
+        f.mi0[k] = -(h * e0);
+        f.mi1[k] = -(h * e1);
+    }
+    // time-dependent slot 2: M85, M94 = h a {-sin, cos}; M58, M49 = h a {sin, cos} (:508)
+    f.dms[8] = -(h * q.a8);  f.dmc[8] = h * q.a8;
+    f.dms[9] = -(h * q.a11); f.dmc[9] = h * q.a11;
+    f.dms[5] = h * q.a8;     f.dmc[5] = h * q.a8;
+    f.dms[4] = h * q.a11;    f.dmc[4] = h * q.a11;
+    // kick weights of Im(w_k conj(w_c)) (:503), scale kickS/kickD * dtQ * gamToE folded in
+    const double kS = q.kickS * q.dtQ * q.gamToE, kD = q.kickD * q.dtQ * q.gamToE;
+    struct KW { int row, col, g; double sgn, scale; };
+    const KW kws[12] = {{1, 2, 0, 1., kS},  {0, 3, 2, 1., kS},  {1, 4, 4, -1., kS}, {0, 5, 5, -1., kS},
+                        {8, 5, 8, 1., kD},  {9, 4, 11, 1., kD}, {10, 3, 14, 1., kD}, {11, 2, 17, 1., kD},
+                        {6, 5, 6, -1., kD}, {7, 4, 9, -1., kD}, {8, 3, 12, -1., kD}, {9, 2, 15, -1., kD}};
+    for (const KW& w : kws)
+        for (int j = 0; j < 3; ++j)
+            if (kFastCol[w.row][j] == w.col) f.kw[j][w.row] = w.sgn * (w.scale * gs[w.g]);
+    f.cphi = 2. * (1. + q.kRat) * q.gamToE;
+    f.dt2 = (0.5 * q.dtQ) * (0.5 * q.dtQ);
+    for (int k = 0; k < 4; ++k) q.hdPh[k] = f.hdp[2 + k];
 }
 
 static double expDetuning_of(const mdqt_params* p, double t) {   // :447
@@ -432,7 +478,10 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
         return fail("cannot create HIP stream on device %d", p->device);
     }
     s->stream = s->own;
-    if (hipMalloc(&s->dTab, sizeof(LaneTab)) != hipSuccess) { mdqt_destroy(s); return fail("hipMalloc lane table"); }
+    if (hipMalloc(&s->dTab, sizeof(LaneTab)) != hipSuccess || hipMalloc(&s->dFTab, sizeof(FastTab)) != hipSuccess) {
+        mdqt_destroy(s);
+        return fail("hipMalloc lane tables");
+    }
     {
         const int f[2] = {0, 1};
         if (hipMalloc(&s->dFlags, sizeof f) != hipSuccess ||
@@ -457,7 +506,8 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
             return fail("drand48 state upload failed");
         }
     }
-    if (hipMemcpy(s->dTab, &s->tab, sizeof(LaneTab), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(s->dTab, &s->tab, sizeof(LaneTab), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s->dFTab, &s->ftab, sizeof(FastTab), hipMemcpyHostToDevice) != hipSuccess) {
         mdqt_destroy(s);
         return fail("upload of the lane table failed");
     }
@@ -476,6 +526,7 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     free_device(s);
     if (s->dTab) (void)hipFree(s->dTab);
+    if (s->dFTab) (void)hipFree(s->dFTab);
     if (s->dComm) (void)hipFree(s->dComm);
     if (s->dX48) (void)hipFree(s->dX48);
     if (s->dFlags) (void)hipFree(s->dFlags);
@@ -800,7 +851,8 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         }
         const bool tm = s->timing && (s->tcount[1]++ % s->tperiod == 0);
         if (tm && mark(s, 1)) return -1;
-        HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream));
+        if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->substep_mode, s->stream));
+        else HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream));
         if (tm && mark(s, 1)) return -1;
         if (advance_t) {
             s->t = t;
@@ -1212,7 +1264,7 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         return ensure_aux(s);
     }
     if (!strcmp(name, "qt_math")) {
-        if (value < 0 || value > 1) return fail("qt_math must be 0 (exact) or 1 (FMA-contracted)");
+        if (value < 0 || value > 2) return fail("qt_math must be 0 (exact), 1 (FMA-contracted) or 2 (reassociated)");
         s->qt_math = value;
         return 0;
     }

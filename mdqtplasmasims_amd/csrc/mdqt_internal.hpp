@@ -31,6 +31,7 @@ struct QTConst {
     double pD;                  // r/(r+1): D-decay branch probability (:589)
     double dP[4];               // decayMatrix diagonal on P levels 2..5 (:1203)
     double hdP[4];              // imag of hamDecayTerm diagonal on P levels (:1202)
+    double hdPh[4];             // h dP[k]: qt_math 2 form of dp (= FastTab::hdp of the P levels)
     double a8, a11;             // OmDP/2*gs[8]/sqrt(r), OmDP/2*gs[11]/sqrt(r) (:508)
     double Mre[NSTATIC], Mim[NSTATIC];   // static off-diagonal M entries
     double thS3, thS4;          // gs[2]^2, gs[4]^2 (S-decay target thresholds)
@@ -53,6 +54,25 @@ struct LaneTab {
     double gA[16], gB[16];       // optical-kick weights of rho_im(w_k, w_colA/colB) (:503)
     double dP[16];               // decayMatrix diagonal (0 off the P levels)
     double hd[16];               // imag of hamDecayTerm diagonal (0 off the P levels)
+};
+
+// qt_math 2 (reassociated QT arithmetic, mdqt_qtfast.hip): row k of M = I - i h H as its
+// diagonal plus three off-diagonal slots with source states kFastCol[k][t] (unused slots point
+// at k itself with a zero coefficient; the time-dependent entry of rows 4, 5, 8, 9 sits in slot
+// 2).  Both QT kernels evaluate every row as the same fixed FMA chain over these slots, so the
+// thread-per-ion and lane-per-state forms stay bit-identical.
+constexpr int kFastCol[NS][3] = {{3, 5, 0}, {2, 4, 1},  {1, 9, 11}, {0, 8, 10}, {1, 7, 9},   {0, 6, 8},
+                                 {5, 6, 6}, {4, 7, 7}, {3, 8, 5},   {2, 9, 4},  {3, 10, 10}, {2, 11, 11}};
+struct FastTab {
+    int col[3][16];              // kFastCol, lanes 12..15 point at themselves
+    double cre[3][16], cim[3][16];   // static M entries of the slots (0 for unused / dynamic)
+    double dms[16], dmc[16];     // slot 2 += {dms sin(phi), dmc cos(phi)} (rows 4, 5, 8, 9)
+    double mre[16];              // Re M_kk = 1 + h Im(hamDecayTerm_kk)
+    double mi0[16], mi1[16];     // Im M_kk = mi0 + mi1 u, u = velQuant + expDetuning (:506-510)
+    double hdp[16];              // h decayMatrix_kk (P levels), 0 elsewhere: dp = sum hdp |y|^2
+    double kw[3][16];            // optical-kick weight of Im(y_k conj(y_slot)), sign and scale folded (:503)
+    double cphi;                 // 2 (1 + kRat) gamToE: phi = u cphi tPart (:508)
+    double dt2;                  // (dtQ/2)^2 of step_R's first substep (:372-378)
 };
 
 struct SubstepArgs {
@@ -132,7 +152,7 @@ struct D48Args {
     const unsigned long long* jA;   // [48] multiplier of 2^b steps
     const unsigned long long* jC;   // [48] increment of 2^b steps
     double* U;                 // out: [5][S]
-    int fast;                  // qt_math of the substep kernel (dp must be bit-identical)
+    int fast;                  // qt_math of the substep kernel (0, 1, 2: dp must be bit-identical)
     QTConst qc;
 };
 hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s);
@@ -148,6 +168,8 @@ hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[
 constexpr int kLaneKernelMaxIons = 98304;
 // fast: qt_math 1 (FMA contraction, refined rsq) instead of the reference's exact operations
 hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s);
+// qt_math 2: the reassociated kernels of mdqt_qtfast.hip (same modes as launch_substeps)
+hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s);
 // deterministic sums: out[0] = sum vx; needs scratch >= 1024 doubles
 hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s);
 // out[0..2] = sum 0.5 (vx-avg)^2, 0.5 vy^2, 0.5 vz^2 ; out[3] = sum of rows[0..nrows) of

@@ -8,58 +8,11 @@
 // Built with -ffp-contract=off and without fast-math: every floating-point expression keeps
 // the reference's operation order (x86-64 g++ -O3 contracts nothing), so the only
 // device/host differences left are libm ulps (exp, sin, cos).  See DESIGN.md §Parity.
-#include "mdqt_internal.hpp"
+#include "mdqt_device.hpp"
 
 #include <math.h>
 
 namespace mdqt {
-
-// ------------------------------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al. SC'11): the counter-based stream keyed by (seed, job) with
-// counter (global ion, qstep index, draw pair); layout in DESIGN.md §RNG (the parity tests
-// check it against the CPU restatement's stream).
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                              uint32_t k0, uint32_t k1, uint32_t o[4]) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
-        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-    o[0] = c0; o[1] = c1; o[2] = c2; o[3] = c3;
-}
-
-__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
-    const uint64_t b = ((((uint64_t)hi) << 32) | lo) >> 11;
-    return (double)b * 0x1.0p-53;
-}
-
-// draws 2p and 2p+1 of (ion, q)
-__device__ __forceinline__ void philox_pair(const QTConst& qc, uint64_t ion, uint64_t q, int p,
-                                            double& ua, double& ub) {
-    uint32_t o[4];
-    philox4x32_10((uint32_t)ion, (uint32_t)q, (uint32_t)(q >> 32),
-                  ((uint32_t)(ion >> 32) << 8) | (uint32_t)p, qc.seed, qc.job, o);
-    ua = u53(o[0], o[1]);
-    ub = u53(o[2], o[3]);
-}
-
-// uniforms 2p, 2p+1 of local ion i at substep (gid, q): the precomputed drand48 reference-order
-// values when U is given (rng_mode 0), else the Philox stream
-__device__ __forceinline__ void draw_pair(const QTConst& qc, const double* U, int S, int i, uint64_t gid,
-                                          uint64_t q, int p, double& ua, double& ub) {
-    if (U) {
-        ua = U[(size_t)(2 * p) * S + i];
-        ub = (2 * p + 1 < 5) ? U[(size_t)(2 * p + 1) * S + i] : 0.;
-    } else {
-        philox_pair(qc, gid, q, p, ua, ub);
-    }
-}
 
 // ------------------------------------------------------------------------------------------
 // drand48 in the reference's consumption order (SpeedUp:486, :575-687).  X' = a X + c mod 2^48;
@@ -98,11 +51,13 @@ __global__ __launch_bounds__(1024) void k_d48_resolve(D48Args a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double re = a.psi[(size_t)(2 * (q + 2)) * S + i], im = a.psi[(size_t)(2 * (q + 2) + 1) * S + i];
-                // exactly decay_term<F> of the substep kernels (same jump decisions)
-                T[q] = a.fast ? fma(re * qc.dP[q], re, (im * qc.dP[q]) * im)
-                              : (re * qc.dP[q]) * re + (im * qc.dP[q]) * im;
+                // exactly the dp of the substep kernel that consumes U (same jump decisions)
+                if (a.fast == 2) T[q] = fma(re, re, im * im) * qc.hdPh[q];
+                else if (a.fast == 1) T[q] = fma(re * qc.dP[q], re, (im * qc.dP[q]) * im);
+                else T[q] = (re * qc.dP[q]) * re + (im * qc.dP[q]) * im;
             }
-            const double dp = qc.h * (((T[0] + T[1]) + T[2]) + T[3]);     // exactly dp_of / row_sum_p
+            const double dp = (a.fast == 2) ? (T[0] + T[1]) + (T[2] + T[3])          // mdqt_qtfast.hip
+                                            : qc.h * (((T[0] + T[1]) + T[2]) + T[3]); // dp_of / row_sum_p
             jmp = !(u1 > dp);
             a.U[i] = u1;
         }
@@ -166,97 +121,6 @@ hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s) {
 // state (R, V, F, psi, tPart) held in registers across the nsub substeps of one launch
 // (legal: between forces() calls no ion reads another ion).
 // ------------------------------------------------------------------------------------------
-struct cxd { double re, im; };
-
-__device__ __forceinline__ cxd cmul(cxd a, cxd b) {   // std::complex<double> operator*
-    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
-}
-__device__ __forceinline__ cxd cadd(cxd a, cxd b) { return {a.re + b.re, a.im + b.im}; }
-
-// The two QT arithmetic modes (option "qt_math"): F = false keeps the reference's operations
-// without contraction (bit-identical to the oracle up to sin/cos ulps); F = true contracts into
-// FMAs and takes 1/sqrt(1 - dp) from a refined v_rsq_f64 (a few ulp per operation).
-template <bool F>
-__device__ __forceinline__ cxd cmulT(cxd a, cxd b) {
-    if (F) return {fma(a.re, b.re, -(a.im * b.im)), fma(a.re, b.im, a.im * b.re)};
-    return cmul(a, b);
-}
-template <bool F>
-__device__ __forceinline__ double decay_term(cxd y, double d) {   // (re d) re + (im d) im
-    if (F) return fma(y.re * d, y.re, (y.im * d) * y.im);
-    return (y.re * d) * y.re + (y.im * d) * y.im;
-}
-template <bool F>
-__device__ __forceinline__ double inv_sqrt_1m(double dp) {        // 1 / sqrt(1 - dp) (:532)
-    if (F) {
-        const double x = 1 - dp;
-        double r = __builtin_amdgcn_rsq(x);
-        const double hx = 0.5 * x;
-        r = r * fma(-hx * r, r, 1.5);
-        r = r * fma(-hx * r, r, 1.5);
-        return r;
-    }
-    return 1 / sqrt(1 - dp);
-}
-template <bool F>
-__device__ __forceinline__ double axpy(double a, double x, double y) {   // y + a x
-    if (F) return fma(a, x, y);
-    return y + a * x;
-}
-template <bool F>
-__device__ __forceinline__ double kstage(double invh, double pref, double ws, double y) {
-    if (F) return invh * fma(pref, ws, -y);                         // invh (pref ws - y)
-    return invh * (pref * ws - y);
-}
-
-// 1 / sqrt(x) (F) or the reference's division by sqrt(x): the renormalisation of :706-712
-template <bool F>
-__device__ __forceinline__ cxd renorm_div(cxd w, double sumsq) {
-    if (F) {
-        double r = __builtin_amdgcn_rsq(sumsq);
-        const double hx = 0.5 * sumsq;
-        r = r * fma(-hx * r, r, 1.5);
-        r = r * fma(-hx * r, r, 1.5);
-        return {w.re * r, w.im * r};
-    }
-    const double nrm = sqrt(sumsq);
-    return {w.re / nrm, w.im / nrm};
-}
-
-// sin and cos of the time-dependent coupling phase (:508).  F = false: the math library's
-// sincos.  F = true: Cody-Waite reduction by pi/2 (three-part constant, FMA) and the classic
-// minimax kernels on [-pi/4, pi/4] (fdlibm's __kernel_sin/__kernel_cos coefficients, < 1 ulp),
-// about a third of the library's instruction count; |x| >= 2^20 takes the library path.
-#ifndef MDQT_FAST_SINCOS
-#define MDQT_FAST_SINCOS 1
-#endif
-template <bool F>
-__device__ __forceinline__ void sincos_q(double x, double& sn, double& cs) {
-    if (!F || !MDQT_FAST_SINCOS || !(fabs(x) < 1048576.)) {
-        sincos(x, &sn, &cs);
-        return;
-    }
-    const double n = rint(x * 0.63661977236758134308);           // 2/pi
-    double r = fma(-n, 1.57079632679489655800e+00, x);            // pi/2 = P1 + P2 + P3
-    r = fma(-n, 6.12323399573676603587e-17, r);
-    r = fma(-n, -1.49738490485916983014e-33, r);
-    const double z = r * r;
-    const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
-                                         2.75573137070700676789e-06), -1.98412698298579493134e-04),
-                          8.33333333332248946124e-03);
-    const double sr = fma(r * z, fma(z, ps, -1.66666666666666324348e-01), r);
-    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
-                                                 -2.75573143513906633035e-07), 2.48015872894767294178e-05),
-                                  -1.38888888888741095749e-03), 4.16666666666666019037e-02);
-    const double hz = 0.5 * z;
-    const double wc = 1.0 - hz;
-    const double cr = wc + (((1.0 - wc) - hz) + z * pc);
-    const int q = (int)n & 3;
-    const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
-    sn = (q & 2) ? -s0 : s0;
-    cs = ((q + 1) & 2) ? -c0 : c0;
-}
-
 // Re(h * y^H D y) with D = decayMatrix (diagonal, P levels only): SpeedUp:484-485, :530-531
 template <bool F>
 __device__ __forceinline__ double dp_of(const QTConst& qc, const cxd* y) {
@@ -289,10 +153,6 @@ __device__ __forceinline__ void matvec(const QTConst& qc, const cxd* Md, const c
     o[10] = cadd(CM(MS(18), y[3]), CM(Md[10], y[10]));
     o[11] = cadd(CM(MS(19), y[2]), CM(Md[11], y[11]));
 #undef CM
-}
-
-__device__ __forceinline__ double rho_im(cxd a, cxd b) {   // Im(a * conj(b)), SpeedUp:490-502
-    return a.re * (-b.im) + a.im * b.re;
 }
 
 // One ion through qstep() (SpeedUp:478-712).  Returns the velocity kick.
@@ -494,46 +354,6 @@ __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
 // k_substeps performs, in the same order (cross-lane moves are exact), so the two kernels
 // are bit-identical — tests/test_gpu_parity.py checks it.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ double gat(double v, int src) {
-    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
-    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ cxd gatc(cxd v, int src) { return {gat(v.re, src), gat(v.im, src)}; }
-
-// DPP moves inside a 16-lane row (one ion): row_shl:n (lane l reads lane l+n), row_shr:n
-// (lane l reads lane l-n), row_newbcast:n (every lane reads lane n of its row).  VALU-latency
-// cross-lane moves for the fixed-pattern sums; exact.
-// Row gathers of the sparse matvec through LDS (one ds_write_b128 + three ds_read_b128 per
-// exchange) instead of twelve ds_bpermute_b32; the 16-lane group lives in one wave, whose LDS
-// operations execute in order, so a wave-scope fence is the only synchronisation needed.
-#ifndef MDQT_GATHER_LDS
-#define MDQT_GATHER_LDS 1
-#endif
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int CTRL>
-__device__ __forceinline__ double dpp(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
-    return __hiloint2double(hi, lo);
-}
-#define SHL(n) (0x100 + (n))
-#define SHR(n) (0x110 + (n))
-#define BCAST(n) (0x150 + (n))
-
-// ((T2 + T3) + T4) + T5 of the ion's lanes 2..5, in every lane of the row
-__device__ __forceinline__ double row_sum_p(double T) {
-    double a = T + dpp<SHL(1)>(T);
-    a = a + dpp<SHL(2)>(T);
-    a = a + dpp<SHL(3)>(T);
-    return dpp<BCAST(2)>(a);
-}
-
 template <bool F>
 __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const LaneTab* __restrict__ tab) {
     const int lane = threadIdx.x & 63;

@@ -1,0 +1,384 @@
+// qt_math 2: the fused step()+qstep() substeps (SpeedUp:356-430, :438-717) with reassociated
+// arithmetic, for throughput.  Same algorithm as mdqt_kernels.hip's k_substeps/_lanes, but
+// every quantity is evaluated in the form that needs the fewest dependent instructions:
+//
+//   * row k of M = I - i h H is ONE fixed FMA chain: diagonal, then three off-diagonal slots
+//     (FastTab; zero coefficients where a row has fewer entries), instead of the dense
+//     product's ascending-column order;
+//   * the RK stages work on d = s - y with s = M y / sqrt(1 - dp(y)) (k = d / h): y1 = w + d1/2,
+//     y2 = w + d2/2, y3 = w + d3, w' = w + (d1 + 3 d2 + 3 d3 + d4)/8 — the reference's
+//     k1 + 3k2 + 3k3 + k4 propagator (:525-567) without the 1/h and h factors;
+//   * dp, the optical kick and the renormalisation norm are fixed-shape trees (the lane
+//     kernel's DPP tree order), constants folded on the host (kick scale, h dP, 2(1+kRat)gamToE);
+//   * step(): one coordinate per lane (lanes 0..11 and 14..15 x, 12 y, 13 z), exact operations.
+//
+// Results differ from the exact mode (qt_math 0) by rounding only (~1e-15 relative per
+// substep; tests/test_gpu_parity.py bounds it against the oracle).  The thread-per-ion and
+// lane-per-state kernels below perform the same operations in the same order: bit-identical.
+#include "mdqt_device.hpp"
+
+#include <math.h>
+
+namespace mdqt {
+
+__device__ __forceinline__ double rsq_nr(double x) {   // 1/sqrt(x): v_rsq_f64 + 2 Newton steps
+    double r = __builtin_amdgcn_rsq(x);
+    const double hx = 0.5 * x;
+    r = r * fma(-hx * r, r, 1.5);
+    r = r * fma(-hx * r, r, 1.5);
+    return r;
+}
+__device__ __forceinline__ double nrm2(cxd y) { return fma(y.re, y.re, y.im * y.im); }
+__device__ __forceinline__ double rho_im_r(cxd a, cxd b) { return fma(a.im, b.re, -(a.re * b.im)); }
+
+// M_kk y + c0 y0 + c1 y1 + c2 y2, one chain per component
+__device__ __forceinline__ cxd row_r(cxd md, cxd y, cxd c0, cxd y0, cxd c1, cxd y1, cxd c2, cxd y2) {
+    double re = md.re * y.re, im = md.re * y.im;
+    re = fma(-md.im, y.im, re);  im = fma(md.im, y.re, im);
+    re = fma(c0.re, y0.re, re);  im = fma(c0.re, y0.im, im);
+    re = fma(-c0.im, y0.im, re); im = fma(c0.im, y0.re, im);
+    re = fma(c1.re, y1.re, re);  im = fma(c1.re, y1.im, im);
+    re = fma(-c1.im, y1.im, re); im = fma(c1.im, y1.re, im);
+    re = fma(c2.re, y2.re, re);  im = fma(c2.re, y2.im, im);
+    re = fma(-c2.im, y2.im, re); im = fma(c2.im, y2.re, im);
+    return {re, im};
+}
+
+__device__ __forceinline__ double kick_term(cxd w, cxd w0, cxd w1, cxd w2, double k0, double k1, double k2) {
+    return fma(rho_im_r(w, w0), k0, fma(rho_im_r(w, w1), k1, rho_im_r(w, w2) * k2));
+}
+
+// sum of 16 values in the lane kernel's DPP tree order (row_shl 1, 2, 4, 8)
+__device__ __forceinline__ double tree16(const double* v) {
+    return (((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]))) +
+           (((v[8] + v[9]) + (v[10] + v[11])) + ((v[12] + v[13]) + (v[14] + v[15])));
+}
+__device__ __forceinline__ double lane_tree16(double v) {
+    double a = v + dpp<SHL(1)>(v);
+    a = a + dpp<SHL(2)>(a);
+    a = a + dpp<SHL(4)>(a);
+    a = a + dpp<SHL(8)>(a);
+    return dpp<BCAST(0)>(a);
+}
+// (T2 + T3) + (T4 + T5) of the ion's lanes 2..5, in every lane of the row
+__device__ __forceinline__ double lane_sum_p(double T) {
+    double a = T + dpp<SHL(1)>(T);
+    a = a + dpp<SHL(2)>(a);
+    return dpp<BCAST(2)>(a);
+}
+
+// step_R(dt/2) of one coordinate (:356-389), the reference's operations (step() stays bit-exact
+// in every qt_math mode); `moving` = t > 0 (:360)
+__device__ __forceinline__ double half_drift(double p, double v, double f, bool moving, double DT,
+                                             double DT2, double L) {
+    p = moving ? p + DT * v : p + (DT * v + DT2 * f);
+    if (p < 0) p += L;
+    if (p > L) p -= L;
+    return p;
+}
+
+// the quantum jump (:573-703), the exact-mode operations of mdqt_kernels.hip
+__device__ __forceinline__ int jump_target(const QTConst& qc, double n3, double n4, double n5, double n6,
+                                           double rand2, double randDOrS, double randDir, double rand3,
+                                           double& kick) {
+    const double tot = n3 + n4 + n5 + n6;
+    const double prob3 = n3 / tot, prob4 = n4 / tot, prob5 = n5 / tot;
+    const bool sDecay = !(randDOrS < qc.pD);
+    if (!sDecay) kick = (randDir < 0.5) ? qc.vKickDP : -qc.vKickDP;
+    else kick = (randDir < 0.5) ? qc.vKick : -qc.vKick;
+    if (rand2 < prob3) {
+        if (sDecay) return 1;
+        return (rand3 < qc.thD[0][0]) ? 11 : (rand3 < qc.thD[0][1]) ? 10 : 9;
+    } else if (rand2 < prob3 + prob4) {
+        if (sDecay) return (rand3 < qc.thS3) ? 0 : 1;
+        return (rand3 < qc.thD[1][0]) ? 10 : (rand3 < qc.thD[1][1]) ? 9 : 8;
+    } else if (rand2 < prob3 + prob4 + prob5) {
+        if (sDecay) return (rand3 < qc.thS4) ? 1 : 0;
+        return (rand3 < qc.thD[2][0]) ? 9 : (rand3 < qc.thD[2][1]) ? 8 : 7;
+    }
+    if (sDecay) return 0;
+    return (rand3 < qc.thD[3][0]) ? 8 : (rand3 < qc.thD[3][1]) ? 7 : 6;
+}
+
+__device__ __forceinline__ double sq(cxd y) { return y.re * y.re + y.im * y.im; }
+
+// ------------------------------------------------------------------------------------------
+// thread per ion
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab* __restrict__ tab) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const QTConst& qc = a.qc;
+    const FastTab& T = *tab;
+    const int S = a.S;
+    double P[3], Vv[3], Fv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        P[c] = a.R[(size_t)c * S + i];
+        Vv[c] = a.V[(size_t)c * S + i];
+        if (a.nseg > 1) {
+            Fv[c] = seg_sum(a.Fpart + (size_t)c * S + i, (size_t)3 * S, a.nseg);
+            a.F[(size_t)c * S + i] = Fv[c];
+        } else {
+            Fv[c] = a.F[(size_t)c * S + i];
+        }
+    }
+    double tPart = a.tPart[i];
+    cxd w[NS];
+    if (a.do_qt) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) w[k] = {a.psi[(size_t)(2 * k) * S + i], a.psi[(size_t)(2 * k + 1) * S + i]};
+    }
+    const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt, DT2 = T.dt2;
+    const uint64_t gid = a.gid0 + (uint64_t)i;
+    for (int s = 0; s < a.nsub; ++s) {
+        if (a.do_step) {
+            const bool moving = a.t[s] > 0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                P[c] = half_drift(P[c], Vv[c], Fv[c], moving, DT, DT2, L);
+                Vv[c] = Vv[c] + dt * Fv[c];
+                P[c] = half_drift(P[c], Vv[c], Fv[c], moving, DT, DT2, L);
+            }
+        }
+        if (!a.do_qt) continue;
+        const double u = Vv[0] * qc.pv2q + a.expDet[s];
+        tPart += qc.dtQ;
+        double Tp[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Tp[q] = nrm2(w[2 + q]) * T.hdp[2 + q];
+        const double dp = (Tp[0] + Tp[1]) + (Tp[2] + Tp[3]);
+        double u1, u2;
+        draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 0, u1, u2);
+        double kick;
+        if (u1 > dp) {
+            double kv[16];
+#pragma unroll
+            for (int k = 0; k < NS; ++k)
+                kv[k] = kick_term(w[k], w[kFastCol[k][0]], w[kFastCol[k][1]], w[kFastCol[k][2]], T.kw[0][k],
+                                  T.kw[1][k], T.kw[2][k]);
+#pragma unroll
+            for (int k = NS; k < 16; ++k) kv[k] = 0.;
+            kick = tree16(kv);
+            const double phi = (u * T.cphi) * tPart;
+            double sn, cs;
+            sincos_q<true>(phi, sn, cs);
+            cxd md[NS], c2[NS];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                md[k] = {T.mre[k], fma(T.mi1[k], u, T.mi0[k])};
+                c2[k] = {fma(T.dms[k], sn, T.cre[2][k]), fma(T.dmc[k], cs, T.cim[2][k])};
+            }
+            cxd y[NS], acc[NS];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) y[k] = w[k];
+#pragma unroll
+            for (int stg = 0; stg < 4; ++stg) {
+                double dpy = dp;
+                if (stg > 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) Tp[q] = nrm2(y[2 + q]) * T.hdp[2 + q];
+                    dpy = (Tp[0] + Tp[1]) + (Tp[2] + Tp[3]);
+                }
+                const double pref = rsq_nr(1. - dpy);
+                cxd ws[NS];
+#pragma unroll
+                for (int k = 0; k < NS; ++k)
+                    ws[k] = row_r(md[k], y[k], cxd{T.cre[0][k], T.cim[0][k]}, y[kFastCol[k][0]],
+                                  cxd{T.cre[1][k], T.cim[1][k]}, y[kFastCol[k][1]], c2[k], y[kFastCol[k][2]]);
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    const cxd d = {fma(pref, ws[k].re, -y[k].re), fma(pref, ws[k].im, -y[k].im)};
+                    if (stg == 0) acc[k] = d;
+                    else if (stg < 3) acc[k] = {fma(3., d.re, acc[k].re), fma(3., d.im, acc[k].im)};
+                    else acc[k] = {acc[k].re + d.re, acc[k].im + d.im};
+                    if (stg < 2) y[k] = {fma(0.5, d.re, w[k].re), fma(0.5, d.im, w[k].im)};
+                    else if (stg == 2) y[k] = {w[k].re + d.re, w[k].im + d.im};
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NS; ++k) w[k] = {fma(0.125, acc[k].re, w[k].re), fma(0.125, acc[k].im, w[k].im)};
+        } else {
+            tPart = 0;
+            double randDOrS, randDir, rand3, dummy;
+            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
+            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
+            (void)dummy;
+            const int target = jump_target(qc, sq(w[2]), sq(w[3]), sq(w[4]), sq(w[5]), u2, randDOrS, randDir,
+                                           rand3, kick);
+#pragma unroll
+            for (int k = 0; k < NS; ++k) w[k] = {k == target ? 1. : 0., 0.};
+        }
+        if (qc.renorm) {                                                    // :706-712
+            double nv[16];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) nv[k] = nrm2(w[k]);
+#pragma unroll
+            for (int k = NS; k < 16; ++k) nv[k] = 0.;
+            const double r = rsq_nr(tree16(nv));
+#pragma unroll
+            for (int k = 0; k < NS; ++k) w[k] = {w[k].re * r, w[k].im * r};
+        }
+        Vv[0] = fma(1., kick, Vv[0]);                                       // :705
+    }
+    const double lo = -0.125 * L, hi = 1.125 * L;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        a.R[(size_t)c * S + i] = P[c];
+        a.V[(size_t)c * S + i] = Vv[c];
+        if (!(P[c] >= lo && P[c] <= hi)) *a.oor = 1;
+    }
+    if (a.do_qt) {
+        a.tPart[i] = tPart;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            a.psi[(size_t)(2 * k) * S + i] = w[k].re;
+            a.psi[(size_t)(2 * k + 1) * S + i] = w[k].im;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// lane per state: one ion per 16-lane group (4 per wave64), lane k = state k.  The integrator
+// coordinate of a lane is x for lanes 0..11, 14, 15 (so every state lane has vx locally), y for
+// lane 12 and z for lane 13.  Lanes 12..15 carry zero amplitudes and zero coefficients.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
+    const int k = threadIdx.x & 15;
+    const int grp = threadIdx.x >> 4;
+    const int iraw = blockIdx.x * 16 + grp;
+    const bool store = iraw < a.n;
+    const int i = store ? iraw : a.n - 1;             // idle groups shadow the last ion
+    const QTConst& qc = a.qc;
+    const int S = a.S;
+    const int c = (k == 12) ? 1 : (k == 13) ? 2 : 0;
+    const bool owner = (k == 0) || (k == 12) || (k == 13);   // stores coordinate c
+    const int base = threadIdx.x & ~15;
+    const int l0 = base + tab->col[0][k], l1 = base + tab->col[1][k], l2 = base + tab->col[2][k];
+    const cxd c0 = {tab->cre[0][k], tab->cim[0][k]}, c1 = {tab->cre[1][k], tab->cim[1][k]};
+    const double c2re = tab->cre[2][k], c2im = tab->cim[2][k], dms = tab->dms[k], dmc = tab->dmc[k];
+    const double mre = tab->mre[k], mi0 = tab->mi0[k], mi1 = tab->mi1[k], hdp = tab->hdp[k];
+    const double kw0 = tab->kw[0][k], kw1 = tab->kw[1][k], kw2 = tab->kw[2][k];
+    const double cphi = tab->cphi, DT2 = tab->dt2;
+    const double kmask = (c == 0) ? 1. : 0.;
+    double p = a.R[(size_t)c * S + i], v = a.V[(size_t)c * S + i], f;
+    if (a.nseg > 1) {
+        f = seg_sum(a.Fpart + (size_t)c * S + i, (size_t)3 * S, a.nseg);
+        if (store && owner) a.F[(size_t)c * S + i] = f;
+    } else {
+        f = a.F[(size_t)c * S + i];
+    }
+    double tPart = a.tPart[i];
+    cxd w = {0., 0.};
+    if (a.do_qt && k < NS) w = {a.psi[(size_t)(2 * k) * S + i], a.psi[(size_t)(2 * k + 1) * S + i]};
+    const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
+    const uint64_t gid = a.gid0 + (uint64_t)i;
+    __shared__ double su[16][MAXSUB][2];
+    if (a.do_qt && !a.U) {
+        for (int s = k; s < a.nsub; s += 16) {
+            double x0, x1;
+            philox_pair(qc, gid, a.q0 + (uint64_t)s, 0, x0, x1);
+            su[grp][s][0] = x0;
+            su[grp][s][1] = x1;
+        }
+    }
+    __syncthreads();
+    __shared__ double2 xg[256];
+    auto exchange = [&](cxd y, cxd& y0, cxd& y1, cxd& y2) {
+        wave_sync();
+        xg[threadIdx.x] = make_double2(y.re, y.im);
+        wave_sync();
+        const double2 t0 = xg[l0], t1 = xg[l1], t2 = xg[l2];
+        y0 = {t0.x, t0.y}; y1 = {t1.x, t1.y}; y2 = {t2.x, t2.y};
+    };
+    for (int s = 0; s < a.nsub; ++s) {
+        if (a.do_step) {
+            const bool moving = a.t[s] > 0;
+            p = half_drift(p, v, f, moving, DT, DT2, L);
+            v = v + dt * f;                           // step_V(dt) :398-409
+            p = half_drift(p, v, f, moving, DT, DT2, L);
+        }
+        if (!a.do_qt) continue;
+        const double u = v * qc.pv2q + a.expDet[s];        // vx on every state lane
+        tPart += qc.dtQ;
+        const double dp = lane_sum_p(nrm2(w) * hdp);
+        double u1, u2;
+        if (a.U) {
+            u1 = a.U[i];
+            u2 = a.U[(size_t)S + i];
+        } else {
+            u1 = su[grp][s][0];
+            u2 = su[grp][s][1];
+        }
+        cxd w0, w1, w2;
+        exchange(w, w0, w1, w2);
+        double kick;
+        if (u1 > dp) {
+            kick = lane_tree16(kick_term(w, w0, w1, w2, kw0, kw1, kw2));
+            const double phi = (u * cphi) * tPart;
+            double sn, cs;
+            sincos_q<true>(phi, sn, cs);
+            const cxd md = {mre, fma(mi1, u, mi0)};
+            const cxd c2 = {fma(dms, sn, c2re), fma(dmc, cs, c2im)};
+            cxd y = w, acc = {0., 0.};
+            cxd y0 = w0, y1 = w1, y2 = w2;
+#pragma unroll
+            for (int stg = 0; stg < 4; ++stg) {
+                double dpy = dp;
+                if (stg > 0) {
+                    dpy = lane_sum_p(nrm2(y) * hdp);
+                    exchange(y, y0, y1, y2);
+                }
+                const double pref = rsq_nr(1. - dpy);
+                const cxd ws = row_r(md, y, c0, y0, c1, y1, c2, y2);
+                const cxd d = {fma(pref, ws.re, -y.re), fma(pref, ws.im, -y.im)};
+                if (stg == 0) acc = d;
+                else if (stg < 3) acc = {fma(3., d.re, acc.re), fma(3., d.im, acc.im)};
+                else acc = {acc.re + d.re, acc.im + d.im};
+                if (stg < 2) y = {fma(0.5, d.re, w.re), fma(0.5, d.im, w.im)};
+                else if (stg == 2) y = {w.re + d.re, w.im + d.im};
+            }
+            w = {fma(0.125, acc.re, w.re), fma(0.125, acc.im, w.im)};
+        } else {                                      // quantum jump (:573-703)
+            tPart = 0;
+            const double nk = sq(w);
+            const double n3 = dpp<BCAST(2)>(nk), n4 = dpp<BCAST(3)>(nk), n5 = dpp<BCAST(4)>(nk), n6 = dpp<BCAST(5)>(nk);
+            double randDOrS, randDir, rand3, dummy;
+            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
+            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
+            (void)dummy;
+            const int target = jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
+            w = {k == target ? 1. : 0., 0.};
+        }
+        if (qc.renorm) w = [&] {                      // :706-712
+            const double r = rsq_nr(lane_tree16(nrm2(w)));
+            return cxd{w.re * r, w.im * r};
+        }();
+        v = fma(kmask, kick, v);                      // :705 (x lanes)
+    }
+    if (store) {
+        if (owner) {
+            a.R[(size_t)c * S + i] = p;
+            a.V[(size_t)c * S + i] = v;
+            if (!(p >= -0.125 * L && p <= 1.125 * L)) *a.oor = 1;
+        }
+        if (a.do_qt) {
+            if (k == 0) a.tPart[i] = tPart;
+            if (k < NS) {
+                a.psi[(size_t)(2 * k) * S + i] = w.re;
+                a.psi[(size_t)(2 * k + 1) * S + i] = w.im;
+            }
+        }
+    }
+}
+
+hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s) {
+    if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
+    if (a.nsub > MAXSUB) return hipErrorInvalidValue;
+    if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
+    if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes_r, dim3((a.n + 15) / 16), dim3(256), 0, s, a, tab);
+    else hipLaunchKernelGGL(k_substeps_r, dim3((a.n + 255) / 256), dim3(256), 0, s, a, tab);
+    return hipGetLastError();
+}
+
+}  // namespace mdqt

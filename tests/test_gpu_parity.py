@@ -147,7 +147,7 @@ def _evolved_state(orc, N0=300, seed=21, nmd=4):
     return o
 
 
-@pytest.mark.parametrize("qt_math", [0, 1])
+@pytest.mark.parametrize("qt_math", [0, 1, 2])
 def test_qstep_matches_oracle(eng, orc, qt_math):
     o = _evolved_state(orc)
     st = o.get_state()
@@ -190,7 +190,7 @@ def test_qstep_jump_branch_exercised(eng, orc):
     assert np.abs(a["V"] - b["V"]).max() < 1e-12
 
 
-@pytest.mark.parametrize("qt,qt_math", [(1, 0), (1, 1), (0, 0)])
+@pytest.mark.parametrize("qt,qt_math", [(1, 0), (1, 1), (1, 2), (0, 0), (0, 2)])
 def test_md_steps_short_horizon(eng, orc, qt, qt_math):
     kw = dict(N0=500, seed=77, rng_mode=1, qt_enabled=qt)
     s = eng.Simulation(**kw).init()
@@ -228,7 +228,7 @@ def test_substeps_fusion_equals_single_substeps(eng):
 
 @pytest.mark.parametrize("N0,extra", [(500, {}), (3500, {}), (300, dict(Om=3.0, OmDP=2.0, reNormalizewvFns=1)),
                                       (300, dict(fracOfSig=0.4, detuningDP=-0.5))])
-@pytest.mark.parametrize("qt_math", [0, 1])
+@pytest.mark.parametrize("qt_math", [0, 1, 2])
 def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra, qt_math):
     """k_substeps_lanes (16 lanes per ion) performs exactly k_substeps' operations"""
     sims = []
@@ -244,14 +244,15 @@ def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra, qt_math):
         assert np.array_equal(a[k], b[k]), (k, jumped)
 
 
-@pytest.mark.parametrize("N0,extra", [(300, {}), (500, dict(Om=3.0, OmDP=2.0)), (3500, {})])
-def test_drand48_reference_order_matches_oracle(eng, orc, N0, extra):
+@pytest.mark.parametrize("N0,extra,qt_math", [(300, {}, 0), (500, dict(Om=3.0, OmDP=2.0), 0), (3500, {}, 0),
+                                              (500, dict(Om=3.0, OmDP=2.0), 2)])
+def test_drand48_reference_order_matches_oracle(eng, orc, N0, extra, qt_math):
     """rng_mode 0: the reference's own drand48 stream consumed in its order (1 draw per ion,
     4-5 per quantum jump) — same jumps, same stream position, same trajectory as the oracle's
     reference-order restatement"""
     kw = dict(N0=N0, seed=12346, rng_mode=0, **extra)
     s = eng.Simulation(**kw).init()
-    s.set_option("qt_math", 0)                  # the reference's exact operations
+    s.set_option("qt_math", qt_math)            # 0: the reference's exact operations
     o = orc.OracleSim(**kw).init()
     assert s.drand48_state == orc.lib().orc_get_drand48_state(o.h)
     s.md_steps(4); o.md_steps(4)

@@ -173,6 +173,8 @@ __device__ __forceinline__ void wave_sync() {
 
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
+    // row_newbcast is a DP-ALU DPP control on gfx950: one v_mov_b64_dpp moves the whole double
+    if constexpr (CTRL >= 0x150 && CTRL <= 0x15F) return __builtin_amdgcn_update_dpp(0., v, CTRL, 0xF, 0xF, true);
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);

@@ -92,7 +92,7 @@ struct mdqt_ctx {
     int pend_nseg = 1;             // partial count of the pending forces (segments or slots)
     int scheme_opt = 0;            // force scheme: 0 auto, 1 rows (owner computes), 2 Newton-3 tiles
     bool use_n3 = false;
-    int nslots = 0, npairs = 0, capPairs = 0, n3split = 1;
+    int nslots = 0, npairs = 0, capPairs = 0;
     int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel
     // rng_mode 0: the reference's drand48 stream, consumed in ion order on the device
     unsigned long long* dX48 = nullptr;   // [1] stream state + [48] jA + [48] jC
@@ -368,11 +368,8 @@ static void choose_segments(mdqt_ctx* s) {
     const bool n3_ok = s->p.world_size == 1 && N >= 128 && N <= 65536;
     s->use_n3 = (s->scheme_opt == 2 && s->p.world_size == 1 && N >= 1) || (s->scheme_opt == 0 && n3_ok);
     const int nt = (N + 63) / 64;
-    // small systems: two waves per off-diagonal tile pair (twice the waves to spread over the
-    // 1024 SIMDs, twice the slots); larger ones: one
-    s->n3split = nt <= 256 ? 2 : 1;
-    s->nslots = s->use_n3 ? (s->n3split == 2 ? 2 * nt : nt + 1) : 0;
-    s->npairs = s->use_n3 ? (s->n3split == 2 ? nt * nt : nt * (nt + 1) / 2) : 0;
+    s->nslots = s->use_n3 ? nt : 0;
+    s->npairs = s->use_n3 ? nt * (nt + 1) / 2 : 0;
 }
 
 // partial-sum buffer (row segments or Newton-3 slots) and the tile-pair table
@@ -395,11 +392,7 @@ static int ensure_aux(mdqt_ctx* s) {
         std::vector<int2> h;
         h.reserve(s->npairs);
         for (int I = 0; I < nt; ++I)
-            for (int J = I; J < nt; ++J) {
-                if (s->n3split == 1) { h.push_back(make_int2(I, J)); continue; }
-                h.push_back(make_int2(I, 2 * J));
-                if (J != I) h.push_back(make_int2(I, 2 * J + 1));
-            }
+            for (int J = I; J < nt; ++J) h.push_back(make_int2(I, J));
         if ((int)h.size() != s->npairs) return fail("tile-pair table size mismatch");
         HIPCHK(hipMemcpyAsync(s->dPairs, h.data(), h.size() * sizeof(int2), hipMemcpyHostToDevice, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
@@ -797,7 +790,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
     if (s->use_n3) {
         N3Args a;
         a.R = s->dR; a.P = s->dFpart; a.pairs = s->dPairs;
-        a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs; a.split = s->n3split;
+        a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs;
         ForceArgs c = force_args(s, nullptr);
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
         a.micGuard = c.micGuard;

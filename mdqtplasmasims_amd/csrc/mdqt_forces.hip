@@ -2,7 +2,7 @@
 // (SpeedUp:244-281).
 //
 //   k_pairs<MODE, VARIANT>   owner-computes rows, LDS-staged j tiles, j split in segments
-//   k_pairs_n3<VARIANT>      Newton-3 over 64x64 tile pairs (one GPU, N <= 65536)
+//   k_pairs_n3<VARIANT>      Newton-3 over 64x64 tile pairs, 4 waves per pair (one GPU)
 //   k_reduce_segments        canonical sum of the partials when a caller asks for F
 //
 // VARIANT 0 keeps the reference's operations (sqrt, the three divisions, libm exp) without
@@ -16,7 +16,7 @@
 namespace mdqt {
 
 struct PairC {
-    double L, T, G, Rcut, lDeb, invlDeb;
+    double L, T, G, Rcut, lDeb, invlDeb, invL;
 };
 
 __device__ __forceinline__ const double* pos_base(const double* Rall, int g, int S) {
@@ -66,6 +66,22 @@ __device__ __forceinline__ void mic(double& dx, double& dy, double& dz, const Pa
     dz = (fabs(dz) >= c.T) ? dz - copysign(c.L, dz) : dz;
 }
 
+// Minimum image of the fast variant: dx -= L rint(dx / L) with the reciprocal (3 operations per
+// axis, any |dx|).  It differs from the reference's round(dx/L) only when dx/L lies within an ulp
+// of +-1/2, i.e. for pairs on the cutoff shell r ~ L/2 (with the other two separations below
+// ~1e-7 L for the pair to fall inside the cutoff either way): a measure-zero event.
+__device__ __forceinline__ void mic_r(double& dx, double& dy, double& dz, const PairC& c) {
+    dx = fma(-__builtin_rint(dx * c.invL), c.L, dx);
+    dy = fma(-__builtin_rint(dy * c.invL), c.L, dy);
+    dz = fma(-__builtin_rint(dz * c.invL), c.L, dz);
+}
+
+template <int VARIANT, bool GUARD>
+__device__ __forceinline__ void mic_v(double& dx, double& dy, double& dz, const PairC& c) {
+    if (VARIANT == 1) mic_r(dx, dy, dz, c);
+    else mic<GUARD>(dx, dy, dz, c);
+}
+
 // Force factor ft of one minimum-image separation (F_i += d * ft), 0 unless 0 < r < L/2
 // (:221-224).  Branch-free: out-of-range values are discarded by the final select.
 template <int VARIANT>
@@ -83,7 +99,7 @@ __device__ __forceinline__ double pair_ft(double dx, double dy, double dz, const
         ri = ri * fma(-hr * ri, ri, 1.5);
         const double dr = r2 * ri;
         const double ft = ((ri + c.invlDeb) * exp_neg(-dr * c.invlDeb)) * (ri * ri);
-        return (r2 > 0 && dr < c.Rcut) ? ft : 0.;
+        return (dr < c.Rcut) ? ft : 0.;          // r2 = 0 (coincident ions) gives dr = NaN: 0
     }
 }
 
@@ -102,7 +118,7 @@ __device__ __forceinline__ double pair_u(double dx, double dy, double dz, const 
         ri = ri * fma(-hr * ri, ri, 1.5);
         const double dr = r2 * ri;
         const double u = exp_neg(-dr * c.invlDeb) * ri;
-        return (r2 > 0 && dr < c.Rcut) ? u : 0.;
+        return (dr < c.Rcut) ? u : 0.;           // r2 = 0 gives dr = NaN: 0
     }
 }
 
@@ -148,7 +164,7 @@ __device__ __forceinline__ void rows_body(const ForceArgs& a, const PairC& c, do
 #pragma unroll 2
             for (int k = 0; k < nj; ++k) {
                 double dx = rx - sx[k], dy = ry - sy[k], dz = rz - sz[k];   // :213-215
-                mic<GUARD>(dx, dy, dz, c);
+                mic_v<VARIANT, GUARD>(dx, dy, dz, c);
                 if (MODE == 0) {
                     const double ft = pair_ft<VARIANT>(dx, dy, dz, c);
                     accum<VARIANT>(fx, dx, ft);
@@ -172,7 +188,7 @@ __device__ __forceinline__ void rows_body(const ForceArgs& a, const PairC& c, do
 template <int MODE, int VARIANT, bool GUARD>
 __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
     __shared__ double sx[FT], sy[FT], sz[FT];
-    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb};
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L};
     rows_body<MODE, VARIANT, GUARD>(a, c, sx, sy, sz);
 }
 
@@ -186,72 +202,106 @@ __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restric
 }
 
 // ------------------------------------------------------------------------------------------
-// Newton-3 tile pairs: wave w takes (I, J) = pairs[w]; lane l holds ion I*64+l and one ion of
-// tile J, which travels one lane per step together with its accumulated force.  Each pair of
-// the two tiles is evaluated once: f goes to i, -f to j (exact: the minimum image and r are
-// sign-symmetric, so f(j,i) == -f(i,j) bit for bit).  Deterministic slots, no atomics.
+// Newton-3 tile pairs: one workgroup (4 waves) per tile pair (I, J), I <= J.  Lane l holds ion
+// I*64 + l; the J tile sits in LDS twice over (positions j and j + 64), so at rotation step s
+// lane l meets ion J*64 + ((l + s) & 63) at LDS index l + s (an immediate offset in the unrolled
+// loop).  Each distinct pair is evaluated once: +f goes to the i accumulator (registers), +f to
+// the j accumulator (ds_add_f64 at index l + s; the wave's LDS operations run in order, so the
+// accumulation order is fixed), and the j side is negated at the end (exact).  Wave q takes
+// rotation steps [16q, 16q + 16) (diagonal tile: lane distances 1 + 8q .. 8 + 8q, the 32nd only
+// for lanes < 32).  The four waves' partials are combined in a fixed order and written to slot
+// J (rows of I) and slot I (rows of J); the diagonal tile's two sides are summed into slot I.
+// F = canonical sum of the ntiles slots (seg_sum).  Deterministic, no global atomics.
 // ------------------------------------------------------------------------------------------
-// rotate a value by one lane across the whole wave64 (DPP wave_rol:1, VALU latency)
-__device__ __forceinline__ int rot_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x134, 0xF, 0xF, true); }
-__device__ __forceinline__ double rot_d(double v) {
-    return __hiloint2double(rot_i(__double2hiint(v)), rot_i(__double2loint(v)));
-}
-
-template <int VARIANT, bool GUARD>
-__device__ __forceinline__ void n3_body(const N3Args& a, const PairC& c) {
-    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int l = threadIdx.x & 63;
-    const int2 IJ = a.pairs[w];
-    const int I = IJ.x;
-    const int J = a.split == 2 ? (IJ.y >> 1) : IJ.y;
-    const int half = a.split == 2 ? (IJ.y & 1) : 0;  // split 2: an off-diagonal pair in two waves
+template <int VARIANT, bool GUARD, bool RAGGED>
+__device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
+                                        double (*pj)[128], double (*accj)[3][128], double* mj,
+                                        double (*ia)[3][64]) {
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int S = a.S, N = a.N;
     const double* X = a.R;
     const double* Y = a.R + S;
     const double* Z = a.R + 2 * S;
+    if (q == 0) {                                   // stage the J tile (twice over)
+        const int j = J * 64 + l;
+        const bool vj = !RAGGED || j < N;
+        const double xj = vj ? X[j] : 0., yj = vj ? Y[j] : 0., zj = vj ? Z[j] : 0.;
+        pj[0][l] = xj; pj[0][l + 64] = xj;
+        pj[1][l] = yj; pj[1][l + 64] = yj;
+        pj[2][l] = zj; pj[2][l + 64] = zj;
+        if (RAGGED) { mj[l] = vj ? 1. : 0.; mj[l + 64] = mj[l]; }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
     const int i = I * 64 + l;
-    const bool vi = i < N;
+    const bool vi = !RAGGED || i < N;
     const double xi = vi ? X[i] : 0., yi = vi ? Y[i] : 0., zi = vi ? Z[i] : 0.;
-    // the second half of a split pair starts half a turn in: the two halves then meet the
-    // complementary lane offsets whichever way the rotation runs
-    int jx = J * 64 + ((l + 32 * half) & 63);
-    double xj = jx < N ? X[jx] : 0., yj = jx < N ? Y[jx] : 0., zj = jx < N ? Z[jx] : 0.;
-    double fxi = 0., fyi = 0., fzi = 0., fxj = 0., fyj = 0., fzj = 0.;
-    const bool diag = (I == J);
-    const int nsteps = diag ? 32 : 64 / a.split;
-    if (diag) {                                     // diagonal: lane distances 1 .. 32 only
-        xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
-    }
-    for (int s = 0; s < nsteps; ++s) {
-        const bool on = vi && jx < N && (!diag || s < 31 || l < 32);
-        double dx = xi - xj, dy = yi - yj, dz = zi - zj;
-        mic<GUARD>(dx, dy, dz, c);
+    const double mi = vi ? 1. : 0.;
+    __syncthreads();
+    double fx = 0., fy = 0., fz = 0.;
+    double* ax = accj[q][0];
+    double* ay = accj[q][1];
+    double* az = accj[q][2];
+    auto step = [&](int idx, double m) {
+        double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
+        mic_v<VARIANT, GUARD>(dx, dy, dz, c);
         double ft = pair_ft<VARIANT>(dx, dy, dz, c);
-        ft = on ? ft : 0.;
+        if (RAGGED) ft *= mi * mj[idx];
+        ft *= m;
         const double px = dx * ft, py = dy * ft, pz = dz * ft;
-        fxi += px; fyi += py; fzi += pz;
-        fxj -= px; fyj -= py; fzj -= pz;
-        xj = rot_d(xj); yj = rot_d(yj); zj = rot_d(zj); jx = rot_i(jx);
-        fxj = rot_d(fxj); fyj = rot_d(fyj); fzj = rot_d(fzj);
+        fx += px; fy += py; fz += pz;
+        __hip_atomic_fetch_add(&ax[idx], px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    };
+    const bool diag = I == J;
+    if (!diag) {
+        const int b = l + 16 * q;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) step(b + t, 1.);
+    } else {
+        const int b = l + 1 + 8 * q;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) step(b + t, 1.);
+        step(b + 7, (q == 3 && l >= 32) ? 0. : 1.);  // lane distance 32: once per pair
     }
-    // slots: split 1: rows of I -> J (I on the diagonal), rows of J -> I (ntiles on the diagonal)
-    //        split 2: rows of I -> 2J+half, rows of J -> 2I+half (diagonal: 2I and 2I+1)
+    ia[q][0][l] = fx; ia[q][1][l] = fy; ia[q][2][l] = fz;
+    __syncthreads();
     const size_t slab3 = (size_t)3 * S;
-    int si, sj;
-    if (a.split == 2) { si = 2 * J + half; sj = diag ? 2 * I + 1 : 2 * I + half; }
-    else { si = J; sj = diag ? a.ntiles : I; }
-    double* Pi = a.P + (size_t)si * slab3;
-    double* Pj = a.P + (size_t)sj * slab3;
-    if (i < S) { Pi[i] = fxi; Pi[S + i] = fyi; Pi[2 * S + i] = fzi; }
-    if (jx < S) { Pj[jx] = fxj; Pj[S + jx] = fyj; Pj[2 * S + jx] = fzj; }
+    if (q == 0) {                                   // rows of I -> slot J (diagonal: I)
+        double* Pi = a.P + (size_t)J * slab3;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            double v = ((ia[0][k][l] + ia[1][k][l]) + ia[2][k][l]) + ia[3][k][l];
+            if (diag) {
+                const double w = (((accj[0][k][l] + accj[0][k][l + 64]) + (accj[1][k][l] + accj[1][k][l + 64])) +
+                                  (accj[2][k][l] + accj[2][k][l + 64])) + (accj[3][k][l] + accj[3][k][l + 64]);
+                v = v - w;
+            }
+            if (i < S) Pi[(size_t)k * S + i] = v;
+        }
+    } else if (q == 1 && !diag) {                   // rows of J -> slot I
+        double* Pj = a.P + (size_t)I * slab3;
+        const int j = J * 64 + l;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double w = (((accj[0][k][l] + accj[0][k][l + 64]) + (accj[1][k][l] + accj[1][k][l + 64])) +
+                              (accj[2][k][l] + accj[2][k][l + 64])) + (accj[3][k][l] + accj[3][k][l + 64]);
+            if (j < S) Pj[(size_t)k * S + j] = -w;
+        }
+    }
 }
 
 template <int VARIANT, bool GUARD>
 __global__ __launch_bounds__(256) void k_pairs_n3(N3Args a) {
-    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;
-    if (w >= a.npairs) return;                      // wave-uniform exit
-    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb};
-    n3_body<VARIANT, GUARD>(a, c);
+    __shared__ double pj[3][128];
+    __shared__ double accj[4][3][128];
+    __shared__ double ia[4][3][64];
+    __shared__ double mj[128];
+    const int2 IJ = a.pairs[blockIdx.x];
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L};
+    if ((a.N & 63) && IJ.y == a.ntiles - 1) n3_tile<VARIANT, GUARD, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+    else n3_tile<VARIANT, GUARD, false>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -287,7 +337,7 @@ hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int 
 
 hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s) {
     if (a.npairs <= 0) return hipSuccess;
-    dim3 grid((a.npairs + 3) / 4);
+    dim3 grid(a.npairs);
     if (variant == 1) {
         if (a.guard) hipLaunchKernelGGL((k_pairs_n3<1, true>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_pairs_n3<1, false>), grid, dim3(256), 0, s, a);

@@ -128,18 +128,16 @@ __device__ __forceinline__ double seg_sum(const double* __restrict__ p, size_t s
     return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
-// Newton-3 tile-pair scheme (world_size 1, small/medium N): one wave per 64x64 tile pair
-// (I <= J), the J tile rotating through the lanes; partials go to slot J (rows of I) and slot
-// I (rows of J), the diagonal tile's two sides to slots I and ntiles.  F = canonical sum of
-// the ntiles + 1 slots (seg_sum), like the row scheme's segments.
+// Newton-3 tile-pair scheme (world_size 1): one workgroup of 4 waves per 64x64 tile pair
+// (I <= J); partials go to slot J (rows of I) and slot I (rows of J), the diagonal tile's two
+// sides to slot I.  F = canonical sum of the ntiles slots (seg_sum), like the row segments.
 struct N3Args {
     const double* R;    // [3][S] (world_size 1)
-    double* P;          // [ntiles + 1][3][S]
-    const int2* pairs;  // (I, J) of every wave; split 2: (I, 2J + half) for off-diagonal pairs
+    double* P;          // [ntiles][3][S]
+    const int2* pairs;  // (I, J) of every workgroup
     int N, S, ntiles, npairs;
-    int split;          // 1 or 2 waves per off-diagonal tile pair (2: small N, load balance)
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
-    int guard;          // as ForceArgs::guard
+    int guard;          // as ForceArgs::guard (exact variant only; the fast one needs no guard)
 };
 
 // drand48 in the reference's order (SpeedUp:486, :575-687: ions in index order, 1 draw per

@@ -273,13 +273,19 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
     if (a.do_qt && k < NS) w = {a.psi[(size_t)(2 * k) * S + i], a.psi[(size_t)(2 * k + 1) * S + i]};
     const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
     const uint64_t gid = a.gid0 + (uint64_t)i;
+    // u1, u2 of every substep of the launch staged in LDS: Philox draws computed lane-parallel
+    // (lane k: substeps k, k + 16), or the rng_mode 0 uniforms of the single substep
     __shared__ double su[16][MAXSUB][2];
-    if (a.do_qt && !a.U) {
-        for (int s = k; s < a.nsub; s += 16) {
-            double x0, x1;
-            philox_pair(qc, gid, a.q0 + (uint64_t)s, 0, x0, x1);
-            su[grp][s][0] = x0;
-            su[grp][s][1] = x1;
+    if (a.do_qt) {
+        if (a.U) {
+            if (k == 0) { su[grp][0][0] = a.U[i]; su[grp][0][1] = a.U[(size_t)S + i]; }
+        } else {
+            for (int s = k; s < a.nsub; s += 16) {
+                double x0, x1;
+                philox_pair(qc, gid, a.q0 + (uint64_t)s, 0, x0, x1);
+                su[grp][s][0] = x0;
+                su[grp][s][1] = x1;
+            }
         }
     }
     __syncthreads();
@@ -302,14 +308,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
         const double u = v * qc.pv2q + a.expDet[s];        // vx on every state lane
         tPart += qc.dtQ;
         const double dp = lane_sum_p(nrm2(w) * hdp);
-        double u1, u2;
-        if (a.U) {
-            u1 = a.U[i];
-            u2 = a.U[(size_t)S + i];
-        } else {
-            u1 = su[grp][s][0];
-            u2 = su[grp][s][1];
-        }
+        const double u1 = su[grp][s][0], u2 = su[grp][s][1];
         cxd w0, w1, w2;
         exchange(w, w0, w1, w2);
         double kick;

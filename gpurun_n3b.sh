@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU: force-scheme tests, then the C5 sharded-path line (one GPU) with a kernel trace
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "newton3 or forces or sharded" > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_c5" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --sharded-config c5 --sharded-steps 3 > "$GRAFT_REPO_ROOT/gpurun_out/prof_c5.log" 2>&1

@@ -48,6 +48,12 @@ int fail(const char* fmt, ...) {
             return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
     } while (0)
 
+#define NCCLCHK(expr)                                                                   \
+    do {                                                                                \
+        ncclResult_t r_ = (expr);                                                       \
+        if (r_ != ncclSuccess) return fail("%s failed: %s", #expr, ncclGetErrorString(r_)); \
+    } while (0)
+
 struct cx { double re, im; };
 inline cx cx_make(double r, double i) { return {r, i}; }
 inline cx cx_mul(cx a, cx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
@@ -90,8 +96,15 @@ struct mdqt_ctx {
     int qt_math = 2;               // 0 exact reference operations, 1 FMA-contracted, 2 reassociated (option "qt_math")
     bool f_pending = false;        // dFpart holds unreduced force partials (pend_nseg > 1)
     int pend_nseg = 1;             // partial count of the pending forces (segments or slots)
-    int scheme_opt = 0;            // force scheme: 0 auto, 1 rows (owner computes), 2 Newton-3 tiles
+    int scheme_opt = 0;            // force scheme: 0 auto, 1 rows (owner computes), 2 Newton-3 tiles, 3 Newton-3 blocks
     bool use_n3 = false;
+    bool use_n3b = false;          // Newton-3 block pairs (k_pairs_n3b): large N, one GPU or sharded
+    N3BArgs n3b;                   // its configuration (pointers and pair constants filled per call)
+    double* dSlots = nullptr;      // its slots [nd + R][3][Npad]
+    size_t capSlots = 0;
+    double* dFr = nullptr;         // sharded n3b: this rank's dense partial forces [world][3][S]
+    bool rs_pending = false;       // in-process group: F = sum of the ranks' dFr chunks, not formed yet
+    const double** dPeerParts = nullptr;   // device array of the group's dFr pointers
     int nslots = 0, npairs = 0, capPairs = 0;
     int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel
     // rng_mode 0: the reference's drand48 stream, consumed in ion order on the device
@@ -364,12 +377,34 @@ static void choose_segments(mdqt_ctx* s) {
     if (nseg < 1) nseg = 1;
     s->seglen = N > 0 ? (N + nseg - 1) / nseg : 1;
     s->nseg = N > 0 ? (N + s->seglen - 1) / s->seglen : 1;
-    // Newton-3 tile pairs: one GPU, and the (ntiles+1) x 3 x S partial slots stay small
-    const bool n3_ok = s->p.world_size == 1 && N >= 128 && N <= 65536;
-    s->use_n3 = (s->scheme_opt == 2 && s->p.world_size == 1 && N >= 1) || (s->scheme_opt == 0 && n3_ok);
+    // Newton-3 tile pairs (one GPU, ntiles slots of 3 x S) up to 64k ions; above that Newton-3
+    // block pairs (O(N^2/1024) slots, one GPU or sharded with a reduce-scatter); owner-computes
+    // rows for small sharded systems (bit-identical across world sizes)
+    const int W = s->p.world_size;
+    int sch = s->scheme_opt;
+    if (sch == 0) {
+        if (W == 1) sch = N > 65536 ? 3 : (N >= 128 ? 2 : 1);
+        else sch = N > 65536 ? 3 : 1;
+    }
+    s->use_n3 = sch == 2 && W == 1 && N >= 1;
+    s->use_n3b = sch == 3 && N >= 1;
     const int nt = (N + 63) / 64;
     s->nslots = s->use_n3 ? nt : 0;
     s->npairs = s->use_n3 ? nt * (nt + 1) / 2 : 0;
+    N3BArgs& b = s->n3b;
+    memset(&b, 0, sizeof b);
+    if (s->use_n3b) {
+        b.N = N; b.T = nt; b.Npad = nt * 64;
+        b.NB = (nt + 15) / 16;
+        b.nd = b.NB / 2 + 1;
+        b.Plo = (int)((long)s->p.rank * b.NB / W);
+        b.Phi = (int)((long)(s->p.rank + 1) * b.NB / W);
+        const int nblk = std::max(b.Phi - b.Plo, 1);
+        // ~4096 workgroups per rank (8 rounds of 2 per CU): short tail
+        int R = std::min(b.nd, (4096 + nblk - 1) / nblk);
+        b.runlen = (b.nd + R - 1) / R;
+        b.R = (b.nd + b.runlen - 1) / b.runlen;
+    }
 }
 
 // partial-sum buffer (row segments or Newton-3 slots) and the tile-pair table
@@ -380,6 +415,17 @@ static int ensure_aux(mdqt_ctx* s) {
         s->dFpart = nullptr;
         HIPCHK(hipMalloc(&s->dFpart, (size_t)s->capS * 3 * need * sizeof(double)));
         s->capNseg = need;
+    }
+    if (s->use_n3b) {
+        const size_t need_s = (size_t)(s->n3b.nd + s->n3b.R) * 3 * s->n3b.Npad;
+        if (need_s > s->capSlots) {
+            if (s->dSlots) HIPCHK(hipFree(s->dSlots));
+            s->dSlots = nullptr;
+            HIPCHK(hipMalloc(&s->dSlots, need_s * sizeof(double)));
+            s->capSlots = need_s;
+        }
+        if (s->p.world_size > 1 && !s->dFr)
+            HIPCHK(hipMalloc(&s->dFr, (size_t)s->capS * 3 * s->p.world_size * sizeof(double)));
     }
     if (s->use_n3 && s->npairs > 0) {
         if (s->npairs > s->capPairs) {
@@ -406,6 +452,11 @@ static void free_device(mdqt_ctx* s) {
     if (s->dPairs) (void)hipFree(s->dPairs);
     s->dPairs = nullptr;
     s->capPairs = 0;
+    if (s->dSlots) (void)hipFree(s->dSlots);
+    if (s->dFr) (void)hipFree(s->dFr);
+    if (s->dPeerParts) (void)hipFree((void*)s->dPeerParts);
+    s->dSlots = nullptr; s->dFr = nullptr; s->dPeerParts = nullptr;
+    s->capSlots = 0;
     s->capS = 0; s->capNseg = 0; s->kdeChunks = 0;
 }
 
@@ -542,7 +593,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "decayRatioD5Halves")) return s->r;
     if (!strcmp(n, "kRat")) return s->kRat;
     if (!strcmp(n, "force_segments")) return s->nseg;
-    if (!strcmp(n, "force_scheme")) return s->use_n3 ? 2 : 1;
+    if (!strcmp(n, "force_scheme")) return s->use_n3b ? 3 : s->use_n3 ? 2 : 1;
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
     return NAN;
@@ -610,6 +661,7 @@ extern "C" int mdqt_set_state(mdqt_ctx* s, int N, const double* R, const double*
 
 extern "C" int mdqt_set_forces(mdqt_ctx* s, const double* F, size_t ld) {
     s->f_pending = false;
+    s->rs_pending = false;
     const int S = s->S, lo = s->lo, n = s->nloc;
     std::vector<double> h((size_t)3 * S, 0.);
     for (int c = 0; c < 3; ++c)
@@ -761,8 +813,31 @@ static ForceArgs force_args(mdqt_ctx* s, double* out) {
     return a;
 }
 
+// in-process rank group with block-pair Newton-3: F of this rank = the ranks' dense partials
+// summed in rank order (RCCL's reduce-scatter in a real group).  Peers' force launches are
+// complete: callers step the group in lockstep (all forces before any substeps).
+static int local_reduce(mdqt_ctx* s) {
+    if (!s->rs_pending) return 0;
+    const int W = s->p.world_size;
+    std::vector<const double*> h(W, nullptr);
+    for (mdqt_ctx* q : s->local) {
+        if (!q->dFr) return fail("local_reduce: rank %d has no partial forces", q->p.rank);
+        h[q->p.rank] = q->dFr;
+        HIPCHK(hipSetDevice(q->dev));
+        HIPCHK(hipStreamSynchronize(q->stream));
+    }
+    HIPCHK(hipSetDevice(s->dev));
+    if (!s->dPeerParts) HIPCHK(hipMalloc((void**)&s->dPeerParts, W * sizeof(double*)));
+    HIPCHK(hipMemcpy((void*)s->dPeerParts, h.data(), W * sizeof(double*), hipMemcpyHostToDevice));
+    HIPCHK(launch_sum_rank_chunks(s->dPeerParts, W, s->p.rank, s->S, s->dF, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    s->rs_pending = false;
+    return 0;
+}
+
 // fold pending force partials into F (consumers other than the substep kernels)
 static int settle_forces(mdqt_ctx* s) {
+    if (local_reduce(s)) return -1;
     if (!s->f_pending) return 0;
     HIPCHK(launch_reduce_segments(s->dFpart, s->dF, s->pend_nseg, s->nloc, s->S, 3, s->stream));
     s->f_pending = false;
@@ -798,6 +873,24 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         HIPCHK(launch_forces_n3(a, s->force_variant, s->stream));
         s->f_pending = true;       // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots;
+    } else if (s->use_n3b) {
+        N3BArgs a = s->n3b;
+        ForceArgs c = force_args(s, nullptr);
+        a.Rall = s->dR; a.slots = s->dSlots; a.S = s->S;
+        a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
+        a.micGuard = c.micGuard; a.guard = c.guard;
+        const int W = s->p.world_size;
+        HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream));
+        if (W > 1) {
+            if (s->comm) {
+                NCCLCHK(ncclReduceScatter(s->dFr, s->dF, (size_t)3 * s->S, ncclDouble, ncclSum, s->comm, s->stream));
+            } else if (!s->local.empty()) {
+                s->rs_pending = true;      // formed by local_reduce once every rank has its partials
+            } else {
+                return fail("mdqt_forces: sharded Newton-3 blocks need a communicator (mdqt_comm_init)");
+            }
+        }
+        s->f_pending = false;
     } else if (s->nseg == 1) {
         HIPCHK(launch_forces(force_args(s, s->dF), s->stream));
     } else {
@@ -811,6 +904,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
 
 // n substeps of (step if do_step; qstep if do_qt_flag) — t advances only when advance_t
 static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int advance_t) {
+    if (local_reduce(s)) return -1;
     HIPCHK(hipSetDevice(s->dev));
     const int do_qt = do_qt_flag && s->p.qt_enabled;
     const bool d48 = do_qt && s->p.rng_mode == 0;
@@ -1249,7 +1343,8 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
 extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     if (!s || !name) return fail("mdqt_set_option: NULL argument");
     if (!strcmp(name, "force_scheme")) {
-        if (value < 0 || value > 2) return fail("force_scheme must be 0 (auto), 1 (rows) or 2 (Newton-3 tiles)");
+        if (value < 0 || value > 3)
+            return fail("force_scheme must be 0 (auto), 1 (rows), 2 (Newton-3 tiles) or 3 (Newton-3 blocks)");
         if (value == 2 && s->p.world_size != 1) return fail("force_scheme 2 needs world_size 1");
         if (settle_forces(s)) return -1;
         s->scheme_opt = value;
@@ -1321,11 +1416,6 @@ extern "C" int mdqt_kernel_time_totals(mdqt_ctx* s, double* force_ms, int* nforc
 // output steps all-reduce a few scalars, the KDE bins and the per-ion file columns.
 // ---------------------------------------------------------------------------------------------
 
-#define NCCLCHK(expr)                                                                   \
-    do {                                                                                \
-        ncclResult_t r_ = (expr);                                                       \
-        if (r_ != ncclSuccess) return fail("%s failed: %s", #expr, ncclGetErrorString(r_)); \
-    } while (0)
 
 extern "C" int mdqt_comm_unique_id(void* out, size_t len) {
     if (!out || len < sizeof(ncclUniqueId)) return fail("mdqt_comm_unique_id: need %zu bytes", sizeof(ncclUniqueId));

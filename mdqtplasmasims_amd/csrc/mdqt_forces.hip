@@ -213,6 +213,24 @@ __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restric
 // J (rows of I) and slot I (rows of J); the diagonal tile's two sides are summed into slot I.
 // F = canonical sum of the ntiles slots (seg_sum).  Deterministic, no global atomics.
 // ------------------------------------------------------------------------------------------
+// one rotation step of a Newton-3 tile pair: lane's ion i against the J-tile ion at LDS index
+// idx; +f to the i accumulator (registers) and to the j accumulator (ds_add_f64, no return)
+template <int VARIANT, bool GUARD, bool RAGGED>
+__device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
+                                        const double (*pj)[128], const double* mj, double* ax, double* ay,
+                                        double* az, double& fx, double& fy, double& fz, const PairC& c) {
+    double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
+    mic_v<VARIANT, GUARD>(dx, dy, dz, c);
+    double ft = pair_ft<VARIANT>(dx, dy, dz, c);
+    if (RAGGED) ft *= mi * mj[idx];
+    ft *= m;
+    const double px = dx * ft, py = dy * ft, pz = dz * ft;
+    fx += px; fy += py; fz += pz;
+    __hip_atomic_fetch_add(&ax[idx], px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 template <int VARIANT, bool GUARD, bool RAGGED>
 __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
@@ -243,16 +261,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     double* ay = accj[q][1];
     double* az = accj[q][2];
     auto step = [&](int idx, double m) {
-        double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
-        mic_v<VARIANT, GUARD>(dx, dy, dz, c);
-        double ft = pair_ft<VARIANT>(dx, dy, dz, c);
-        if (RAGGED) ft *= mi * mj[idx];
-        ft *= m;
-        const double px = dx * ft, py = dy * ft, pz = dz * ft;
-        fx += px; fy += py; fz += pz;
-        __hip_atomic_fetch_add(&ax[idx], px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        n3_step<VARIANT, GUARD, RAGGED>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
     };
     const bool diag = I == J;
     if (!diag) {
@@ -305,6 +314,145 @@ __global__ __launch_bounds__(256) void k_pairs_n3(N3Args a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Newton-3 over BLOCK pairs (large N, one GPU or sharded): blocks of 16 tiles (1024 ions); a
+// workgroup of 16 waves holds block P (wave q: tile I = 16P + q in registers) and walks the
+// block distances db of its run, db in [0, NB/2] of the cyclic half shell (block Q = P + db mod
+// NB; db = NB/2 only from P < NB/2 when NB is even; db = 0: tile pairs I <= J).  For every J
+// tile of Q all 16 waves run their (I, J) rotation (64 steps; 32 on the diagonal tile) against
+// the J tile in LDS with per-wave j accumulators, which are then combined in wave order and
+// written to j-slot db (rows of J); each wave's i accumulator spans the whole run and goes to
+// i-slot nd + run.  Slots: [nd + R][3][Npad], nd = NB/2 + 1 — O(N^2/1024) doubles, not O(N^2/64).
+// The canonical per-ion sum (k_n3b_reduce) takes the j-slots in db order, then the i-slots in
+// run order, skipping slots this rank does not write.
+// ------------------------------------------------------------------------------------------
+constexpr int BW = 16;                              // tiles per block = waves per workgroup
+
+__device__ __forceinline__ const double* tile_base(const double* Rall, int tile, int S) {
+    const int g = tile * 64;                        // S is a multiple of 64: tiles never straddle slabs
+    const int w = g / S;
+    return Rall + (size_t)w * 3 * S + (g - w * S);
+}
+
+template <int VARIANT, bool GUARD, bool RAGGED>
+__device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi, double zi, double mi,
+                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
+                                         double* az, double& fx, double& fy, double& fz, const PairC& c) {
+    if (!diag) {
+        for (int t0 = 0; t0 < 64; t0 += 16) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                n3_step<VARIANT, GUARD, RAGGED>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+        }
+    } else {
+        for (int t0 = 1; t0 < 33; t0 += 16) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const double m = (t0 + t == 32 && l >= 32) ? 0. : 1.;   // lane distance 32: once
+                n3_step<VARIANT, GUARD, RAGGED>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+            }
+        }
+    }
+}
+
+template <int VARIANT, bool GUARD>
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pairs_n3b(N3BArgs a) {
+    __shared__ double pj[3][128];
+    __shared__ double mj[128];
+    __shared__ double accj[BW][3][128];
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int P = a.Plo + (int)blockIdx.x / a.R;
+    const int run = (int)blockIdx.x % a.R;
+    const int d0 = run * a.runlen, d1 = min(a.nd, d0 + a.runlen);
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L};
+    const int T = a.T, N = a.N, S = a.S;
+    const bool ragN = (N & 63) != 0;
+    const int I = P * BW + q;
+    const bool vI = I < T;
+    const int i = I * 64 + l;
+    double xi = 0., yi = 0., zi = 0., mi = 0.;
+    if (vI && i < N) {
+        const double* p = tile_base(a.Rall, I, S) + l;
+        xi = p[0]; yi = p[S]; zi = p[2 * S]; mi = 1.;
+    }
+    double fx = 0., fy = 0., fz = 0.;
+    double* ax = accj[q][0];
+    double* ay = accj[q][1];
+    double* az = accj[q][2];
+    const size_t plane = (size_t)3 * a.Npad;
+    for (int db = d0; db < d1; ++db) {
+        if (!(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2) continue;   // the other half covers it
+        const int Q = (P + db) % a.NB;
+        for (int b = 0; b < BW; ++b) {
+            const int J = Q * BW + b;
+            if (J >= T) break;
+            if (q == 0) {                           // stage J (twice over)
+                const int j = J * 64 + l;
+                const bool vj = j < N;
+                const double* p = tile_base(a.Rall, J, S) + l;
+                const double xj = vj ? p[0] : 0., yj = vj ? p[S] : 0., zj = vj ? p[2 * S] : 0.;
+                pj[0][l] = xj; pj[0][l + 64] = xj;
+                pj[1][l] = yj; pj[1][l + 64] = yj;
+                pj[2][l] = zj; pj[2][l + 64] = zj;
+                mj[l] = vj ? 1. : 0.; mj[l + 64] = mj[l];
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
+            __syncthreads();
+            if (vI && (db > 0 || J >= I)) {
+                const bool diag = (db == 0 && J == I);
+                if (ragN && (I == T - 1 || J == T - 1))
+                    n3b_pair<VARIANT, GUARD, true>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+                else
+                    n3b_pair<VARIANT, GUARD, false>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+            }
+            __syncthreads();
+            if (q < 3) {                            // j side of J's rows -> j-slot db
+                double v = 0.;
+#pragma unroll
+                for (int w = 0; w < BW; ++w) v = v + (accj[w][q][l] + accj[w][q][l + 64]);
+                a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = -v;
+            }
+            __syncthreads();
+        }
+    }
+    if (vI) {                                       // i side -> i-slot nd + run
+        double* o = a.slots + (size_t)(a.nd + run) * plane + i;
+        o[0] = fx; o[a.Npad] = fy; o[2 * (size_t)a.Npad] = fz;
+    }
+}
+
+// canonical per-ion sum of the slots this rank wrote: j-slots db = 0 .. nd-1, then i-slots.
+// out: world 1 -> F [3][S]; sharded -> the rank's dense partial [world][3][S] (reduce-scattered)
+__global__ __launch_bounds__(256) void k_n3b_reduce(N3BArgs a, double* __restrict__ out) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int k = blockIdx.y;
+    if (g >= a.N) return;
+    const int B = (g >> 6) / BW;
+    const size_t plane = (size_t)3 * a.Npad;
+    const double* p = a.slots + (size_t)k * a.Npad + g;
+    double acc = 0.;
+    for (int db = 0; db < a.nd; ++db) {
+        const int P = (B - db + a.NB) % a.NB;
+        const bool skip = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
+        if (!skip && P >= a.Plo && P < a.Phi) acc = acc + p[(size_t)db * plane];
+    }
+    if (B >= a.Plo && B < a.Phi)
+        for (int r = 0; r < a.R; ++r) acc = acc + p[(size_t)(a.nd + r) * plane];
+    const int w = g / a.S;
+    out[(size_t)w * 3 * a.S + (size_t)k * a.S + (g - w * a.S)] = acc;
+}
+
+// in-process rank group (tests): F of rank `rank` = sum over ranks r = 0.. of part[r]'s chunk
+__global__ __launch_bounds__(256) void k_sum_rank_chunks(const double* const* parts, int world, int rank, int S,
+                                                         double* __restrict__ F) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * S) return;
+    double acc = 0.;
+    for (int r = 0; r < world; ++r) acc = acc + parts[r][(size_t)rank * 3 * S + i];
+    F[i] = acc;
+}
+
+// ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
 static int seg_blocks(int nrows) { return (nrows + FT - 1) / FT; }
@@ -345,6 +493,26 @@ hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s) {
         if (a.guard) hipLaunchKernelGGL((k_pairs_n3<0, true>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_pairs_n3<0, false>), grid, dim3(256), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s) {
+    const int nblk = (a.Phi - a.Plo) * a.R;
+    if (nblk > 0) {
+        if (variant == 1) {
+            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<1, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            else hipLaunchKernelGGL((k_pairs_n3b<1, false>), dim3(nblk), dim3(BW * 64), 0, s, a);
+        } else {
+            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<0, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            else hipLaunchKernelGGL((k_pairs_n3b<0, false>), dim3(nblk), dim3(BW * 64), 0, s, a);
+        }
+    }
+    hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, a, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_rank_chunks, dim3((3 * S + 255) / 256), dim3(256), 0, s, parts, world, rank, S, F);
     return hipGetLastError();
 }
 

@@ -140,6 +140,21 @@ struct N3Args {
     int guard;          // as ForceArgs::guard (exact variant only; the fast one needs no guard)
 };
 
+// Newton-3 over block pairs (mdqt_forces.hip k_pairs_n3b): blocks of 16 tiles, cyclic half
+// shell of block distances, slots [nd + R][3][Npad] (j-slots by distance, i-slots by run).
+// A rank runs the workgroups of blocks [Plo, Phi); k_n3b_reduce sums the slots it wrote.
+struct N3BArgs {
+    const double* Rall; // gathered positions [world][3][S]
+    double* slots;      // [nd + R][3][Npad]
+    int N, S, T, Npad;  // ions, slab stride, tiles, T * 64
+    int NB, nd, R, runlen;   // blocks, half-shell distances NB/2 + 1, runs per block, distances per run
+    int Plo, Phi;       // this rank's blocks
+    double L, lDeb, Rcut, invlDeb, micT, micGuard;
+    int guard;
+};
+hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
+hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
+
 // drand48 in the reference's order (SpeedUp:486, :575-687: ions in index order, 1 draw per
 // ion, 4-5 for a quantum jump): one workgroup assigns every ion its uniforms from the single
 // stream, by LCG jump-ahead from the stream state, restarting after each (rare) jump.

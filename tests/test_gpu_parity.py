@@ -96,7 +96,7 @@ def test_init_matches_oracle_bitwise(eng, orc, N0):
     assert abs(ca["Epot0"] - cb["Epot0"]) <= 1e-12 * abs(cb["Epot0"])
 
 
-@pytest.mark.parametrize("scheme,variant", [(1, 0), (1, 1), (2, 0), (2, 1)])
+@pytest.mark.parametrize("scheme,variant", [(1, 0), (1, 1), (2, 0), (2, 1), (3, 0), (3, 1)])
 def test_forces_match_oracle_after_init(eng, orc, scheme, variant):
     """both force schemes (owner-computes rows; Newton-3 tile pairs) x both pair variants"""
     s, o = pair(eng, orc, N0=3500, seed=12346)
@@ -121,6 +121,65 @@ def test_newton3_tiles_ragged_sizes(eng, orc, N0):
     s2.md_steps(2)
     o.md_steps(2)
     assert np.abs(s2.get_state()["V"] - o.get_state()["V"]).max() < 1e-10
+
+
+@pytest.mark.parametrize("N0", [200, 1100, 2500, 5000])
+def test_newton3_blocks_sizes(eng, orc, N0):
+    """Newton-3 block pairs (half shell of 16-tile blocks): one block, even and odd block counts,
+    ragged last tile; then two MD steps"""
+    s, o = pair(eng, orc, N0=N0, seed=23)
+    s.set_option("force_scheme", 3)
+    assert s.const("force_scheme") == 3
+    s.forces(); o.forces()
+    assert rel(s.get_state()["F"], o.get_state()["F"]) < 1e-13
+    s2 = eng.Simulation(N0=N0, seed=23).init()
+    s2.set_option("force_scheme", 3)
+    s2.md_steps(2)
+    o.md_steps(2)
+    assert np.abs(s2.get_state()["V"] - o.get_state()["V"]).max() < 1e-10
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_newton3_blocks_local_group(eng, orc, world):
+    """sharded Newton-3 block pairs: every rank computes its blocks' pairs for all ions, the dense
+    partials are reduce-scattered (in-process group: summed in rank order) — forces within the
+    1e-13 gate of the oracle, trajectories within the short-horizon gate"""
+    from mdqtplasmasims_amd.engine import comm_init_local
+    kw = dict(N0=5000, seed=9)
+    o = orc.OracleSim(nthreads=8, rng_mode=1, **kw).init()
+    st = o.get_state()
+    sims = [eng.Simulation(world_size=world, rank=r, **kw) for r in range(world)]
+    for s in sims:
+        s.set_option("force_scheme", 3)
+        s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+    comm_init_local(sims)
+    for s in sims:
+        s.allgather_positions()
+    for s in sims:
+        s.forces()
+    o.forces()
+    G = o.get_state()["F"]
+    for s in sims:
+        lo, hi = s.slab_bounds()
+        F = s.get_state()["F"][:, lo:hi]
+        assert rel(F, G[:, lo:hi]) < 1e-13
+    for _ in range(2):
+        for s in sims:
+            s.substeps(25)
+        for s in sims:
+            s.allgather_positions()
+        for s in sims:
+            s.forces()
+    for s in sims:
+        s.substeps(25)
+    o.substeps(25)
+    o.md_steps(2)
+    b = o.get_state()
+    for s in sims:
+        lo, hi = s.slab_bounds()
+        a = s.get_state()
+        assert np.abs(a["R"][:, lo:hi] - b["R"][:, lo:hi]).max() < 1e-10
+        assert np.abs(a["V"][:, lo:hi] - b["V"][:, lo:hi]).max() < 1e-10
 
 
 @pytest.mark.parametrize("t0", [0.0, 0.5])

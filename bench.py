@@ -60,7 +60,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r01_c2_pmc.json")):
+def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r01_v9_c2_pmc.json")):
     """HBM bytes per launch of the kernel from the committed rocprofv3 --pmc summary of the same
     C2 workload (FETCH_SIZE and WRITE_SIZE in separate passes, kB -> B; no gfx950 x2 read
     correction: the kernel's loads are 8 B/lane, outside the guide's calibrated 16 B/lane case)."""
@@ -149,13 +149,15 @@ def main():
         f_avg = f_ms / max(nf, 1) * 1e-3
         s_avg = s_ms / max(ns, 1) * 1e-3
         if qt and s_ms >= f_ms:
-            nsub_per_launch = ratio * args.steps / max(ns, 1)
+            nsub_per_launch = ratio                 # one fused launch per MD interval (ratio <= 32)
             bytes_launch = B_Q_PER_ION * N
             ach = bytes_launch / s_avg / 1e9
             flops = F_Q_PER_QSTEP * N * nsub_per_launch
             roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("k_substeps"),
-                    "kernel": "k_substeps_lanes (fused 25 x step+qstep)" if N < 98304 else "k_substeps",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(("k_substeps_lanes" if N < 98304 else "k_substeps") +
+                                                                     ("_r" if args.qt_math == 2 else "")),
+                    "kernel": ("k_substeps_lanes" if N < 98304 else "k_substeps") +
+                              ("_r" if args.qt_math == 2 else "") + " (fused 25 x step+qstep)",
                     "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
                     "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS}
         else:
@@ -231,7 +233,8 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     N = sim.N
     sim.close()
     unit_steps = ratio if qt else 1
-    return {"workload": desc + ", one system sharded over all ranks (RCCL position all-gather)",
+    return {"workload": desc + ", one system sharded over all ranks (RCCL position all-gather; "
+                           "Newton-3 block-pair forces reduce-scattered)",
             "N": N, "n_gpus": world, "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",

@@ -61,6 +61,13 @@ typedef struct mdqt_params {
     int world_size;       /* ions sharded over world_size contexts (1 = whole system here)     */
     int rank;             /* this context's slab: ions [rank*S, min((rank+1)*S, N))             */
     int force_segments;   /* j-split of the force sum (0 = auto, a function of N only)         */
+    int qt_model;         /* level scheme of qstep(): 0 = SpeedUp Sr+ 12-level laser cooling (default);
+                           * optical pumping ("spin tagging", Philox stream and qt_math 2 only):
+                           * 1 = 408 nm linear, 7 levels (randomFrozenStartTag408Linear.cpp:396,
+                           *     MonteCarloFollowedByQTTagging408Linear.cpp:555),
+                           * 2 = 408 nm quad, 7 levels (randomFrozenStartTag408Quad.cpp:399),
+                           * 3 = 422 nm linear, 5 levels (randomFrozenStartTag422Linear.cpp:390).
+                           * Pumping models use states 0..6 / 0..4 of the 12-state psi layout. */
     char saveDirectory[256]; /* SpeedUp:56 */
 } mdqt_params;
 
@@ -127,12 +134,19 @@ int         mdqt_output(mdqt_ctx* c);                        /* output(),  Speed
 int         mdqt_write_conditions(mdqt_ctx* c, int c0);      /* writeConditions, :725-784       */
 int         mdqt_read_conditions(mdqt_ctx* c, int c0);       /* readConditions,  :785-916       */
 int         mdqt_run(mdqt_ctx* c);                           /* main() time loop, :1139-1383    */
+/* optical-pumping models: tag every ion spin-up with probability |<up|psi>|^2 —
+ * measureSpinUps (randomFrozenStartTag408Linear.cpp:600, randomFrozenStartTag422Linear.cpp:568)
+ * = tagParticles (MonteCarloFollowedByQTTagging408Linear.cpp:1022).  tags: [N] (may be NULL;
+ * a sharded context fills its slab), *n_up: number tagged (this context's ions). */
+int         mdqt_tag_spin_up(mdqt_ctx* c, int* tags, int* n_up);
 
 /* ---- tuning knobs ----
  *   "substep_kernel": 0 = auto, 1 = thread per ion, 2 = 16-lane group per ion
  *   "force_kernel":   1 = fast reciprocal form (default), 0 = the reference's exact operations
  *                     (the two differ by a few ulp per pair; both meet the 1e-13 force gate)
  *   "force_scheme":   0 = auto, 1 = owner-computes rows, 2 = Newton-3 tile pairs (one GPU)
+ *   "qt_enabled":     1 = qstep() runs in the substeps, 0 = skipped (t still advances): the
+ *                     pumping programs' pump window (randomFrozenStartTag408Linear.cpp main)
  *   "qt_math":        0 = the reference's exact operations, 1 = FMA-contracted with a refined
  *                     rsq for 1/sqrt(1-dp), 2 = reassociated (default: fixed FMA chains per row
  *                     of M, folded constants; ~3x fewer instructions per substep).  1 and 2

@@ -26,7 +26,8 @@ class MdqtParams(C.Structure):
         ("N0", C.c_int), ("newRun", C.c_int), ("c0", C.c_int), ("sampleFreq", C.c_int),
         ("reNormalizewvFns", C.c_int), ("qt_enabled", C.c_int), ("rng_mode", C.c_int),
         ("seed", C.c_uint32), ("job", C.c_uint32), ("device", C.c_int), ("world_size", C.c_int),
-        ("rank", C.c_int), ("force_segments", C.c_int), ("saveDirectory", C.c_char * 256),
+        ("rank", C.c_int), ("force_segments", C.c_int), ("qt_model", C.c_int),
+        ("saveDirectory", C.c_char * 256),
     ]
 
 
@@ -67,6 +68,7 @@ SIGNATURES = [
     ("mdqt_write_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_read_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_run", C.c_int, [C.c_void_p]),
+    ("mdqt_tag_spin_up", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("mdqt_set_option", C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     ("mdqt_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("mdqt_get_stream", C.c_void_p, [C.c_void_p]),

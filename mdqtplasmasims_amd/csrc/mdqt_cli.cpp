@@ -44,7 +44,7 @@ int main(int argc, char** argv) {
 #define IPAR(name) if (!strcmp(key, #name)) { p.name = atoi(v); continue; }
         DPAR(Ge) DPAR(tmax) DPAR(density) DPAR(sig0) DPAR(Te) DPAR(fracOfSig) DPAR(detuning)
         DPAR(detuningDP) DPAR(Om) DPAR(OmDP)
-        IPAR(N0) IPAR(newRun) IPAR(c0) IPAR(sampleFreq) IPAR(reNormalizewvFns) IPAR(device)
+        IPAR(N0) IPAR(newRun) IPAR(c0) IPAR(sampleFreq) IPAR(reNormalizewvFns) IPAR(device) IPAR(qt_model)
 #undef DPAR
 #undef IPAR
         if (!strcmp(key, "qt")) { p.qt_enabled = atoi(v); continue; }

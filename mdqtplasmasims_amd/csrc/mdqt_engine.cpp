@@ -163,7 +163,7 @@ extern "C" void mdqt_default_params(mdqt_params* p) {
     p->detuning = -1; p->detuningDP = 1; p->Om = 1; p->OmDP = 1;                               // :70-73
     p->N0 = 3500; p->newRun = 1; p->c0 = 0; p->sampleFreq = 40; p->reNormalizewvFns = 0;       // :61-78
     p->qt_enabled = 1; p->rng_mode = 1; p->seed = 12345; p->job = 1;
-    p->device = -1; p->world_size = 1; p->rank = 0; p->force_segments = 0;
+    p->device = -1; p->world_size = 1; p->rank = 0; p->force_segments = 0; p->qt_model = 0;
     strcpy(p->saveDirectory, "dataLaserCool/");                                              // :56
 }
 
@@ -174,6 +174,58 @@ extern "C" int mdqt_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+// FastTab of the optical-pumping models (qt_model 1..3).  Decay channels cs[j] = |a><b| with
+// weights gs[j] (randomFrozenStartTag408Linear.cpp main :1000-1019; ...422Linear.cpp main):
+// decayMatrix_bb = sum_j gs[j] over the channels leaving b, hamDecayTerm = -i/2 decayMatrix;
+// H = detunings on the P levels (-det -/+ v_q, :439) + S-P couplings -Om/2 sqrt(gs[x]) |a><b|
+// + h.c. (:438); M = I - i h H.  No optical kick, no time-dependent coupling.
+static void build_pump_tables(const mdqt_params* p, QTConst& q, FastTab& f) {
+    const double r = 0.0617, h = q.h;                          // decayRatio (:118)
+    // channel j = |a_j><b_j|: 408 a = {0,0,0,1,1,1,6,6,6,6}, 422 a = {1,1,0,0,4,4}; only b enters D
+    static const int B408[10] = {2, 3, 4, 3, 4, 5, 2, 3, 4, 5};
+    const double G408[10] = {1, 2. / 3, 1. / 3, 1. / 3, 2. / 3, 1, r, r, r, r};
+    static const int B422[6] = {2, 3, 3, 2, 2, 3};
+    const double G422[6] = {2. / 3, 1. / 3, 2. / 3, 1. / 3, r, r};
+    const int m = p->qt_model;
+    const int nch = m == 3 ? 6 : 10;
+    double D[NS] = {0.};
+    for (int j = 0; j < nch; ++j) {
+        const int b = m == 3 ? B422[j] : B408[j];
+        D[b] += m == 3 ? G422[j] : G408[j];
+    }
+    // couplings (row, col, sqrt(gs) factor): |a><b| and its conjugate
+    struct Cp { int a, b; double g; };
+    Cp cp[4];
+    int ncp = 0;
+    if (m == 1) { cp[0] = {1, 3, G408[3]}; cp[1] = {1, 5, G408[5]}; cp[2] = {0, 2, G408[0]}; cp[3] = {0, 4, G408[2]}; ncp = 4; }
+    if (m == 2) { cp[0] = {1, 5, G408[5]}; cp[1] = {0, 4, G408[2]}; ncp = 2; }
+    if (m == 3) { cp[0] = {1, 2, G422[0]}; cp[1] = {0, 3, G422[2]}; ncp = 2; }
+    memset(&f, 0, sizeof f);
+    for (int k = 0; k < 16; ++k)
+        for (int j = 0; j < 3; ++j) f.col[j][k] = k < NS ? kFastColM[m][k][j] : k;
+    const int nst = kModelStates[m];
+    const int nP = m == 3 ? 2 : 4;
+    for (int k = 0; k < nst; ++k) {
+        f.mre[k] = 1. + h * (-0.5 * D[k]);
+        f.hdp[k] = h * D[k];
+        double e1 = 0.;
+        if (k >= 2 && k < 2 + nP) e1 = (k < 2 + nP / 2) ? -1. : 1.;   // right (-v) / left (+v) P levels
+        const double e0 = (k >= 2 && k < 2 + nP) ? -p->detuning : 0.;
+        f.mi0[k] = -(h * e0);
+        f.mi1[k] = -(h * e1);
+    }
+    for (int c = 0; c < ncp; ++c) {
+        const double v = (-p->Om / 2) * sqrt(cp[c].g);      // H_ab = H_ba = v; M = -i h v
+        const int rc[2][2] = {{cp[c].a, cp[c].b}, {cp[c].b, cp[c].a}};
+        for (const auto& e : rc)
+            for (int j = 0; j < 3; ++j)
+                if (kFastColM[m][e[0]][j] == e[1]) { f.cre[j][e[0]] = 0.; f.cim[j][e[0]] = -(h * v); }
+    }
+    f.cphi = 0.;
+    q.kickS = q.kickD = 0.;
+    q.vKick = q.vKickDP = 0.;
 }
 
 static void build_constants(mdqt_ctx* s) {
@@ -252,6 +304,7 @@ static void build_constants(mdqt_ctx* s) {
     q.thD[3][0] = gs[8] * gs[8] / r;   q.thD[3][1] = gs[8] * gs[8] / r + gs[7] * gs[7] / r;       // :675-697
     for (int k = 0; k < 18; ++k) q.gs[k] = gs[k];
     q.renorm = p->reNormalizewvFns;
+    q.model = p->qt_model;
     q.seed = p->seed; q.job = p->job;
     for (int i = 0; i < NBINS; ++i) s->vel[i] = (double)i * 0.0025;   // :340-344
     // lane tables of the lane-per-state kernel: row k of M, slots A < B < C by column
@@ -335,6 +388,7 @@ static void build_constants(mdqt_ctx* s) {
         for (int j = 0; j < 3; ++j)
             if (kFastCol[w.row][j] == w.col) f.kw[j][w.row] = w.sgn * (w.scale * gs[w.g]);
     f.cphi = 2. * (1. + q.kRat) * q.gamToE;
+    if (p->qt_model != 0) build_pump_tables(p, q, f);
     f.dt2 = (0.5 * q.dtQ) * (0.5 * q.dtQ);
     for (int k = 0; k < 4; ++k) q.hdPh[k] = f.hdp[2 + k];
 }
@@ -505,6 +559,9 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
     if (p->world_size < 1 || p->rank < 0 || p->rank >= p->world_size) return fail("bad world_size/rank");
     if (p->N0 < 1) return fail("N0 must be >= 1");
     if (p->sampleFreq < 1) return fail("sampleFreq must be >= 1");
+    if (p->qt_model < 0 || p->qt_model >= NMODELS) return fail("qt_model must be 0..%d", NMODELS - 1);
+    if (p->qt_model != 0 && p->rng_mode != 1)
+        return fail("the optical-pumping qt_models run on the Philox stream (rng_mode 1)");
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev < 1) return fail("no HIP device available (%s)", hipGetErrorString(e));
@@ -907,6 +964,7 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
     if (local_reduce(s)) return -1;
     HIPCHK(hipSetDevice(s->dev));
     const int do_qt = do_qt_flag && s->p.qt_enabled;
+    if (do_qt && s->p.qt_model != 0 && s->qt_math != 2) return fail("the optical-pumping qt_models need qt_math 2");
     const bool d48 = do_qt && s->p.rng_mode == 0;
     while (n > 0) {
         const int m = d48 ? 1 : (n < MAXSUB ? n : MAXSUB);   // drand48: the stream orders ions per substep
@@ -947,6 +1005,31 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         }
         n -= m;
     }
+    return 0;
+}
+
+// measureSpinUps / tagParticles of the optical-pumping programs (see include/mdqt.h)
+extern "C" int mdqt_tag_spin_up(mdqt_ctx* s, int* tags, int* n_up) {
+    if (!s) return fail("NULL context");
+    if (s->p.qt_model == 0) return fail("mdqt_tag_spin_up: qt_model 0 (laser cooling) has no spin tagging");
+    HIPCHK(hipSetDevice(s->dev));
+    const int n = s->nloc;
+    int* d = nullptr;
+    if (n > 0) {
+        HIPCHK(hipMalloc(&d, (size_t)n * sizeof(int)));
+        HIPCHK(launch_tag_spin_up(s->dPsi, n, s->S, (uint64_t)s->lo, s->qidx, s->qc, d, s->stream));
+    }
+    std::vector<int> h((size_t)n, 0);
+    if (n > 0) {
+        HIPCHK(hipMemcpyAsync(h.data(), d, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        HIPCHK(hipFree(d));
+    }
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) cnt += h[i];
+    if (tags)
+        for (int i = 0; i < n; ++i) tags[s->lo + i] = h[i];
+    if (n_up) *n_up = cnt;
     return 0;
 }
 
@@ -1115,8 +1198,13 @@ extern "C" int mdqt_observables(mdqt_ctx* s, double out7[7], double* Pvel, doubl
             const double* w = psi.data() + (size_t)24 * i;
             auto nrm = [&](int k) { return w[2 * k] * w[2 * k] + w[2 * k + 1] * w[2 * k + 1]; };
             pops[3 * i + 0] = nrm(0) + nrm(1);
-            pops[3 * i + 1] = nrm(2) + nrm(3) + nrm(4) + nrm(5);
-            pops[3 * i + 2] = nrm(6) + nrm(7) + nrm(8) + nrm(9) + nrm(10) + nrm(11);
+            if (s->p.qt_model == 3) {                       // 422 pumping: P = 2, 3; D = 4
+                pops[3 * i + 1] = nrm(2) + nrm(3);
+                pops[3 * i + 2] = nrm(4);
+            } else {
+                pops[3 * i + 1] = nrm(2) + nrm(3) + nrm(4) + nrm(5);
+                pops[3 * i + 2] = nrm(6) + nrm(7) + nrm(8) + nrm(9) + nrm(10) + nrm(11);
+            }
         }
     }
     return 0;
@@ -1351,8 +1439,14 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         choose_segments(s);
         return ensure_aux(s);
     }
+    if (!strcmp(name, "qt_enabled")) {                 // pump window of the tagging programs
+        if (value < 0 || value > 1) return fail("qt_enabled must be 0 or 1");
+        s->p.qt_enabled = value;
+        return 0;
+    }
     if (!strcmp(name, "qt_math")) {
         if (value < 0 || value > 2) return fail("qt_math must be 0 (exact), 1 (FMA-contracted) or 2 (reassociated)");
+        if (value != 2 && s->p.qt_model != 0) return fail("the optical-pumping qt_models need qt_math 2");
         s->qt_math = value;
         return 0;
     }

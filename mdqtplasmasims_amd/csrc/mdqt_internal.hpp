@@ -38,6 +38,7 @@ struct QTConst {
     double thD[4][2];           // cumulative D-decay thresholds per P level (:612-697)
     double gs[18];
     int renorm;                 // reNormalizewvFns (:706-712)
+    int model;                  // QT model (QTModel): level scheme, couplings and jump rule
     uint32_t seed, job;         // Philox key
 };
 
@@ -61,8 +62,27 @@ struct LaneTab {
 // at k itself with a zero coefficient; the time-dependent entry of rows 4, 5, 8, 9 sits in slot
 // 2).  Both QT kernels evaluate every row as the same fixed FMA chain over these slots, so the
 // thread-per-ion and lane-per-state forms stay bit-identical.
-constexpr int kFastCol[NS][3] = {{3, 5, 0}, {2, 4, 1},  {1, 9, 11}, {0, 8, 10}, {1, 7, 9},   {0, 6, 8},
-                                 {5, 6, 6}, {4, 7, 7}, {3, 8, 5},   {2, 9, 4},  {3, 10, 10}, {2, 11, 11}};
+//
+// QT models (mdqt_params.qt_model): 0 = the SpeedUp Sr+ 12-level laser cooling (default);
+// the optical-pumping ("spin tagging") variants, one per reference program family:
+//   1 = 408 nm linear, 7 levels   randomFrozenStartTag408Linear.cpp:396, MonteCarloFollowedByQTTagging408Linear.cpp:555
+//   2 = 408 nm quad,   7 levels   randomFrozenStartTag408Quad.cpp (qstep :399: 2 couplings)
+//   3 = 422 nm linear, 5 levels   randomFrozenStartTag422Linear.cpp:390, MonteCarloFollowedByQTTagging422Linear.cpp:552
+// Levels of the pumping models: 0 S-1/2, 1 S+1/2, P levels from 2, then one D level (6 or 4).
+// They have no optical-force kick, no time-dependent coupling and no jump kick; the kernels
+// are the same template with another sparse H (FastTab) and jump table (jump_target_pump).
+constexpr int NMODELS = 4;
+constexpr int kModelStates[NMODELS] = {12, 7, 7, 5};
+constexpr int kFastColM[NMODELS][NS][3] = {
+    {{3, 5, 0}, {2, 4, 1}, {1, 9, 11}, {0, 8, 10}, {1, 7, 9}, {0, 6, 8},
+     {5, 6, 6}, {4, 7, 7}, {3, 8, 5}, {2, 9, 4}, {3, 10, 10}, {2, 11, 11}},
+    {{2, 4, 0}, {3, 5, 1}, {0, 2, 2}, {1, 3, 3}, {0, 4, 4}, {1, 5, 5},
+     {6, 6, 6}, {7, 7, 7}, {8, 8, 8}, {9, 9, 9}, {10, 10, 10}, {11, 11, 11}},
+    {{4, 0, 0}, {5, 1, 1}, {2, 2, 2}, {3, 3, 3}, {0, 4, 4}, {1, 5, 5},
+     {6, 6, 6}, {7, 7, 7}, {8, 8, 8}, {9, 9, 9}, {10, 10, 10}, {11, 11, 11}},
+    {{3, 0, 0}, {2, 1, 1}, {1, 2, 2}, {0, 3, 3}, {4, 4, 4}, {5, 5, 5},
+     {6, 6, 6}, {7, 7, 7}, {8, 8, 8}, {9, 9, 9}, {10, 10, 10}, {11, 11, 11}}};
+inline constexpr const int (&kFastCol)[NS][3] = kFastColM[0];
 struct FastTab {
     int col[3][16];              // kFastCol, lanes 12..15 point at themselves
     double cre[3][16], cim[3][16];   // static M entries of the slots (0 for unused / dynamic)
@@ -183,6 +203,10 @@ constexpr int kLaneKernelMaxIons = 98304;
 hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s);
 // qt_math 2: the reassociated kernels of mdqt_qtfast.hip (same modes as launch_substeps)
 hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s);
+// measureSpinUps (randomFrozenStartTag408Linear.cpp:600, :422Linear) / tagParticles
+// (MonteCarloFollowedByQTTagging408Linear.cpp:1022): tag[i] = 1 with probability of spin up
+hipError_t launch_tag_spin_up(const double* psi, int n, int S, uint64_t gid0, uint64_t q, const QTConst& qc,
+                              int* tags, hipStream_t s);
 // deterministic sums: out[0] = sum vx; needs scratch >= 1024 doubles
 hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s);
 // out[0..2] = sum 0.5 (vx-avg)^2, 0.5 vy^2, 0.5 vz^2 ; out[3] = sum of rows[0..nrows) of

@@ -100,12 +100,36 @@ __device__ __forceinline__ int jump_target(const QTConst& qc, double n3, double 
     return (rand3 < qc.thD[3][0]) ? 8 : (rand3 < qc.thD[3][1]) ? 7 : 6;
 }
 
+// quantum jump of the optical-pumping models (no kick).  Draws in the reference's order: u1,
+// rand2, randDOrS, then 408: randDir (unused), [rand3]; 422: [rand3] — i.e. rand3 is draw 4 for
+// 408 (randomFrozenStartTag408Linear.cpp:521-590) and draw 3 for 422 (...422Linear.cpp:174-231)
+__device__ __forceinline__ int jump_target_pump(const QTConst& qc, double n3, double n4, double n5, double n6,
+                                                double rand2, double randDOrS, double d3, double d4,
+                                                double& kick) {
+    kick = 0.;
+    const bool sDecay = !(randDOrS < qc.pD);
+    if (qc.model == 3) {                            // 422: P levels 2, 3; D level 4
+        const double tot = n3 + n4;
+        const double prob3 = n3 / tot;
+        if (rand2 < prob3) return sDecay ? ((d3 < 2. / 3) ? 1 : 0) : 4;
+        return sDecay ? ((d3 < 2. / 3) ? 0 : 1) : 4;
+    }
+    const double tot = n3 + n4 + n5 + n6;           // 408: P levels 2..5; D level 6
+    const double prob3 = n3 / tot, prob4 = n4 / tot, prob5 = n5 / tot;
+    if (rand2 < prob3) return sDecay ? 0 : 6;
+    if (rand2 < prob3 + prob4) return sDecay ? ((d4 < 2. / 3) ? 0 : 1) : 6;
+    if (rand2 < prob3 + prob4 + prob5) return sDecay ? ((d4 < 1. / 3) ? 0 : 1) : 6;
+    return sDecay ? 1 : 6;
+}
+
 __device__ __forceinline__ double sq(cxd y) { return y.re * y.re + y.im * y.im; }
 
 // ------------------------------------------------------------------------------------------
 // thread per ion
 // ------------------------------------------------------------------------------------------
+template <int MODEL>
 __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab* __restrict__ tab) {
+    constexpr const int(&COL)[NS][3] = kFastColM[MODEL];
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     const QTConst& qc = a.qc;
@@ -155,7 +179,7 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
             double kv[16];
 #pragma unroll
             for (int k = 0; k < NS; ++k)
-                kv[k] = kick_term(w[k], w[kFastCol[k][0]], w[kFastCol[k][1]], w[kFastCol[k][2]], T.kw[0][k],
+                kv[k] = kick_term(w[k], w[COL[k][0]], w[COL[k][1]], w[COL[k][2]], T.kw[0][k],
                                   T.kw[1][k], T.kw[2][k]);
 #pragma unroll
             for (int k = NS; k < 16; ++k) kv[k] = 0.;
@@ -184,8 +208,8 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
                 cxd ws[NS];
 #pragma unroll
                 for (int k = 0; k < NS; ++k)
-                    ws[k] = row_r(md[k], y[k], cxd{T.cre[0][k], T.cim[0][k]}, y[kFastCol[k][0]],
-                                  cxd{T.cre[1][k], T.cim[1][k]}, y[kFastCol[k][1]], c2[k], y[kFastCol[k][2]]);
+                    ws[k] = row_r(md[k], y[k], cxd{T.cre[0][k], T.cim[0][k]}, y[COL[k][0]],
+                                  cxd{T.cre[1][k], T.cim[1][k]}, y[COL[k][1]], c2[k], y[COL[k][2]]);
 #pragma unroll
                 for (int k = 0; k < NS; ++k) {
                     const cxd d = {fma(pref, ws[k].re, -y[k].re), fma(pref, ws[k].im, -y[k].im)};
@@ -204,8 +228,10 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
             draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
             draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
             (void)dummy;
-            const int target = jump_target(qc, sq(w[2]), sq(w[3]), sq(w[4]), sq(w[5]), u2, randDOrS, randDir,
-                                           rand3, kick);
+            const int target = MODEL == 0 ? jump_target(qc, sq(w[2]), sq(w[3]), sq(w[4]), sq(w[5]), u2, randDOrS,
+                                                        randDir, rand3, kick)
+                                          : jump_target_pump(qc, sq(w[2]), sq(w[3]), sq(w[4]), sq(w[5]), u2,
+                                                             randDOrS, randDir, rand3, kick);
 #pragma unroll
             for (int k = 0; k < NS; ++k) w[k] = {k == target ? 1. : 0., 0.};
         }
@@ -346,7 +372,8 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
             draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
             draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
             (void)dummy;
-            const int target = jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
+            const int target = qc.model == 0 ? jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick)
+                                             : jump_target_pump(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
             w = {k == target ? 1. : 0., 0.};
         }
         if (qc.renorm) w = [&] {                      // :706-712
@@ -375,8 +402,52 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
     if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
     if (a.nsub > MAXSUB) return hipErrorInvalidValue;
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
-    if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes_r, dim3((a.n + 15) / 16), dim3(256), 0, s, a, tab);
-    else hipLaunchKernelGGL(k_substeps_r, dim3((a.n + 255) / 256), dim3(256), 0, s, a, tab);
+    if (a.qc.model < 0 || a.qc.model >= NMODELS) return hipErrorInvalidValue;
+    const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256);
+    if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes_r, gl, dim3(256), 0, s, a, tab);
+    else if (a.qc.model == 0) hipLaunchKernelGGL(k_substeps_r<0>, gt, dim3(256), 0, s, a, tab);
+    else if (a.qc.model == 1) hipLaunchKernelGGL(k_substeps_r<1>, gt, dim3(256), 0, s, a, tab);
+    else if (a.qc.model == 2) hipLaunchKernelGGL(k_substeps_r<2>, gt, dim3(256), 0, s, a, tab);
+    else hipLaunchKernelGGL(k_substeps_r<3>, gt, dim3(256), 0, s, a, tab);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// spin-up tagging after the pump window: measureSpinUps (randomFrozenStartTag408Linear.cpp:600,
+// randomFrozenStartTag422Linear.cpp:568) = tagParticles (MonteCarloFollowedByQTTagging408Linear.cpp
+// :1022).  Draws: Philox (ion, qstep index, draws 6 and 7) for rand and rand2/rand3.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tag_spin_up(const double* __restrict__ psi, int n, int S, uint64_t gid0,
+                                                     uint64_t q, QTConst qc, int* __restrict__ tags) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double nr[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const double re = psi[(size_t)(2 * k) * S + i], im = psi[(size_t)(2 * k + 1) * S + i];
+        nr[k] = re * re + im * im;                                   // std::norm
+    }
+    double rnd, r2;
+    philox_pair(qc, gid0 + (uint64_t)i, q, 3, rnd, r2);
+    int up;
+    if (qc.model == 3) {                                             // 422 (:592-631)
+        if (rnd < nr[0]) up = 1;
+        else if (rnd < nr[0] + nr[2]) up = r2 < 1. / 3;
+        else if (rnd < nr[0] + nr[2] + nr[3]) up = r2 < 2. / 3;
+        else up = 0;
+    } else {                                                         // 408 (:600-640)
+        if (rnd < nr[0] + nr[2]) up = 1;
+        else if (rnd < nr[0] + nr[2] + nr[3]) up = r2 < 2. / 3;
+        else if (rnd < nr[0] + nr[2] + nr[3] + nr[4]) up = r2 < 1. / 3;
+        else up = 0;
+    }
+    tags[i] = up;
+}
+
+hipError_t launch_tag_spin_up(const double* psi, int n, int S, uint64_t gid0, uint64_t q, const QTConst& qc,
+                              int* tags, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tag_spin_up, dim3((n + 255) / 256), dim3(256), 0, s, psi, n, S, gid0, q, qc, tags);
     return hipGetLastError();
 }
 

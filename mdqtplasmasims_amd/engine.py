@@ -200,6 +200,14 @@ class Simulation:
     def md_steps(self, n: int):
         check(lib().mdqt_md_steps(self.h, int(n)), "md_steps")
 
+    def tag_spin_up(self):
+        """measureSpinUps / tagParticles of the optical-pumping models: (tags[N], n_up)"""
+        tags = np.zeros(self.N, dtype=np.int32)
+        n = C.c_int()
+        check(lib().mdqt_tag_spin_up(self.h, tags.ctypes.data_as(C.POINTER(C.c_int)), C.byref(n)),
+              "tag_spin_up")
+        return tags, n.value
+
     def Epotential(self) -> float:
         e = C.c_double()
         check(lib().mdqt_epotential(self.h, C.byref(e)), "Epotential")

@@ -676,11 +676,180 @@ static int qstep_ion(const orc_sim* s, double t, double expDetuning, double* psi
     return jumped;
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* optical-pumping qstep (randomFrozenStartTag408Linear.cpp:396-598, 408Quad :399, 422Linear   */
+/* :390-566; MonteCarloFollowedByQTTagging*.cpp :555): dense literal restatement               */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct { int nst, nch, ncp; int a[10], b[10]; double g[10]; int ca[4], cb[4], cg[4]; } pump_model;
+
+/* cs[j] = |a_j><b_j|, gs[j] (408 main :1000-1019; 422 main), couplings (:438) */
+static void pump_model_of(int m, double r, pump_model* pm) {
+    static const int A408[10] = {0, 0, 0, 1, 1, 1, 6, 6, 6, 6}, B408[10] = {2, 3, 4, 3, 4, 5, 2, 3, 4, 5};
+    static const int A422[6] = {1, 1, 0, 0, 4, 4}, B422[6] = {2, 3, 3, 2, 2, 3};
+    memset(pm, 0, sizeof(*pm));
+    if (m == 3) {
+        const double G[6] = {2. / 3, 1. / 3, 2. / 3, 1. / 3, r, r};
+        pm->nst = 5; pm->nch = 6;
+        for (int j = 0; j < 6; ++j) { pm->a[j] = A422[j]; pm->b[j] = B422[j]; pm->g[j] = G[j]; }
+        /* -Om/2 wvFn2 wvFn3^H sqrt(gs[0]) - Om/2 wvFn1 wvFn4^H sqrt(gs[2]) (422Linear :97) */
+        pm->ncp = 2; pm->ca[0] = 1; pm->cb[0] = 2; pm->cg[0] = 0; pm->ca[1] = 0; pm->cb[1] = 3; pm->cg[1] = 2;
+    } else {
+        const double G[10] = {1, 2. / 3, 1. / 3, 1. / 3, 2. / 3, 1, r, r, r, r};
+        pm->nst = 7; pm->nch = 10;
+        for (int j = 0; j < 10; ++j) { pm->a[j] = A408[j]; pm->b[j] = B408[j]; pm->g[j] = G[j]; }
+        if (m == 1) {   /* wvFn2 wvFn4^H gs3, wvFn2 wvFn6^H gs5, wvFn1 wvFn3^H gs0, wvFn1 wvFn5^H gs2 */
+            pm->ncp = 4;
+            pm->ca[0] = 1; pm->cb[0] = 3; pm->cg[0] = 3;
+            pm->ca[1] = 1; pm->cb[1] = 5; pm->cg[1] = 5;
+            pm->ca[2] = 0; pm->cb[2] = 2; pm->cg[2] = 0;
+            pm->ca[3] = 0; pm->cb[3] = 4; pm->cg[3] = 2;
+        } else {        /* 408Quad: wvFn2 wvFn6^H gs5, wvFn1 wvFn5^H gs2 */
+            pm->ncp = 2;
+            pm->ca[0] = 1; pm->cb[0] = 5; pm->cg[0] = 5;
+            pm->ca[1] = 0; pm->cb[1] = 4; pm->cg[1] = 2;
+        }
+    }
+}
+
+/* dpmat = sum_j (c * y^H cs_j^H cs_j y) * gs[j] (:419-425); cs_j^H cs_j = |b_j><b_j| */
+static double pump_dp(const pump_model* pm, const cx* y, double c) {
+    double dp = 0.;
+    for (int j = 0; j < pm->nch; ++j) {
+        const cx yb = y[pm->b[j]];
+        dp = dp + (c * cx_mul(cx_conj(yb), yb).re) * pm->g[j];
+    }
+    return dp;
+}
+
+static int qstep_ion_pump(const orc_sim* s, double* psi, double* vx, double* tPart, rngsrc* g) {
+    const orc_params* p = &s->p;
+    const int m = p->qt_model;
+    pump_model pm;
+    pump_model_of(m, s->r, &pm);
+    const int nP = m == 3 ? 2 : 4;
+    const double dtQuant = s->dtQ, gamToE = s->gamToE;
+    const double h = dtQuant * gamToE;
+    cx wvFn[NS];
+    for (int k = 0; k < NS; ++k) wvFn[k] = cx_make(psi[2 * k], psi[2 * k + 1]);
+    const double velQuant = (*vx) * s->plasVelToQuantVel;                       /* :407-408 */
+    *tPart += dtQuant;   /* engine bookkeeping only: the pumping H has no time-dependent term */
+    const double dp = pump_dp(&pm, wvFn, h);                                    /* :419-425 */
+    const double rand = draw(g);                                                /* :426 */
+    int jumped = 0;
+    if (rand > dp) {
+        const double totalDetRightSP = -p->detuning - velQuant;                 /* :436 */
+        const double totalDetLeftSP = -p->detuning + velQuant;                  /* :437 */
+        cx C[NS][NS];
+        memset(C, 0, sizeof(C));
+        for (int c = 0; c < pm.ncp; ++c)                                        /* :438 */
+            C[pm.ca[c]][pm.cb[c]] = cx_add(C[pm.ca[c]][pm.cb[c]], cx_make((-p->Om / 2) * sqrt(pm.g[pm.cg[c]]), 0.));
+        double E[NS] = {0};                                                     /* :439 */
+        for (int k = 2; k < 2 + nP; ++k) E[k] = (k < 2 + nP / 2) ? totalDetRightSP : totalDetLeftSP;
+        double Dd[NS] = {0};                                                    /* :444-447 */
+        for (int j = 0; j < pm.nch; ++j) Dd[pm.b[j]] = Dd[pm.b[j]] + pm.g[j];
+        cx M[NS][NS];
+        const cx sI = cx_make(0., h);
+        for (int a = 0; a < NS; ++a)
+            for (int b = 0; b < NS; ++b) {
+                cx hm = cx_add(cx_add(cx_make(a == b ? E[a] : 0., 0.), C[a][b]), cx_conj(C[b][a]));
+                if (a == b) hm = cx_add(hm, cx_make(0., -0.5 * Dd[a]));          /* hamDecayTerm */
+                M[a][b] = cx_sub(cx_make(a == b ? 1. : 0., 0.), cx_mul(sI, hm));  /* :465 */
+            }
+        const double dtHalf = h / 2, invh = 1. / h;
+        cx y[NS], ws[NS], k1[NS], k2[NS], k3[NS], k4[NS], yk[NS];
+        double pref = 1 / sqrt(1 - pump_dp(&pm, wvFn, h));                    /* :457-468 */
+        matvec(M, wvFn, ws);
+        for (int k = 0; k < NS; ++k) {
+            k1[k] = cx_rscale(invh, cx_sub(cx_rscale(pref, ws[k]), wvFn[k]));
+            yk[k] = cx_add(wvFn[k], cx_rscale(dtHalf, k1[k]));
+        }
+        memcpy(y, yk, sizeof(y));                                               /* :471-481 */
+        pref = 1 / sqrt(1 - pump_dp(&pm, y, h));
+        matvec(M, y, ws);
+        for (int k = 0; k < NS; ++k) {
+            k2[k] = cx_rscale(invh, cx_sub(cx_rscale(pref, ws[k]), y[k]));
+            yk[k] = cx_add(wvFn[k], cx_rscale(dtHalf, k2[k]));
+        }
+        memcpy(y, yk, sizeof(y));                                               /* :486-496 */
+        pref = 1 / sqrt(1 - pump_dp(&pm, y, h));
+        matvec(M, y, ws);
+        for (int k = 0; k < NS; ++k) {
+            k3[k] = cx_rscale(invh, cx_sub(cx_rscale(pref, ws[k]), y[k]));
+            yk[k] = cx_add(wvFn[k], cx_rscale(h, k3[k]));
+        }
+        memcpy(y, yk, sizeof(y));                                               /* :500-510 */
+        pref = 1 / sqrt(1 - pump_dp(&pm, y, h));
+        matvec(M, y, ws);
+        for (int k = 0; k < NS; ++k) k4[k] = cx_rscale(invh, cx_sub(cx_rscale(pref, ws[k]), y[k]));
+        for (int k = 0; k < NS; ++k) {                                          /* :511 */
+            cx sum = cx_add(cx_add(cx_add(k1[k], cx_rscale(3., k2[k])), cx_rscale(3., k3[k])), k4[k]);
+            wvFn[k] = cx_add(wvFn[k], cx_rscale(h, cx_rscale(1. / 8, sum)));
+        }
+    } else {                                                                    /* :513-596 */
+        jumped = 1;
+        *tPart = 0;
+        const double rand2 = draw(g);
+        const double n3 = cx_norm(wvFn[2]), n4 = cx_norm(wvFn[3]);
+        const double n5 = cx_norm(wvFn[4]), n6 = cx_norm(wvFn[5]);
+        for (int k = 0; k < NS; ++k) wvFn[k] = cx_make(0., 0.);
+        int target;
+        const double randDOrS = draw(g);
+        const int sDecay = !(randDOrS < (s->r / (s->r + 1)));
+        if (m == 3) {                                           /* 422Linear :174-231 */
+            const double totalNorm = n3 + n4, prob3 = n3 / totalNorm;
+            if (rand2 < prob3) target = sDecay ? ((draw(g) < 2. / 3) ? 1 : 0) : 4;
+            else target = sDecay ? ((draw(g) < 2. / 3) ? 0 : 1) : 4;
+        } else {                                                /* 408 :513-590 */
+            const double totalNorm = n3 + n4 + n5 + n6;
+            const double prob3 = n3 / totalNorm, prob4 = n4 / totalNorm, prob5 = n5 / totalNorm;
+            (void)draw(g);                                      /* randDir (unused) */
+            if (rand2 < prob3) target = sDecay ? 0 : 6;
+            else if (rand2 < prob3 + prob4) target = sDecay ? ((draw(g) < 2. / 3) ? 0 : 1) : 6;
+            else if (rand2 < prob3 + prob4 + prob5) target = sDecay ? ((draw(g) < 1. / 3) ? 0 : 1) : 6;
+            else target = sDecay ? 1 : 6;
+        }
+        wvFn[target] = cx_make(1., 0.);
+    }
+    (void)pm.a;
+    for (int k = 0; k < NS; ++k) { psi[2 * k] = wvFn[k].re; psi[2 * k + 1] = wvFn[k].im; }
+    return jumped;
+}
+
+int orc_tag_spin_up(const orc_sim* s, int* tags) {
+    const int m = s->p.qt_model;
+    if (m == 0) return -1;
+    int cnt = 0;
+    for (int i = 0; i < s->N; ++i) {
+        const double* w = s->psi + (size_t)24 * i;
+        double nr[5];
+        for (int k = 0; k < 5; ++k) nr[k] = w[2 * k] * w[2 * k] + w[2 * k + 1] * w[2 * k + 1];
+        const double rnd = orc_philox_uniform(s->p.seed, s->p.job, (uint64_t)i, s->qidx, 6);
+        const double r2 = orc_philox_uniform(s->p.seed, s->p.job, (uint64_t)i, s->qidx, 7);
+        int up;
+        if (m == 3) {                                           /* 422Linear :568-600 */
+            if (rnd < nr[0]) up = 1;
+            else if (rnd < nr[0] + nr[2]) up = r2 < 1. / 3;
+            else if (rnd < nr[0] + nr[2] + nr[3]) up = r2 < 2. / 3;
+            else up = 0;
+        } else {                                                /* 408Linear :600-640 */
+            if (rnd < nr[0] + nr[2]) up = 1;
+            else if (rnd < nr[0] + nr[2] + nr[3]) up = r2 < 2. / 3;
+            else if (rnd < nr[0] + nr[2] + nr[3] + nr[4]) up = r2 < 1. / 3;
+            else up = 0;
+        }
+        if (tags) tags[i] = up;
+        cnt += up;
+    }
+    return cnt;
+}
+
 int orc_qstep_ion(const orc_sim* s, double t, double* psi, double* vx, double* tPart,
                   const double u[5], int* ndraws) {
     rngsrc g; memset(&g, 0, sizeof(g));
     g.mode = 2; g.tape = u;
-    int j = qstep_ion(s, t, expDetuning_of(s, t), psi, vx, tPart, &g);
+    int j = s->p.qt_model != 0 ? qstep_ion_pump(s, psi, vx, tPart, &g)
+                               : qstep_ion(s, t, expDetuning_of(s, t), psi, vx, tPart, &g);
     if (ndraws) *ndraws = g.n;
     return j;
 }
@@ -693,8 +862,10 @@ void orc_qstep(orc_sim* s) {
             /* drand48: one shared stream consumed in ion order (1-thread reference) */
             rngsrc g; memset(&g, 0, sizeof(g));
             g.mode = 0; g.x48 = &s->x48;
-            for (int i = 0; i < s->N; i++)
-                qstep_ion(s, s->t, expDet, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
+            for (int i = 0; i < s->N; i++) {
+                if (s->p.qt_model != 0) qstep_ion_pump(s, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
+                else qstep_ion(s, s->t, expDet, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
+            }
         } else {
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static) num_threads(s->p.nthreads > 0 ? s->p.nthreads : 1)
@@ -702,7 +873,8 @@ void orc_qstep(orc_sim* s) {
             for (int i = 0; i < s->N; i++) {
                 rngsrc g; memset(&g, 0, sizeof(g));
                 g.mode = 1; g.seed = s->p.seed; g.job = s->p.job; g.ion = (uint64_t)i; g.qidx = s->qidx;
-                qstep_ion(s, s->t, expDet, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
+                if (s->p.qt_model != 0) qstep_ion_pump(s, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
+                else qstep_ion(s, s->t, expDet, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
             }
         }
         (void)c;

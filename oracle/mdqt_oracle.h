@@ -54,6 +54,8 @@ typedef struct orc_params {
     uint32_t seed;        /* value given to srand48 (reference: time(NULL)+job, SpeedUp:1219) */
     uint32_t job;         /* SpeedUp:1145 */
     int nthreads;         /* OpenMP threads for the race-free parallel loops (1 = serial) */
+    int qt_model;         /* 0 = SpeedUp 12-level cooling; 1/2/3 = 408 linear / 408 quad / 422 linear
+                           * optical pumping (randomFrozenStartTag*.cpp qstep; Philox only) */
     char saveDirectory[256]; /* SpeedUp:56 */
 } orc_params;
 
@@ -127,6 +129,9 @@ double orc_philox_uniform(uint32_t seed, uint32_t job, uint64_t ion, uint64_t qs
  * psi[24] in/out, *vx in/out (kick applied), *tPart in/out; u[5] are the uniforms u1..u5
  * the reference would draw (only u[0] used when no jump).  t is the global time used for the
  * expanding-frame detuning.  Returns 1 if a quantum jump occurred, 0 otherwise. */
+/* spin-up tagging of the pumping models (measureSpinUps, randomFrozenStartTag408Linear.cpp:600,
+ * randomFrozenStartTag422Linear.cpp:568): Philox draws 6 and 7 of (ion, current qstep index) */
+int    orc_tag_spin_up(const orc_sim* s, int* tags);
 int    orc_qstep_ion(const orc_sim* s, double t, double* psi, double* vx, double* tPart,
                      const double u[5], int* ndraws);
 

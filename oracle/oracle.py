@@ -27,7 +27,7 @@ class OrcParams(C.Structure):
         ("detuningDP", C.c_double), ("Om", C.c_double), ("OmDP", C.c_double),
         ("N0", C.c_int), ("newRun", C.c_int), ("c0", C.c_int), ("sampleFreq", C.c_int),
         ("reNormalizewvFns", C.c_int), ("qt_enabled", C.c_int), ("rng_mode", C.c_int),
-        ("seed", C.c_uint32), ("job", C.c_uint32), ("nthreads", C.c_int),
+        ("seed", C.c_uint32), ("job", C.c_uint32), ("nthreads", C.c_int), ("qt_model", C.c_int),
         ("saveDirectory", C.c_char * 256),
     ]
 
@@ -100,6 +100,8 @@ def lib():
         L.orc_philox_uniform.restype = C.c_double
         L.orc_philox_uniform.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_int]
         L.orc_qstep_ion.argtypes = [C.c_void_p, C.c_double, _dp, _dp, _dp, _dp, C.POINTER(C.c_int)]
+        L.orc_tag_spin_up.restype = C.c_int
+        L.orc_tag_spin_up.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -201,6 +203,12 @@ class OracleSim:
 
     def qstep(self):
         lib().orc_qstep(self.h)
+
+    def tag_spin_up(self):
+        """measureSpinUps / tagParticles of the pumping models: (tags[N], n_up)"""
+        tags = np.zeros(self.N, dtype=np.int32)
+        n = lib().orc_tag_spin_up(self.h, tags.ctypes.data_as(C.POINTER(C.c_int)))
+        return tags, n
 
     def substeps(self, n: int):
         lib().orc_substeps(self.h, n)

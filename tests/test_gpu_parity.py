@@ -265,6 +265,93 @@ def test_md_steps_short_horizon(eng, orc, qt, qt_math):
         assert np.array_equal(a["tPart"] == 0, b["tPart"] == 0)
 
 
+PUMP = [(1, dict(Om=0.7, detuning=-2.5)), (2, dict(Om=2.0, detuning=0.0)), (3, dict(Om=1.3, detuning=-1.0))]
+
+
+@pytest.mark.parametrize("model,kw", PUMP)
+def test_pump_qstep_matches_oracle(eng, orc, model, kw):
+    """optical-pumping qstep (randomFrozenStartTag408Linear/408Quad/422Linear.cpp) vs the oracle"""
+    kw = dict(kw, qt_model=model, N0=300, seed=21, rng_mode=1)
+    o = orc.OracleSim(nthreads=4, **kw).init()
+    o.md_steps(3)
+    st = o.get_state()
+    s = eng.Simulation(**kw)
+    s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+    s.set_forces(st["F"])
+    s.qstep_index = o.qstep_index
+    for _ in range(5):
+        s.qstep(); o.qstep()
+    a, b = s.get_state(), o.get_state()
+    assert np.abs(a["psi"] - b["psi"]).max() < 1e-12
+    assert np.array_equal(a["V"], b["V"])            # no optical force, no jump kick
+    assert np.array_equal(a["tPart"] == 0, b["tPart"] == 0)
+    n = 5 if model == 3 else 7
+    assert np.all(a["psi"][:, n:, :] == 0)
+
+
+@pytest.mark.parametrize("model,kw", PUMP)
+def test_pump_jumps_and_md_steps(eng, orc, model, kw):
+    """forced P population: many jumps through the model's jump table; then 3 MD steps"""
+    kw = dict(kw, qt_model=model, N0=400, seed=5, rng_mode=1)
+    o = orc.OracleSim(nthreads=4, **kw).init()
+    st = o.get_state()
+    n = 5 if model == 3 else 7
+    rng = np.random.default_rng(model)
+    z = np.zeros((st["psi"].shape[0], 12), complex)
+    z[:, :n] = rng.normal(size=(z.shape[0], n)) + 1j * rng.normal(size=(z.shape[0], n))
+    z /= np.linalg.norm(z, axis=1, keepdims=True)
+    psi = np.stack([z.real, z.imag], -1)
+    s = eng.Simulation(**kw)
+    for x in (s, o):
+        x.set_state(st["R"], st["V"], psi, st["tPart"], 0.0)
+    s.md_steps(3); o.md_steps(3)
+    a, b = s.get_state(), o.get_state()
+    njump = int((b["tPart"] < 3 * 25 * 8e-5 - 1e-12).sum())
+    assert njump > 20
+    assert np.array_equal(a["tPart"] < 3 * 25 * 8e-5 - 1e-12, b["tPart"] < 3 * 25 * 8e-5 - 1e-12)
+    assert np.abs(a["psi"] - b["psi"]).max() < 1e-9
+    assert np.abs(a["R"] - b["R"]).max() < 1e-10
+    assert np.abs(a["V"] - b["V"]).max() < 1e-10
+
+
+@pytest.mark.parametrize("model,kw", PUMP)
+def test_pump_lane_and_thread_kernels_bit_identical(eng, model, kw):
+    sims = []
+    for mode in (1, 2):
+        s = eng.Simulation(N0=500, seed=31, qt_model=model, **kw).init()
+        s.set_option("substep_kernel", mode)
+        s.md_steps(3)
+        sims.append(s.get_state())
+    for k in ("R", "V", "psi", "tPart"):
+        assert np.array_equal(sims[0][k], sims[1][k]), k
+
+
+@pytest.mark.parametrize("model,kw", PUMP)
+def test_tag_spin_up_matches_oracle(eng, orc, model, kw):
+    """measureSpinUps / tagParticles: same state, same draws -> the same tags"""
+    kw = dict(kw, qt_model=model, N0=2000, seed=44, rng_mode=1)
+    o = orc.OracleSim(nthreads=4, **kw).init()
+    o.md_steps(2)
+    st = o.get_state()
+    s = eng.Simulation(**kw)
+    s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+    s.qstep_index = o.qstep_index
+    ta, na = s.tag_spin_up()
+    tb, nb = o.tag_spin_up()
+    assert na == nb and np.array_equal(ta, tb)
+    assert 0 < na < len(ta)
+
+
+def test_pump_models_reject_unsupported_modes(eng):
+    s = eng.Simulation(N0=200, qt_model=1)
+    with pytest.raises(RuntimeError):
+        s.set_option("qt_math", 0)
+    with pytest.raises(RuntimeError):
+        eng.Simulation(N0=200, qt_model=1, rng_mode=0)
+    with pytest.raises(RuntimeError):
+        eng.Simulation(N0=200).tag_spin_up()
+
+
 def test_substeps_fusion_equals_single_substeps(eng):
     """one fused launch of n substeps == n launches of one (bit for bit)"""
     a = eng.Simulation(N0=400, seed=5).init()

@@ -197,6 +197,53 @@ def test_qstep_kat_single_P_level(orc):
     assert np.all(res["psi"][np.r_[0:4, 6:24]] == 0)
 
 
+@pytest.mark.parametrize("model,Om,det", [(1, 0.7, -2.5), (2, 2.0, 0.0), (3, 1.3, -1.0)])
+def test_pump_qstep_matches_dense_transcription(orc, model, Om, det):
+    """optical-pumping qstep (randomFrozenStartTag*.cpp) of the oracle vs the numpy transcription:
+    the no-jump RK branch to 1e-14, every jump branch exactly"""
+    from tests import dense_pump
+    rng = np.random.default_rng(7 + model)
+    n = 5 if model == 3 else 7
+    s = orc.OracleSim(qt_model=model, Om=Om, detuning=det)
+    for trial in range(20):
+        z = np.zeros(12, complex)
+        z[:n] = rng.normal(size=n) + 1j * rng.normal(size=n)
+        z /= np.linalg.norm(z)
+        vx = rng.normal(0, 0.3)
+        res = s.qstep_ion(0.0, np.stack([z.real, z.imag], -1).reshape(-1), vx, 0.01, [1.0, 0, 0, 0, 0])
+        d_psi, d_vx, d_tp, d_j = dense_pump.qstep_ion(z, vx, 0.01, [1.0], model, Om, det)
+        assert not res["jumped"] and not d_j
+        got = res["psi"].reshape(12, 2)
+        assert np.abs(got[:, 0] + 1j * got[:, 1] - d_psi).max() < 1e-14
+        assert res["vx"] == vx                       # no optical force in the pumping models
+    targets = set()
+    for trial in range(600):
+        z = np.zeros(12, complex)
+        z[:n] = rng.normal(size=n) + 1j * rng.normal(size=n)
+        z /= np.linalg.norm(z)
+        u = [0.0] + list(rng.uniform(size=4))
+        res = s.qstep_ion(0.0, np.stack([z.real, z.imag], -1).reshape(-1), 0.1, 0.02, u)
+        d_psi, d_vx, d_tp, d_j = dense_pump.qstep_ion(z, 0.1, 0.02, u, model, Om, det)
+        assert res["jumped"] and d_j
+        got = res["psi"].reshape(12, 2)
+        assert np.array_equal(got[:, 0] + 1j * got[:, 1], d_psi)
+        assert res["vx"] == 0.1 and res["tPart"] == 0.0
+        targets.add(int(np.argmax(np.abs(d_psi))))
+    assert targets == ({0, 1, 4} if model == 3 else {0, 1, 6})
+
+
+def test_pump_kat_decay_matrix(orc):
+    """KAT: the pumping decay matrix sum_j gs[j] cs_j^H cs_j is (1 + r) on every P level for both
+    level schemes (408: 1 + r, 2/3 + 1/3 + r, 1/3 + 2/3 + r, 1 + r; 422: 2/3 + 1/3 + r each)"""
+    from tests import dense_pump
+    for model in (1, 3):
+        n, w, cs, gs = dense_pump.operators(model)
+        D = sum(gs[j] * cs[j].conj().T @ cs[j] for j in range(len(cs)))
+        P = range(2, 6) if model == 1 else range(2, 4)
+        for k in range(n):
+            assert abs(D[k, k] - ((1 + dense_pump.decayRatio) if k in P else 0.)) < 1e-15
+
+
 def test_run_layout_and_formats(orc, tmp_path):
     s = orc.OracleSim(N0=60, tmax=0.09, sampleFreq=5, seed=99, job=3, rng_mode=0,
                       saveDirectory=str(tmp_path) + "/")

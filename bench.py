@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--qt-math", type=int, default=2, choices=[0, 1, 2],
                     help="0: the reference's exact QT operations, 1: FMA-contracted, 2: reassociated "
                          "(option qt_math, the library default)")
+    ap.add_argument("--no-pump-lines", action="store_true",
+                    help="skip the optical-pumping model lines (SURVEY §8(f)3)")
     ap.add_argument("--timing-period", type=int, default=8,
                     help="bracket every k-th kernel launch of the timed region with HIP events")
     return ap.parse_args()
@@ -191,6 +193,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(params, qt, args.cpu_seconds, 12345 + job, job)
+        if world == 1 and not args.no_pump_lines:
+            out["pump_models"] = pump_lines(local)
     sim.close()
     # secondary line item: one large system sharded over all ranks (RCCL all-gather per MD step)
     if args.sharded_config != "none":
@@ -202,6 +206,35 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+PUMP_MODELS = [
+    (1, dict(Om=0.7, detuning=-2.5), "408 nm linear pumping, 7 levels (randomFrozenStartTag408Linear.cpp)"),
+    (2, dict(Om=2.0, detuning=0.0), "408 nm quad pumping, 7 levels (randomFrozenStartTag408Quad.cpp)"),
+    (3, dict(Om=1.3, detuning=-1.0), "422 nm linear pumping, 5 levels (randomFrozenStartTag422Linear.cpp)"),
+]
+
+
+def pump_lines(local, steps=100):
+    """the optical-pumping QT models on the C2 system: MD + pump qsteps"""
+    import torch
+    import mdqtplasmasims_amd as M
+    res = []
+    for model, kw, desc in PUMP_MODELS:
+        sim = M.Simulation(device=local, N0=3500, seed=12346, job=1, qt_model=model, **kw).init()
+        ratio = int(sim.const("plasmaToQuantumTimestepRatio"))
+        sim.md_steps(10)
+        sim.synchronize()
+        t0 = time.perf_counter()
+        sim.md_steps(steps)
+        sim.synchronize()
+        el = time.perf_counter() - t0
+        res.append({"qt_model": model, "workload": desc + ", N0=3500, density 2", "N": sim.N,
+                    "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
+                    "value": sim.N * ratio * steps / el, "unit": "particle-qsteps/s"})
+        sim.close()
+    torch.cuda.synchronize()
+    return res
 
 
 def sharded_run(cfg, steps, rank, world, local, dist, barrier):

@@ -1,4 +1,4 @@
-"""ctypes binding of libmdqt.so (the C ABI declared in include/mdqt.h).
+"""ctypes binding of libmdqt.so (the C ABIs declared in include/mdqt.h and include/mdmc.h).
 
 The library is built in-tree (``python -m mdqtplasmasims_amd.build`` or ``__graft_entry__.build()``)
 into ``mdqtplasmasims_amd/lib/libmdqt.so``.  There is no fallback: if the library is missing or
@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MDQT_LIB: an alternative build of the same library (kernel A/B experiments, tools/expt.sh)
 LIB_PATH = os.environ.get("MDQT_LIB") or os.path.join(HERE, "lib", "libmdqt.so")
 CLI_PATH = os.path.join(HERE, "bin", "mdqt")
+MDMC_CLI_PATH = os.path.join(HERE, "bin", "mdmc")
 
 _dp = C.POINTER(C.c_double)
 
@@ -30,6 +31,49 @@ class MdqtParams(C.Structure):
         ("saveDirectory", C.c_char * 256),
     ]
 
+
+class MdmcParams(C.Structure):
+    """mirror of ``struct mdmc_params`` (include/mdmc.h)."""
+    _fields_ = [
+        ("N", C.c_int), ("kappa", C.c_double), ("Gamma", C.c_double), ("n", C.c_double),
+        ("collisionFreq", C.c_double), ("monteCarloSteps", C.c_int), ("maxRStep", C.c_double),
+        ("pairPairStep", C.c_double), ("timeStep", C.c_double), ("numPreRecordMDSteps", C.c_int),
+        ("numVelAutoCorrsSteps", C.c_int), ("numInstantaneousAnisotropySteps", C.c_int),
+        ("numReestablishEquilSteps", C.c_int), ("tempPercentDiff", C.c_double),
+        ("applyForceAlongOneAxisOnly", C.c_int), ("beta", C.c_double),
+        ("anisotropyEstablishmentTime", C.c_int), ("anisotropyFromForcesRelaxSteps", C.c_int),
+        ("seed", C.c_uint32), ("job", C.c_uint32), ("device", C.c_int), ("force_kernel", C.c_int),
+        ("saveDirectory", C.c_char * 256),
+    ]
+
+
+_ip = C.POINTER(C.c_int)
+
+# include/mdmc.h
+MDMC_SIGNATURES = [
+    ("mdmc_default_params", None, [C.POINTER(MdmcParams)]),
+    ("mdmc_create", C.c_int, [C.POINTER(MdmcParams), C.POINTER(C.c_void_p)]),
+    ("mdmc_destroy", None, [C.c_void_p]),
+    ("mdmc_get_const", C.c_double, [C.c_void_p, C.c_char_p]),
+    ("mdmc_init", C.c_int, [C.c_void_p]),
+    ("mdmc_monte_carlo", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_longlong)]),
+    ("mdmc_md_steps", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdmc_set_collision_freq", C.c_int, [C.c_void_p, C.c_double]),
+    ("mdmc_set_laser_force", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdmc_pair_corr", C.c_int, [C.c_void_p, _dp, C.c_int, _ip]),
+    ("mdmc_record_velocities", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdmc_autocorrelations", C.c_int, [C.c_void_p, _dp]),
+    ("mdmc_set_velocity_store", C.c_int, [C.c_void_p, _dp]),
+    ("mdmc_temperatures", C.c_int, [C.c_void_p, _dp]),
+    ("mdmc_anisotropize", C.c_int, [C.c_void_p]),
+    ("mdmc_tag_particles", C.c_int, [C.c_void_p, _ip]),
+    ("mdmc_tagged_moments", C.c_int, [C.c_void_p, _dp]),
+    ("mdmc_get_state", C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp]),
+    ("mdmc_set_state", C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp]),
+    ("mdmc_setup_directories", C.c_int, [C.c_void_p]),
+    ("mdmc_save_directory", C.c_char_p, [C.c_void_p]),
+    ("mdmc_run", C.c_int, [C.c_void_p, C.c_int]),
+]
 
 # (name, restype, argtypes) of every symbol include/mdqt.h declares
 SIGNATURES = [
@@ -103,7 +147,7 @@ def lib():
             raise MdqtError(f"{LIB_PATH} not built: run `python -m mdqtplasmasims_amd.build` "
                             "(the MDQT engine has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
-        for name, res, args in SIGNATURES:
+        for name, res, args in SIGNATURES + MDMC_SIGNATURES:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -168,6 +168,18 @@ extern "C" void mdqt_default_params(mdqt_params* p) {
 }
 
 extern "C" const char* mdqt_last_error(void) { return g_err.c_str(); }
+
+namespace mdqt {
+int set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+}  // namespace mdqt
 extern "C" const char* mdqt_version(void) { return "mdqt-mi355x 0.1 (gfx950)"; }
 
 extern "C" int mdqt_device_count(void) {

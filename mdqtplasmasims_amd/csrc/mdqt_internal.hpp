@@ -175,6 +175,43 @@ struct N3BArgs {
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 
+// ---- Monte-Carlo + MD analytics program (mdmc_kernels.hip) ----
+struct MCArgs {
+    double* R;          // [3][S]
+    double* U;          // [N] per-particle potential energies (MCMD:123)
+    double* D;          // [N] scratch: the candidate U'
+    uint32_t* mt;       // [625]: std::mt19937 state words + position (in/out)
+    unsigned long long* accepted;   // in/out
+    int N, S, nsteps;
+    double L, kappa, rCut, maxRStep, Gamma;
+};
+struct VVArgs {
+    double* V;
+    const double* A;
+    const double* Aold;
+    const double* hits;        // [nhits][4] = (i, vx, vy, vz): this step's collisions (host-drawn)
+    int nhits;
+    int N, S, laser, oneAxis;
+    double dt, p6, beta, sqrtn; // p6 = pow(10, -6), sqrtn = sqrt(n) (MCMD:491-496)
+};
+hipError_t launch_particle_potentials(const double* R, int N, int S, double L, double kappa, double rCut, double* U,
+                                      hipStream_t s);
+hipError_t launch_monte_carlo(const MCArgs& a, hipStream_t s);
+hipError_t launch_vv_positions(double* R, const double* V, const double* A, double* Aold, int N, int S, double dt,
+                               double L, hipStream_t s);
+hipError_t launch_vv_velocities(const VVArgs& a, hipStream_t s);   // + the collision scatter when nhits > 0
+hipError_t launch_pair_hist(const double* R, int N, int S, double L, double step, int nbins, unsigned* hist,
+                            hipStream_t s);
+int autocorr_blocks(int N);
+hipError_t launch_autocorr(const double* vs, int N, int T, double c2, double c4, double* part, double* out,
+                           hipStream_t s);
+hipError_t launch_temperatures(const double* V, int N, int S, double* out, hipStream_t s);
+hipError_t launch_tag_moments(const double* V, const int* tags, int N, double* out, hipStream_t s);
+hipError_t launch_anisotropize(double* V, int N, int S, double tpd, hipStream_t s);
+hipError_t launch_store_velocities(const double* V, int N, int S, int T, int t, double* vs, hipStream_t s);
+// error message of the C ABI (mdqt_last_error), shared by the mdmc_* entry points
+int set_error(const char* fmt, ...);
+
 // drand48 in the reference's order (SpeedUp:486, :575-687: ions in index order, 1 draw per
 // ion, 4-5 for a quantum jump): one workgroup assigns every ion its uniforms from the single
 // stream, by LCG jump-ahead from the stream state, restarting after each (rare) jump.

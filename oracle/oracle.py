@@ -334,3 +334,149 @@ def ref_step_positions(R, V, A):
     V = np.ascontiguousarray(V, dtype=np.float64); A = np.ascontiguousarray(A, dtype=np.float64)
     ref().mdref_step_positions(_p(R), _p(V), _p(A))
     return R
+
+
+class RefMCMD:
+    """The reference's MonteCarloFollowedByMDAndTempAnisotropy.cpp program state (its globals in
+    oracle/_ref/libmdref.so, one instance per process), with its mt19937 reseeded.  Stages are the
+    reference's own functions (oracle/ref/ref_harness.cpp)."""
+
+    N = 4096
+    T = 2500
+
+    def __init__(self, seed: int, save_directory: str = "data/"):
+        L = ref()
+        if not getattr(L, "_mcmd_bound", False):
+            L.mdref_seed.argtypes = [C.c_uint]
+            L.mdref_set_collision_freq.argtypes = [C.c_double]
+            L.mdref_set_laser_force.argtypes = [C.c_int]
+            L.mdref_set_save_directory.argtypes = [C.c_char_p]
+            L.mdref_get.argtypes = [_dp, _dp, _dp, _dp]
+            L.mdref_set.argtypes = [_dp, _dp, _dp, _dp]
+            L.mdref_monte_carlo.argtypes = [C.c_int]
+            L.mdref_md_steps.argtypes = [C.c_int]
+            L.mdref_pair_corr.argtypes = [C.c_int]
+            L.mdref_autocorrelations.argtypes = [_dp, C.c_int, _dp]
+            L.mdref_record_temp_axes.argtypes = [C.c_int]
+            L.mdref_tag_particles.argtypes = [C.POINTER(C.c_int)]
+            L.mdref_tagged_moments.argtypes = [C.c_int]
+            L._mcmd_bound = True
+        self.L = L
+        L.mdref_seed(int(seed))
+        L.mdref_set_collision_freq(0.25)
+        L.mdref_set_laser_force(0)
+        self.set_save_directory(save_directory)
+
+    def set_save_directory(self, d: str):
+        self.L.mdref_set_save_directory(d.encode())
+
+    def init(self):
+        self.L.mdref_init()
+
+    def monte_carlo(self, n: int):
+        self.L.mdref_monte_carlo(int(n))
+
+    def md_steps(self, n: int):
+        self.L.mdref_md_steps(int(n))
+
+    def set_collision_freq(self, f: float):
+        self.L.mdref_set_collision_freq(float(f))
+
+    def set_laser_force(self, on: bool):
+        self.L.mdref_set_laser_force(int(bool(on)))
+
+    def get_state(self):
+        R = np.zeros((3, 4096)); V = np.zeros((3, 4096)); A = np.zeros((3, 4096)); U = np.zeros(4096)
+        self.L.mdref_get(_p(R), _p(V), _p(A), _p(U))
+        return R, V, A, U
+
+    def set_state(self, R=None, V=None, A=None, U=None):
+        arr = [None if x is None else np.ascontiguousarray(x, dtype=np.float64) for x in (R, V, A, U)]
+        self.L.mdref_set(*[None if x is None else _p(x) for x in arr])
+
+    def pair_corr_file(self, step: int):      # writes <dir>pairPairCorrStepNum<step>.dat
+        self.L.mdref_pair_corr(int(step))
+
+    def autocorrelations(self, vs: np.ndarray) -> np.ndarray:   # vs [3][4096][T] -> [4][T]
+        vs = np.ascontiguousarray(vs, dtype=np.float64)
+        T = vs.shape[2]
+        out = np.zeros((4, 2500))
+        self.L.mdref_autocorrelations(_p(vs), T, _p(out))
+        return out[:, :T]
+
+    def record_temperature(self):
+        self.L.mdref_record_temperature()
+
+    def record_temp_axes(self, step: int):
+        self.L.mdref_record_temp_axes(int(step))
+
+    def tag_particles(self) -> np.ndarray:
+        t = np.zeros((4, 4096), dtype=np.int32)
+        self.L.mdref_tag_particles(t.ctypes.data_as(C.POINTER(C.c_int)))
+        return t
+
+    def tagged_moments_file(self, step: int):
+        self.L.mdref_tagged_moments(int(step))
+
+
+# ---------------------------------------------------------------------------------------------
+# restatements for MonteCarloFollowedByMDAndTempAnisotropy.cpp ("MCMD", SURVEY §8(f)4)
+# ---------------------------------------------------------------------------------------------
+def mcmd_autocorrelations(vs: np.ndarray, Gamma: float) -> np.ndarray:
+    """VAF, longViscAutoCorr, vCubeAutoCorr, vFourthAutoCorr of MCMD:655-807 over vs [3][N][T]:
+    out[f][td] = sum_{i, j < T-td} term_f(j, j+td) / (N (T - td)), with the -3/Gamma^2 and
+    -27/Gamma^4 offsets of :710 / :785 applied once per term.  Lag sums through a zero-padded
+    FFT (float64): equal to the reference's direct sums up to summation rounding."""
+    vs = np.asarray(vs, dtype=np.float64)
+    _, N, T = vs.shape
+    n = 1 << int(np.ceil(np.log2(2 * T)))
+
+    def lagsum(a):                      # sum over (component, particle) of sum_j a[j] a[j + td]
+        f = np.fft.rfft(a, n=n, axis=-1)
+        return np.fft.irfft((f * np.conj(f)).sum(axis=(0, 1)), n=n)[:T]
+
+    cnt = N * (T - np.arange(T)).astype(np.float64)
+    v2 = vs * vs
+    out = np.empty((4, T))
+    out[0] = lagsum(vs) / cnt
+    out[1] = lagsum(v2) / cnt - 3 / (Gamma * Gamma)
+    out[2] = lagsum(v2 * vs) / cnt
+    out[3] = lagsum(v2 * v2) / cnt - 3 * 9 / (Gamma * Gamma * Gamma * Gamma)
+    return out
+
+
+class MT19937:
+    """std::mt19937 (C++ [rand.predef]) + libstdc++'s generate_canonical<double, 53> behind
+    uniform_real_distribution<double>(0, 1) (MCMD:53-54): u = (g1 + g2 2^32) / 2^64, values >= 1
+    mapped to the largest double below 1.  The restatement the device MC kernel follows."""
+
+    def __init__(self, seed: int = 5489):
+        x = [0] * 624
+        x[0] = seed & 0xFFFFFFFF
+        for i in range(1, 624):
+            x[i] = (1812433253 * (x[i - 1] ^ (x[i - 1] >> 30)) + i) & 0xFFFFFFFF
+        self.x, self.p = x, 624
+
+    def _twist(self):
+        x = self.x
+        for k in range(624):
+            y = (x[k] & 0x80000000) | (x[(k + 1) % 624] & 0x7FFFFFFF)
+            x[k] = x[(k + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+        self.p = 0
+
+    def __call__(self) -> int:
+        if self.p >= 624:
+            self._twist()
+        z = self.x[self.p]
+        self.p += 1
+        z ^= z >> 11
+        z ^= (z << 7) & 0x9D2C5680
+        z ^= (z << 15) & 0xEFC60000
+        z ^= z >> 18
+        return z & 0xFFFFFFFF
+
+    def uniform(self) -> float:
+        s = float(self())
+        s = s + float(self()) * 4294967296.0
+        r = s / 18446744073709551616.0
+        return r if r < 1.0 else float(np.nextafter(1.0, 0.0))

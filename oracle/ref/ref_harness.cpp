@@ -3,11 +3,16 @@
 // /root/reference/MonteCarloFollowedByMDAndTempAnisotropy.cpp (its main() is renamed by a
 // -D flag so this file can call its functions).  It gives the tests the reference's own
 // Yukawa force law / minimum image / cutoff (calculateAccelerations :387-448, calcAIJ
-// :161-169), pair potential (calculatePotentialEnergyForParticles :207-244, calcUIJ :153-159)
-// and position update + periodic wrap (stepPositions :453-467).
-// Reference globals (N = 4096, kappa = 0.5, L = (4096*4pi/3)^(1/3)) are fixed by that file.
+// :161-169), pair potential (calculatePotentialEnergyForParticles :207-244, calcUIJ :153-159),
+// position update + periodic wrap (stepPositions :453-467), and — with its global mt19937
+// reseeded (the reference seeds it from std::random_device, :52-53) — its init (:173-203),
+// Metropolis MC (:315-382), velocity-Verlet MD with collisions (:469-511), g(r) (:584-652),
+// velocity autocorrelations (:655-807), tagging (:810-921, :923-1028) and temperatures.
+// Reference globals (N = 4096, kappa = 0.5, Gamma = 3, L = (4096*4pi/3)^(1/3)) are fixed by that file.
+#include <cstdio>
 #include <cstring>
 #include <omp.h>
+#include <random>
 
 extern double R[3][4096];
 extern double V[3][4096];
@@ -15,9 +20,33 @@ extern double A[3][4096];
 extern double U[4096];
 extern double L;
 extern double rCut;
+extern double collisionFreq;
+extern int addLaserForce;
+extern char saveDirectory[256];
+extern std::mt19937 rng;
+extern std::uniform_real_distribution<double> uni;
+extern std::normal_distribution<double> velocityDistribution;
+extern double vStore[3][4096][2500];
+extern double VAF[2500];
+extern double longViscAutoCorr[2500];
+extern double vCubeAutoCorr[2500];
+extern double vFourthAutoCorr[2500];
+extern bool taggedOne[4096], taggedTwo[4096], taggedThree[4096], taggedFour[4096];
+void init();
+void MonteCarloStep();
 void calculateAccelerations(int tS);
 void calculatePotentialEnergyForParticles();
 void stepPositions();
+void MDStep(int tS);
+void recordPairPairCorr(int stepNum);
+void recordVAF(void);
+void recordLongViscAutoCorr(void);
+void recordVCubeAutoCorr(void);
+void recordVFourthAutoCorr(void);
+void recordTemperature(void);
+void tagParticles();
+void recordTaggedParticleMoments(int step);
+void recordTempForEachAxis(char fileName[256], int step);
 double calcUIJ(double totalDist);
 double calcAIJ(double totalDist);
 
@@ -49,4 +78,68 @@ void mdref_step_positions(double* Rio, const double* Vin, const double* Ain) {
     stepPositions();
     std::memcpy(Rio, R, sizeof(R));
 }
+
+// ---- seeded program stages (the reference's own code; only the seed is ours) ----
+// rng as right after the program's static initialisation with seed s: mt19937 seeded, one
+// uniform drawn by `auto random_double = uni(rng);` (:52-55)
+void mdref_seed(unsigned s) {
+    rng.seed(s);
+    uni.reset();
+    velocityDistribution.reset();
+    (void)uni(rng);
+}
+void mdref_set_collision_freq(double f) { collisionFreq = f; }
+void mdref_set_laser_force(int on) { addLaserForce = on; }
+void mdref_set_save_directory(const char* d) {
+    std::strncpy(saveDirectory, d, sizeof(saveDirectory) - 1);
+    saveDirectory[sizeof(saveDirectory) - 1] = 0;
+}
+void mdref_get(double* Ro, double* Vo, double* Ao, double* Uo) {
+    if (Ro) std::memcpy(Ro, R, sizeof(R));
+    if (Vo) std::memcpy(Vo, V, sizeof(V));
+    if (Ao) std::memcpy(Ao, A, sizeof(A));
+    if (Uo) std::memcpy(Uo, U, sizeof(U));
+}
+void mdref_set(const double* Ri, const double* Vi, const double* Ai, const double* Ui) {
+    if (Ri) std::memcpy(R, Ri, sizeof(R));
+    if (Vi) std::memcpy(V, Vi, sizeof(V));
+    if (Ai) std::memcpy(A, Ai, sizeof(A));
+    if (Ui) std::memcpy(U, Ui, sizeof(U));
+}
+void mdref_init() { init(); calculatePotentialEnergyForParticles(); }   // main() steps 1-2 (:1062-1065)
+void mdref_monte_carlo(int n) { for (int k = 0; k < n; ++k) MonteCarloStep(); }
+void mdref_md_steps(int n) {
+    omp_set_num_threads(1);
+    for (int k = 0; k < n; ++k) MDStep(k);
+}
+void mdref_pair_corr(int step) { recordPairPairCorr(step); }          // writes pairPairCorrStepNum<k>.dat
+// vin: [3][4096][T] (T <= 2500, the rest zero); out: VAF, longVisc, vCube, vFourth [4][2500]
+void mdref_autocorrelations(const double* vin, int T, double* out) {
+    std::memset(vStore, 0, sizeof(vStore));
+    for (int c = 0; c < 3; ++c)
+        for (int i = 0; i < 4096; ++i)
+            for (int t = 0; t < T; ++t) vStore[c][i][t] = vin[((size_t)c * 4096 + i) * T + t];
+    recordVAF();
+    recordLongViscAutoCorr();
+    recordVCubeAutoCorr();
+    recordVFourthAutoCorr();
+    std::memcpy(out, VAF, sizeof(VAF));
+    std::memcpy(out + 2500, longViscAutoCorr, sizeof(VAF));
+    std::memcpy(out + 5000, vCubeAutoCorr, sizeof(VAF));
+    std::memcpy(out + 7500, vFourthAutoCorr, sizeof(VAF));
+}
+void mdref_record_temperature() { recordTemperature(); }              // appends temperature.dat
+void mdref_record_temp_axes(int step) {                               // appends tempAxes.dat
+    char f[256];
+    std::snprintf(f, sizeof f, "%stempAxes.dat", saveDirectory);
+    recordTempForEachAxis(f, step);
+}
+void mdref_tag_particles(int* tags4) {                                  // [4][4096]
+    tagParticles();
+    for (int i = 0; i < 4096; ++i) {
+        tags4[i] = taggedOne[i]; tags4[4096 + i] = taggedTwo[i];
+        tags4[8192 + i] = taggedThree[i]; tags4[12288 + i] = taggedFour[i];
+    }
+}
+void mdref_tagged_moments(int step) { recordTaggedParticleMoments(step); }   // appends taggedV*Moments.dat
 }

@@ -1,0 +1,256 @@
+"""Parity of the Monte-Carlo + MD analytics engine (include/mdmc.h) with the
+reference program MonteCarloFollowedByMDAndTempAnisotropy.cpp ("MCMD").
+
+The oracle here is the reference itself: its source built unmodified into oracle/_ref/libmdref.so
+(oracle/ref/Makefile), its global std::mt19937 reseeded (oracle.RefMCMD), plus the committed
+golden autocorrelations (tests/golden/make_mcmd_golden.py) and the numpy/Python restatements in
+oracle/oracle.py (FFT lag sums, mt19937 + generate_canonical).
+
+Tolerances (per test):
+  * init (lattice + Maxwellian draws) and the MC trajectory: positions bit for bit (same mt19937
+    stream, same Metropolis decisions); U <= 1e-12 relative (libm exp ulps and the parallel order
+    of the energy sums);
+  * MD steps: <= 1e-10 absolute after 10 steps (the device force is the reciprocal Yukawa form,
+    <= 2 ulp per pair from the reference's pow(r,-3) form; summation order differs);
+  * g(r): every bin equal (integer counts, same normalisation expression);
+  * autocorrelations: <= 1e-9 of the largest term (10^7-term sums in different orders).
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden", "mcmd_autocorr.npz")
+
+
+def _velocity_store(**kw):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_mcmd_golden", os.path.join(HERE, "golden", "make_mcmd_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.velocity_store(**kw)
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU: the restatements against the reference's fixtures / known answers
+# ---------------------------------------------------------------------------------------------
+
+def test_mt19937_known_answer(orc):
+    """C++ [rand.predef]: the 10000th invocation of a default-constructed mt19937 is 4123659995."""
+    m = orc.MT19937()
+    for _ in range(9999):
+        m()
+    assert m() == 4123659995
+
+
+def test_generate_canonical_form(orc):
+    m1, m2 = orc.MT19937(42), orc.MT19937(42)
+    for _ in range(100):
+        u = m1.uniform()
+        g1, g2 = m2(), m2()
+        assert u == (g1 + g2 * 2.0 ** 32) / 2.0 ** 64 and 0.0 <= u < 1.0
+
+
+def test_autocorrelation_restatement_matches_reference_golden(orc):
+    g = np.load(GOLD)
+    vs = _velocity_store(seed=int(g["seed"]))
+    assert np.allclose([vs.sum(), (vs * vs).sum()], g["vs_checksum"], rtol=0, atol=1e-9)
+    out = orc.mcmd_autocorrelations(vs, 3.0)
+    ref = g["out"]
+    for f in range(4):
+        scale = np.abs(ref[f]).max() + (3 / 9.0 if f == 1 else 27 / 81.0 if f == 3 else 0)
+        assert np.abs(out[f] - ref[f]).max() <= 1e-9 * scale, f
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: the HIP path through the C ABI against the reference program
+# ---------------------------------------------------------------------------------------------
+
+@pytest.fixture(scope="module")
+def mc():
+    import mdqtplasmasims_amd as M
+    from mdqtplasmasims_amd import mdmc
+    if M.device_count() < 1:
+        pytest.fail("no GPU visible to the gpu-marked tests")
+    return mdmc
+
+
+@pytest.fixture(scope="module")
+def refmc(orc):
+    if not orc.ref_available():
+        pytest.fail("oracle/_ref/libmdref.so not built (oracle/ref/Makefile)")
+    return orc
+
+
+def _pair(mc, refmc, seed, tmp):
+    ref = refmc.RefMCMD(seed=seed, save_directory=tmp + "/")
+    eng = mc.MonteCarloMD(seed=seed, saveDirectory=tmp + "/")
+    return ref, eng
+
+
+@pytest.mark.gpu
+def test_init_matches_reference(mc, refmc):
+    with tempfile.TemporaryDirectory() as tmp:
+        ref, eng = _pair(mc, refmc, 11, tmp)
+        ref.init()
+        eng.init()
+        R0, V0, A0, U0 = ref.get_state()
+        R1, V1, A1, U1 = eng.get_state()
+        assert np.array_equal(R0, R1)          # i*L/pow(N,1/3.) + 0.5
+        assert np.array_equal(V0, V1)          # the reference's normal_distribution draws
+        assert np.abs(U1 - U0).max() <= 1e-13 * np.abs(U0).max()
+        assert eng.const("L") == refmc.ref().mdref_L()
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_monte_carlo_matches_reference(mc, refmc):
+    with tempfile.TemporaryDirectory() as tmp:
+        ref, eng = _pair(mc, refmc, 12, tmp)
+        ref.init(); eng.init()
+        ref.monte_carlo(1500); acc = eng.monte_carlo(1500)
+        ref.monte_carlo(1500); acc += eng.monte_carlo(1500)   # the rng state handed over twice
+        R0, V0, _, U0 = ref.get_state()
+        R1, V1, _, U1 = eng.get_state()
+        assert 0 < acc <= 3000
+        assert np.array_equal(R0, R1)
+        assert np.abs(U1 - U0).max() <= 1e-12 * np.abs(U0).max()
+        # the rng streams agree after the anneal: the tag rolls are the reference's
+        assert np.array_equal(ref.tag_particles(), eng.tag_particles())
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_md_steps_with_collisions_and_laser_match_reference(mc, refmc):
+    with tempfile.TemporaryDirectory() as tmp:
+        ref, eng = _pair(mc, refmc, 13, tmp)
+        ref.init(); eng.init()
+        ref.monte_carlo(500); eng.monte_carlo(500)
+        R, V, A, U = ref.get_state()
+        assert np.array_equal(R, eng.get_state()[0])
+        ref.set_collision_freq(20.0); eng.set_collision_freq(20.0)     # ~10% of ions collide per step
+        ref.md_steps(4); eng.md_steps(4)
+        ref.set_collision_freq(0.0); eng.set_collision_freq(0.0)
+        ref.set_laser_force(True); eng.set_laser_force(True)
+        ref.md_steps(3); eng.md_steps(3)
+        ref.set_laser_force(False); eng.set_laser_force(False)
+        ref.md_steps(3); eng.md_steps(3)
+        R0, V0, A0, _ = ref.get_state()
+        R1, V1, A1, _ = eng.get_state()
+        assert np.abs(R1 - R0).max() <= 1e-10
+        assert np.abs(V1 - V0).max() <= 1e-10
+        assert np.abs(A1 - A0).max() <= 1e-10 * max(1.0, np.abs(A0).max())
+        assert np.array_equal(ref.tag_particles(), eng.tag_particles())
+        eng.close()
+
+
+def _read_cols(path):
+    return np.loadtxt(path, ndmin=2)
+
+
+@pytest.mark.gpu
+def test_pair_corr_temperatures_and_moments_match_reference(mc, refmc):
+    with tempfile.TemporaryDirectory() as tmp:
+        ref, eng = _pair(mc, refmc, 14, tmp)
+        ref.init(); eng.init()
+        ref.monte_carlo(2000); eng.monte_carlo(2000)
+        ref.pair_corr_file(7)
+        gref = _read_cols(os.path.join(tmp, "pairPairCorrStepNum7.dat"))
+        g = eng.pair_corr()
+        assert g.size == gref.shape[0] == int(eng.const("nbins"))
+        assert np.array_equal(np.array([float("%lg" % x) for x in g]), gref[:, 1])
+        # temperatures (recordTemperature, recordTempForEachAxis) and tagged moments
+        ref.record_temperature(); ref.record_temp_axes(3)
+        t = eng.temperatures()
+        assert float("%lg" % t[0]) == _read_cols(os.path.join(tmp, "temperature.dat"))[0, 0]
+        ax = _read_cols(os.path.join(tmp, "tempAxes.dat"))[0]
+        assert np.array_equal([float("%lg" % x) for x in t[1:]], ax[1:])
+        tags = ref.tag_particles()
+        assert np.array_equal(tags, eng.tag_particles())
+        ref.tagged_moments_file(5)
+        m = eng.tagged_moments()
+        names = ["One", "Two", "Three", "Four"]
+        for k in range(4):
+            row = _read_cols(os.path.join(tmp, f"taggedV{names[k]}Moments.dat"))[0]
+            assert row[0] == float("%lg" % (5 * 0.005))
+            np.testing.assert_allclose(m[k], row[1:], rtol=2e-5, atol=1e-6)
+        # anisotropize (:548-558): exact scalings
+        _, V0, _, _ = eng.get_state()
+        eng.anisotropize()
+        _, V1, _, _ = eng.get_state()
+        assert np.array_equal(V1[0], np.sqrt(1 + 0.15) * V0[0])
+        assert np.array_equal(V1[1], np.sqrt(1 - 0.15 / 2) * V0[1])
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_autocorrelations_match_reference_golden(mc, orc):
+    g = np.load(GOLD)
+    vs = _velocity_store(seed=int(g["seed"]))
+    eng = mc.MonteCarloMD()
+    eng.set_velocity_store(vs)
+    out = eng.autocorrelations()
+    ref = g["out"]
+    for f in range(4):
+        scale = np.abs(ref[f]).max() + (3 / 9.0 if f == 1 else 27 / 81.0 if f == 3 else 0)
+        assert np.abs(out[f] - ref[f]).max() <= 1e-9 * scale, f
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 70, 300])
+def test_autocorrelations_small_T_match_restatement(mc, orc, T):
+    vs = _velocity_store(seed=5, N=4096, T=T)
+    eng = mc.MonteCarloMD(numVelAutoCorrsSteps=T)
+    eng.set_velocity_store(vs)
+    out = eng.autocorrelations()
+    o = orc.mcmd_autocorrelations(vs, 3.0)
+    for f in range(4):
+        assert np.abs(out[f] - o[f]).max() <= 1e-11 * (np.abs(o[f]).max() + 1), f
+    # recordVelsForAutocorrelations: the store is what the steps recorded
+    eng.init()
+    for k in range(min(T, 3)):
+        eng.record_velocities(k)
+        eng.md_steps(1)
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_run_writes_the_reference_files(mc):
+    """main()'s stages at reduced sizes: every file the reference writes, with its row counts."""
+    with tempfile.TemporaryDirectory() as tmp:
+        eng = mc.MonteCarloMD(N=512, monteCarloSteps=20000, numPreRecordMDSteps=20, numVelAutoCorrsSteps=150,
+                              numInstantaneousAnisotropySteps=30, numReestablishEquilSteps=10,
+                              anisotropyEstablishmentTime=1, anisotropyFromForcesRelaxSteps=25, job=3,
+                              saveDirectory=tmp + "/", seed=9)
+        eng.run()
+        d = os.path.join(tmp, "Gamma300Kappa50NumIons512", "job3")
+        assert os.path.isdir(d)
+        nb = int(eng.const("nbins"))
+        for k in (0, 10000, 100):
+            assert _read_cols(os.path.join(d, f"pairPairCorrStepNum{k}.dat")).shape == (nb, 2)
+        assert _read_cols(os.path.join(d, "temperature.dat")).shape == (150, 1)
+        for f in ("VAF", "longViscAutoCorr", "vCubeAutoCorr", "vFourthAutoCorr"):
+            a = _read_cols(os.path.join(d, f + ".dat"))
+            assert a.shape == (150, 2) and np.isfinite(a).all()
+        for k in ("One", "Two", "Three", "Four"):
+            assert _read_cols(os.path.join(d, f"taggedV{k}Moments.dat")).shape == (150, 5)
+        nest = int(round(.8 * 1 * np.sqrt(0.4) / 0.005))
+        for f, n in (("Instantaneous", 30), ("DuringForcePeriod", nest), ("AfterForcePeriod", 25)):
+            a = _read_cols(os.path.join(d, f"TemperaturesAlongAxes{f}.dat"))
+            assert a.shape == (n, 4)
+        T = _read_cols(os.path.join(d, "temperature.dat"))[:, 0]
+        assert np.all(np.abs(T - 1 / 3) < 0.1)       # equilibrated near 1/Gamma
+        eng.close()
+
+
+def test_mdmc_create_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from mdqtplasmasims_amd import mdmc
+    from mdqtplasmasims_amd._lib import MdqtError
+    with pytest.raises(MdqtError):
+        mdmc.MonteCarloMD()

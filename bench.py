@@ -57,6 +57,8 @@ def parse():
                          "(option qt_math, the library default)")
     ap.add_argument("--no-pump-lines", action="store_true",
                     help="skip the optical-pumping model lines (SURVEY §8(f)3)")
+    ap.add_argument("--no-mcmd-lines", action="store_true",
+                    help="skip the Monte-Carlo + MD analytics program line (SURVEY §8(f)4)")
     ap.add_argument("--timing-period", type=int, default=8,
                     help="bracket every k-th kernel launch of the timed region with HIP events")
     return ap.parse_args()
@@ -195,6 +197,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(params, qt, args.cpu_seconds, 12345 + job, job)
         if world == 1 and not args.no_pump_lines:
             out["pump_models"] = pump_lines(local)
+        if world == 1 and not args.no_mcmd_lines:
+            out["mcmd"] = mcmd_line(local, cpu=not args.no_cpu_baseline)
     sim.close()
     # secondary line item: one large system sharded over all ranks (RCCL all-gather per MD step)
     if args.sharded_config != "none":
@@ -235,6 +239,58 @@ def pump_lines(local, steps=100):
         sim.close()
     torch.cuda.synchronize()
     return res
+
+
+def mcmd_line(local, cpu=True, mc_steps=20000, md_steps=2000):
+    """MonteCarloFollowedByMDAndTempAnisotropy.cpp at its own size, N = 4096:
+    Metropolis steps/s, MD steps/s (collisionless and collisional), the analytics, and the whole
+    main() estimated from the stage rates; beside it the reference build (oracle/_ref) on 1 core."""
+    import tempfile
+    import numpy as np
+    from mdqtplasmasims_amd import mdmc
+    tmp = tempfile.mkdtemp(prefix="mcmd_bench_")
+    e = mdmc.MonteCarloMD(device=local, seed=3, saveDirectory=tmp + "/")
+    p = e.p
+    e.init()
+    e.monte_carlo(1000)
+    t0 = time.perf_counter(); acc = e.monte_carlo(mc_steps); mc_s = time.perf_counter() - t0
+    e.md_steps(50)
+    rates = {}
+    for cf in (0.0, 0.25):
+        e.set_collision_freq(cf)
+        t0 = time.perf_counter(); e.md_steps(md_steps); rates[cf] = md_steps / (time.perf_counter() - t0)
+    t0 = time.perf_counter(); e.pair_corr(); g_ms = (time.perf_counter() - t0) * 1e3
+    vs = np.random.default_rng(1).normal(0, 0.5, (3, e.N, e.T))
+    e.set_velocity_store(vs)
+    e.autocorrelations()
+    t0 = time.perf_counter(); e.autocorrelations(); ac_ms = (time.perf_counter() - t0) * 1e3
+    e.close()
+    mc_rate = mc_steps / mc_s
+    nest = round(.8 * p.anisotropyEstablishmentTime * np.sqrt(p.n) / p.timeStep)
+    n_free = p.numVelAutoCorrsSteps + p.numInstantaneousAnisotropySteps + nest + p.anisotropyFromForcesRelaxSteps
+    n_coll = p.numPreRecordMDSteps + p.numReestablishEquilSteps
+    est = p.monteCarloSteps / mc_rate + n_free / rates[0.0] + n_coll / rates[0.25] + ac_ms / 1e3 \
+        + (p.monteCarloSteps // 10000 + p.numVelAutoCorrsSteps // 100) * g_ms / 1e3
+    line = {"workload": "MonteCarloFollowedByMDAndTempAnisotropy.cpp main(): N=4096, kappa=0.5, Gamma=3 "
+                        "(200000 MC steps, 8712 MD steps, g(r), 4 autocorrelations over 2500 steps)",
+            "N": e.N, "mc_steps_per_s": mc_rate, "mc_acceptance": acc / mc_steps,
+            "md_steps_per_s": rates[0.0], "md_collisional_steps_per_s": rates[0.25],
+            "md_particle_steps_per_s": rates[0.0] * e.N,
+            "pair_corr_ms": g_ms, "autocorrelations_ms": ac_ms, "main_estimate_s": est,
+            "cpu_baseline": None}
+    if cpu:
+        from oracle import oracle as O
+        if O.ref_available():
+            r = O.RefMCMD(seed=3, save_directory=tmp + "/")
+            r.init()
+            t0 = time.perf_counter(); r.monte_carlo(2000); rmc = 2000 / (time.perf_counter() - t0)
+            t0 = time.perf_counter(); r.md_steps(3); rmd = 3 / (time.perf_counter() - t0)
+            rest = p.monteCarloSteps / rmc + (n_free + n_coll) / rmd
+            line["cpu_baseline"] = {"kind": "reference", "cores": 1, "mc_steps_per_s": rmc, "md_steps_per_s": rmd,
+                                    "main_estimate_s": rest,
+                                    "sample": "the reference's MonteCarloStep x2000 and MDStep x3 "
+                                              "(oracle/_ref/libmdref.so, 1 thread)"}
+    return line
 
 
 def sharded_run(cfg, steps, rank, world, local, dist, barrier):

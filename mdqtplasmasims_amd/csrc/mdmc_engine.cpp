@@ -11,8 +11,8 @@
 #include <string.h>
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <random>
-#include <sstream>
 #include <string>
 #include <vector>
 
@@ -28,6 +28,50 @@ using namespace mdqt;
             return set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);   \
     } while (0)
 
+// std::mt19937 ([rand.predef]) with the state in plain view: the same sequence as the
+// reference's engine (so uniform_real_distribution / normal_distribution draw the same values
+// from it), a discard that skips the tempering, and the device MC kernel's [624 words, position]
+// layout without a text round trip.
+struct Mt32 {
+    using result_type = uint32_t;
+    static constexpr result_type min() { return 0u; }
+    static constexpr result_type max() { return 0xffffffffu; }
+    uint32_t x[625];   // x[624] = position
+    void seed(uint32_t s) {
+        x[0] = s;
+        for (uint32_t i = 1; i < 624; ++i) x[i] = 1812433253u * (x[i - 1] ^ (x[i - 1] >> 30)) + i;
+        x[624] = 624;
+    }
+    void twist() {
+        uint32_t* v = x;
+        auto f = [](uint32_t a, uint32_t b, uint32_t m) {
+            const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+            return m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        };
+        for (int k = 0; k < 227; ++k) v[k] = f(v[k], v[k + 1], v[k + 397]);
+        for (int k = 227; k < 623; ++k) v[k] = f(v[k], v[k + 1], v[k - 227]);
+        v[623] = f(v[623], v[0], v[396]);
+        x[624] = 0;
+    }
+    result_type operator()() {
+        if (x[624] >= 624) twist();
+        uint32_t z = x[x[624]++];
+        z ^= z >> 11;
+        z ^= (z << 7) & 0x9d2c5680u;
+        z ^= (z << 15) & 0xefc60000u;
+        z ^= z >> 18;
+        return z;
+    }
+    void discard(unsigned long long n) {
+        while (n) {
+            if (x[624] >= 624) twist();
+            const unsigned long long k = std::min<unsigned long long>(n, 624 - x[624]);
+            x[624] += (uint32_t)k;
+            n -= k;
+        }
+    }
+};
+
 struct mdmc_ctx {
     mdmc_params p;
     int N = 0, S = 0, nbins = 0, T = 0, nt = 0, npairs = 0;
@@ -35,13 +79,15 @@ struct mdmc_ctx {
     double collisionFreq = 0.;
     int addLaserForce = 0;
     // the reference's RNG (MCMD:52-55, :87)
-    std::mt19937 rng;
+    Mt32 rng;
     std::uniform_real_distribution<double> uni{0., 1.};
     std::normal_distribution<double> vd;
     int dev = 0;
     hipStream_t st = nullptr;
-    double *dR = nullptr, *dV = nullptr, *dA = nullptr, *dAold = nullptr, *dU = nullptr, *dD = nullptr;
-    double *dSlots = nullptr, *dNewV = nullptr, *dVS = nullptr, *dPart = nullptr, *dOut = nullptr;
+    double *dR = nullptr, *dV = nullptr, *dA = nullptr, *dU = nullptr, *dD = nullptr;
+    double* dRn = nullptr;          // positions of the next MDStep, pre-advanced by k_vv_step
+    bool rnValid = false;           // dRn == stepPositions(dR, dV, dA): cleared by every other writer
+    double *dSlots = nullptr, *dVS = nullptr, *dPart = nullptr, *dOut = nullptr;
     double *dTemp = nullptr, *dMom = nullptr;   // per-step observables of the run (4 / 20 per step)
     int capTemp = 0;
     int2* dPairs = nullptr;
@@ -68,35 +114,21 @@ double mic_threshold(double L) {   // smallest d with fl(d / L) >= 0.5 (Newton-3
     return d;
 }
 
-// std::mt19937 <-> the device layout [624 words, position] through the engine's text form
+// the rng state to / from the device MC kernel (the same [624 words, position] layout)
 int rng_to_device(mdmc_ctx* c) {
-    std::ostringstream os;
-    os << c->rng;
-    std::istringstream is(os.str());
-    uint32_t h[625];
-    for (int k = 0; k < 625; ++k) {
-        unsigned long long v;
-        if (!(is >> v)) return set_error("mt19937 state serialisation");
-        h[k] = (uint32_t)v;
-    }
-    HIPCHK(hipMemcpyAsync(c->dMT, h, sizeof h, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->dMT, c->rng.x, sizeof c->rng.x, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
 int rng_from_device(mdmc_ctx* c) {
-    uint32_t h[625];
-    HIPCHK(hipMemcpyAsync(h, c->dMT, sizeof h, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(c->rng.x, c->dMT, sizeof c->rng.x, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    std::ostringstream os;
-    for (int k = 0; k < 624; ++k) os << h[k] << ' ';
-    os << h[624];
-    std::istringstream is(os.str());
-    is >> c->rng;
-    if (!is) return set_error("mt19937 state deserialisation");
+    if (c->rng.x[624] > 624) return set_error("device MC kernel returned a bad mt19937 position");
     return 0;
 }
 
-// calculateAccelerations (:387-448): the Newton-3 tile kernel (lDeb = 1/kappa) + slot sum
+// calculateAccelerations (:387-448): the Newton-3 tile kernel (lDeb = 1/kappa); its slots are
+// summed into A by k_vv_step
 int accelerations(mdmc_ctx* c) {
     N3Args a;
     memset(&a, 0, sizeof a);
@@ -105,7 +137,6 @@ int accelerations(mdmc_ctx* c) {
     a.L = c->L; a.lDeb = 1. / c->p.kappa; a.Rcut = c->rCut; a.invlDeb = c->p.kappa;
     a.micT = mic_threshold(c->L); a.micGuard = 1.25 * c->L; a.guard = 0;
     HIPCHK(launch_forces_n3(a, c->p.force_kernel, c->st));
-    HIPCHK(launch_reduce_segments(c->dSlots, c->dA, c->nt, c->N, c->S, 3, c->st));
     return 0;
 }
 
@@ -136,7 +167,7 @@ extern "C" void mdmc_destroy(mdmc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    void* ps[] = {c->dR, c->dV, c->dA, c->dAold, c->dU, c->dD, c->dSlots, c->dNewV, c->dVS, c->dPart, c->dOut,
+    void* ps[] = {c->dR, c->dV, c->dA, c->dRn, c->dU, c->dD, c->dSlots, c->dVS, c->dPart, c->dOut,
                   c->dTemp, c->dMom, c->dPairs, c->dHist, c->dTags, c->dMT, c->dAcc};
     for (void* q : ps)
         if (q) (void)hipFree(q);
@@ -186,9 +217,9 @@ extern "C" int mdmc_create(const mdmc_params* p, mdmc_ctx** out) {
     const size_t S = c->S, sz = S * sizeof(double);
     const int nblk = autocorr_blocks(N);
     bool ok = hipMalloc(&c->dR, 3 * sz) == hipSuccess && hipMalloc(&c->dV, 3 * sz) == hipSuccess &&
-              hipMalloc(&c->dA, 3 * sz) == hipSuccess && hipMalloc(&c->dAold, 3 * sz) == hipSuccess &&
+              hipMalloc(&c->dA, 3 * sz) == hipSuccess && hipMalloc(&c->dRn, 3 * sz) == hipSuccess &&
               hipMalloc(&c->dU, sz) == hipSuccess && hipMalloc(&c->dD, sz) == hipSuccess &&
-              hipMalloc(&c->dSlots, 3 * sz * c->nt) == hipSuccess && hipMalloc(&c->dNewV, 3 * sz) == hipSuccess &&
+              hipMalloc(&c->dSlots, 3 * sz * c->nt) == hipSuccess &&
               hipMalloc(&c->dVS, (size_t)3 * N * c->T * sizeof(double)) == hipSuccess &&
               hipMalloc(&c->dPart, (size_t)nblk * 4 * c->T * sizeof(double)) == hipSuccess &&
               hipMalloc(&c->dOut, (size_t)4 * c->T * sizeof(double)) == hipSuccess &&
@@ -232,6 +263,7 @@ extern "C" double mdmc_get_const(const mdmc_ctx* c, const char* n) {
 // then calculatePotentialEnergyForParticles() :207-245
 extern "C" int mdmc_init(mdmc_ctx* c) {
     if (!c) return set_error("NULL context");
+    c->rnValid = false;
     const int N = c->N, S = c->S;
     const double L = c->L;
     std::vector<double> R((size_t)3 * S, 0.), V((size_t)3 * S, 0.);
@@ -261,6 +293,7 @@ extern "C" int mdmc_init(mdmc_ctx* c) {
 // MonteCarloStep() x nsteps (:315-382) on the device with the reference's mt19937 stream
 extern "C" int mdmc_monte_carlo(mdmc_ctx* c, int nsteps, long long* accepted) {
     if (!c) return set_error("NULL context");
+    c->rnValid = false;
     if (nsteps < 0) return set_error("nsteps < 0");
     HIPCHK(hipSetDevice(c->dev));
     if (rng_to_device(c)) return -1;
@@ -269,6 +302,7 @@ extern "C" int mdmc_monte_carlo(mdmc_ctx* c, int nsteps, long long* accepted) {
     a.R = c->dR; a.U = c->dU; a.D = c->dD; a.mt = c->dMT; a.accepted = c->dAcc;
     a.N = c->N; a.S = c->S;
     a.L = c->L; a.kappa = c->p.kappa; a.rCut = c->rCut; a.maxRStep = c->p.maxRStep; a.Gamma = c->p.Gamma;
+    a.micT = mic_threshold(c->L);
     for (int done = 0; done < nsteps;) {                      // bounded launches
         a.nsteps = std::min(10000, nsteps - done);
         HIPCHK(launch_monte_carlo(a, c->st));
@@ -287,7 +321,9 @@ extern "C" int mdmc_monte_carlo(mdmc_ctx* c, int nsteps, long long* accepted) {
 static int md_step_async(mdmc_ctx* c) {
     const int N = c->N;
     const double dt = c->p.timeStep;
-    HIPCHK(launch_vv_positions(c->dR, c->dV, c->dA, c->dAold, N, c->S, dt, c->L, c->st));   // :452-467
+    if (!c->rnValid)                                                                          // :452-467
+        HIPCHK(launch_vv_positions(c->dR, c->dV, c->dA, c->dRn, N, c->S, dt, c->L, c->st));
+    std::swap(c->dR, c->dRn);
     if (accelerations(c)) return -1;                                                          // :508
     int nh = 0;
     double* hits = nullptr;
@@ -313,10 +349,12 @@ static int md_step_async(mdmc_ctx* c) {
         c->hitOff += nh;
     }
     VVArgs v;
-    v.V = c->dV; v.A = c->dA; v.Aold = c->dAold; v.hits = hits; v.nhits = nh; v.N = N; v.S = c->S;
+    v.V = c->dV; v.A = c->dA; v.slots = c->dSlots; v.nslots = c->nt; v.R = c->dR; v.Rn = c->dRn; v.L = c->L;
+    v.hits = hits; v.nhits = nh; v.N = N; v.S = c->S;
     v.laser = c->addLaserForce; v.oneAxis = c->p.applyForceAlongOneAxisOnly;
     v.dt = dt; v.p6 = pow(10, -6); v.beta = c->p.beta; v.sqrtn = sqrt(c->p.n);
     HIPCHK(launch_vv_velocities(v, c->st));                                                   // :469-502
+    c->rnValid = true;
     return 0;
 }
 
@@ -421,6 +459,7 @@ extern "C" int mdmc_temperatures(mdmc_ctx* c, double out4[4]) {
 
 extern "C" int mdmc_anisotropize(mdmc_ctx* c) {                  // :548-558
     if (!c) return set_error("NULL context");
+    c->rnValid = false;
     HIPCHK(hipSetDevice(c->dev));
     HIPCHK(launch_anisotropize(c->dV, c->N, c->S, c->p.tempPercentDiff, c->st));
     return 0;
@@ -507,8 +546,12 @@ extern "C" int mdmc_get_state(mdmc_ctx* c, double* R, double* V, double* A, doub
 
 extern "C" int mdmc_set_state(mdmc_ctx* c, const double* R, const double* V, const double* A, const double* U) {
     if (!c) return set_error("NULL context");
+    c->rnValid = false;
     HIPCHK(hipSetDevice(c->dev));
     const int N = c->N, S = c->S;
+    if (R)   // the kernels' division-free minimum image needs |dx| < 1.25 L: the box of :262-271, :459-464
+        for (size_t k = 0; k < (size_t)3 * N; ++k)
+            if (!(R[k] >= 0 && R[k] <= c->L)) return set_error("mdmc_set_state: position %zu = %g outside [0, L]", k, R[k]);
     double* dst[3] = {c->dR, c->dV, c->dA};
     const double* src[3] = {R, V, A};
     for (int q = 0; q < 3; ++q) {

@@ -159,24 +159,213 @@ __global__ __launch_bounds__(MCT) void k_monte_carlo(MCArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// velocity Verlet (MDStep :504-511): stepPositions :452-467 (keeps the old A), and after the
-// new accelerations stepVelocities :469-502 (Verlet update + laser force; the collided particles
-// of the step are then overwritten from the host-drawn list)
+// LDS-resident Metropolis for N <= NPT * 1024 (N = 4096: NPT = 4).  Positions live in LDS
+// (24 N bytes), each thread keeps U[j] and the candidate U'[j] of its NPT particles in
+// registers, a step costs two barriers, and the minimum image is the division-free form
+// d - L s, s = (d >= micT) - (d <= -micT) (= round(d/L) exactly for |d| < 1.25 L; positions
+// stay in [0, L], MCMD:262-271).  The mt19937 state is double-buffered in LDS: the last wave
+// twists the next block of 624 words (three dependency phases, 64 lanes) while the step's
+// energies are summed, so lane 0 never runs the serial twist unless a step draws > 624 words.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_vv_positions(double* __restrict__ R, const double* __restrict__ V,
-                                                      const double* __restrict__ A, double* __restrict__ Aold,
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);     // lgkmcnt(0): the wave's LDS writes have landed
+    __builtin_amdgcn_wave_barrier();
+}
+// Y = twist(X) by one wave (X untouched)
+__device__ void mt_twist_wave(const uint32_t* X, uint32_t* Y, int lane) {
+    for (int k = lane; k < 227; k += 64) Y[k] = mt_mix(X[k], X[k + 1], X[k + 397]);
+    lds_wave_sync();
+    for (int k = 227 + lane; k < 454; k += 64) Y[k] = mt_mix(X[k], X[k + 1], Y[k - 227]);
+    lds_wave_sync();
+    for (int k = 454 + lane; k < 623; k += 64) Y[k] = mt_mix(X[k], X[k + 1], Y[k - 227]);
+    lds_wave_sync();
+    if (lane == 0) Y[623] = mt_mix(X[623], Y[0], Y[396]);
+    lds_wave_sync();
+}
+struct MtLds {
+    uint32_t w[2][624];
+    int p, cur, ahead;      // position in w[cur]; ahead: w[cur ^ 1] == twist(w[cur])
+};
+struct MtPos {
+    int p, cur, ahead;      // thread 0's register copy of the MtLds bookkeeping
+};
+__device__ __forceinline__ double mt_uniform_lds(MtLds& m, MtPos& r) {
+    double r2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (r.p >= 624) {
+            if (r.ahead) { r.cur ^= 1; r.ahead = 0; }
+            else mt_twist(m.w[r.cur]);                        // > 624 words in one step: in place
+            r.p = 0;
+        }
+        uint32_t z = m.w[r.cur][r.p++];
+        z ^= z >> 11;
+        z ^= (z << 7) & 0x9d2c5680u;
+        z ^= (z << 15) & 0xefc60000u;
+        z ^= z >> 18;
+        r2[h] = (double)z;
+    }
+    const double u = (r2[0] + r2[1] * 4294967296.0) / 18446744073709551616.0;
+    return u >= 1.0 ? 0x1.fffffffffffffp-1 : u;
+}
+__device__ __forceinline__ double mic_t(double d, double L, double T) {
+    const double s = (double)(d >= T) - (double)(d <= -T);
+    return d - L * s;
+}
+
+template <int NPT>
+__global__ __launch_bounds__(MCT) void k_monte_carlo_lds(MCArgs a) {
+    extern __shared__ double sR[];                   // [3][N]
+    __shared__ MtLds mt;
+    __shared__ int s_P, s_acc;
+    __shared__ double s_d[3], s_tot, s_UP;
+    __shared__ double s_part[2][MCT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int N = a.N, S = a.S;
+    const double L = a.L, T = a.micT;
+    double* X = sR;
+    double* Y = sR + N;
+    double* Z = sR + 2 * N;
+    for (int k = tid; k < N; k += MCT) { X[k] = a.R[k]; Y[k] = a.R[S + k]; Z[k] = a.R[2 * S + k]; }
+    for (int k = tid; k < 624; k += MCT) mt.w[0][k] = a.mt[k];
+    double U[NPT], Un[NPT];
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+        const int j = tid + q * MCT;
+        U[q] = j < N ? a.U[j] : 0.;
+        Un[q] = U[q];
+    }
+    if (tid == 0) { mt.p = (int)a.mt[624]; mt.cur = 0; mt.ahead = 0; s_acc = 0; }
+    __syncthreads();
+    if (w == MCT / 64 - 1) {
+        mt_twist_wave(mt.w[0], mt.w[1], lane);
+        if (lane == 0) mt.ahead = 1;
+    }
+    __syncthreads();
+    unsigned long long acc = 0;
+    auto draw = [&](MtPos& r) {                                      // MCMD:325-334 (tid 0)
+        int P;
+        double rx, ry, rz;
+        for (;;) {
+            const double randPart = mt_uniform_lds(mt, r);
+            P = (int)floor(randPart * N);
+            rx = a.maxRStep * (2 * mt_uniform_lds(mt, r) - 1);
+            ry = a.maxRStep * (2 * mt_uniform_lds(mt, r) - 1);
+            rz = a.maxRStep * (2 * mt_uniform_lds(mt, r) - 1);
+            if (rx * rx + ry * ry + rz * rz < a.maxRStep * a.maxRStep) break;
+        }
+        s_P = P; s_d[0] = rx; s_d[1] = ry; s_d[2] = rz;
+    };
+    if (tid == 0 && a.nsteps > 0) {
+        MtPos r{mt.p, mt.cur, mt.ahead};
+        draw(r);
+        mt.p = r.p; mt.cur = r.cur; mt.ahead = r.ahead;
+    }
+    __syncthreads();
+    int prevP = -1;
+    double nx = 0., ny = 0., nz = 0.;
+    for (int step = 0; step < a.nsteps; ++step) {
+        // ---- all threads: the previous step's acceptance, then the energy change (:249-313)
+        if (s_acc) {
+            const double tt = s_tot;
+#pragma unroll
+            for (int q = 0; q < NPT; ++q) U[q] = (tid + q * MCT == prevP) ? tt : Un[q];   // U[NPart] = totalU
+        }
+        const int P = s_P;
+        const double ox = X[P], oy = Y[P], oz = Z[P];
+        nx = ox + s_d[0]; ny = oy + s_d[1]; nz = oz + s_d[2];          // :262-271
+        if (nx < 0) nx += L;
+        if (nx > L) nx -= L;
+        if (ny < 0) ny += L;
+        if (ny > L) ny -= L;
+        if (nz < 0) nz += L;
+        if (nz > L) nz -= L;
+        double tot = 0., dsum = 0.;
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) {
+            const int j = tid + q * MCT;
+            Un[q] = U[q];
+            if (j >= N) continue;
+            if (j == P) { s_UP = U[q]; continue; }
+            const double cx = X[j], cy = Y[j], cz = Z[j];
+            const double xn = mic_t(nx - cx, L, T), yn = mic_t(ny - cy, L, T), zn = mic_t(nz - cz, L, T);
+            const double xo = mic_t(ox - cx, L, T), yo = mic_t(oy - cy, L, T), zo = mic_t(oz - cz, L, T);
+            const double dO = sqrt(xo * xo + yo * yo + zo * zo);
+            const double dN = sqrt(xn * xn + yn * yn + zn * zn);
+            const double uN = mc_uij(dN, a.kappa, a.rCut), uO = mc_uij(dO, a.kappa, a.rCut);
+            tot = tot + uN;
+            Un[q] = U[q] + (uN - uO);                                   // U[j] += (UijNew - UijOld)
+            dsum = dsum + (Un[q] - U[q]);
+        }
+        tot = wave_sum(tot);
+        dsum = wave_sum(dsum);
+        if (lane == 0) { s_part[0][w] = tot; s_part[1][w] = dsum; }
+        if (w == MCT / 64 - 1 && !mt.ahead) {                           // twist ahead off the critical path
+            mt_twist_wave(mt.w[mt.cur], mt.w[mt.cur ^ 1], lane);
+            if (lane == 0) mt.ahead = 1;
+        }
+        prevP = P;
+        __syncthreads();
+        // ---- thread 0: accept / reject (:341-381), then the next step's draws
+        if (tid == 0) {
+            MtPos r{mt.p, mt.cur, mt.ahead};
+            double Tt = 0., Dd = 0.;
+            for (int q = 0; q < MCT / 64; ++q) { Tt = Tt + s_part[0][q]; Dd = Dd + s_part[1][q]; }
+            const double dE = Dd + (Tt - s_UP);
+            bool good = dE < 0;
+            if (!good) good = mt_uniform_lds(mt, r) < exp(-(dE / 2) * a.Gamma);
+            s_acc = good;
+            s_tot = Tt;
+            if (good) { X[P] = nx; Y[P] = ny; Z[P] = nz; ++acc; }
+            if (step + 1 < a.nsteps) draw(r);
+            mt.p = r.p; mt.cur = r.cur; mt.ahead = r.ahead;
+        }
+        __syncthreads();
+    }
+    if (s_acc) {
+        const double tt = s_tot;
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) U[q] = (tid + q * MCT == prevP) ? tt : Un[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+        const int j = tid + q * MCT;
+        if (j < N) a.U[j] = U[q];
+    }
+    for (int k = tid; k < N; k += MCT) { a.R[k] = X[k]; a.R[S + k] = Y[k]; a.R[2 * S + k] = Z[k]; }
+    for (int k = tid; k < 624; k += MCT) a.mt[k] = mt.w[mt.cur][k];
+    if (tid == 0) { a.mt[624] = (uint32_t)mt.p; *a.accepted += acc; }
+}
+
+// ------------------------------------------------------------------------------------------
+// velocity Verlet (MDStep :504-511).  k_vv_positions is stepPositions :452-467 (R -> Rn).  After
+// the Newton-3 force kernel, k_vv_step sums the force slots (canonical order) into a(t + dt),
+// runs stepVelocities :469-502 (Verlet update + laser force) and pre-advances the positions of
+// the next MDStep, r + dt v + dt^2/2 a with the box wrap, into Rn: the same expression on the same
+// values stepPositions would read, so a step is two launches.  k_collide then overwrites the
+// collided particles of the step from the host-drawn list (and redoes their Rn).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double step_pos(double r, double v, double a, double dt, double L) {   // :455-464
+    r = r + dt * v + dt * dt / 2 * a;
+    if (r < 0) r += L;
+    if (r > L) r -= L;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_vv_positions(const double* __restrict__ R, const double* __restrict__ V,
+                                                      const double* __restrict__ A, double* __restrict__ Rn,
                                                       int N, int S, double dt, double L) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= N) return;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const size_t k = (size_t)c * S + i;
-        const double a = A[k];
-        Aold[k] = a;
-        double r = R[k] + dt * V[k] + dt * dt / 2 * a;             // :455-457
-        if (r < 0) r += L;                                         // :459-464
-        if (r > L) r -= L;
-        R[k] = r;
+        Rn[k] = step_pos(R[k], V[k], A[k], dt, L);
     }
 }
 
@@ -190,19 +379,35 @@ __device__ __forceinline__ void laser_kick(const VVArgs& a, double* v) {      //
     }
 }
 
-__global__ __launch_bounds__(256) void k_vv_velocities(VVArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.N) return;
-    const int S = a.S;
-    double v[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const size_t k = (size_t)c * S + i;
-        v[c] = a.V[k] + a.dt / 2 * (a.Aold[k] + a.A[k]);           // :484-486
-    }
-    if (a.laser) laser_kick(a, v);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) a.V[(size_t)c * S + i] = v[c];
+__device__ __forceinline__ double laser_term(const VVArgs& a, int c, double v) {   // :488-498, component c
+    if (a.oneAxis) return c == 0 ? v + v * a.dt * 1.234 * a.p6 * a.beta / a.sqrtn : v;
+    if (c == 0) return v + v * a.dt * 1.234 * a.p6 * a.beta / a.sqrtn / 2;
+    return v + v * a.dt * 1.234 * a.p6 * a.beta / a.sqrtn / 4 * (-1);
+}
+
+// workgroup = 64 particles x one component; wave q sums the slots q, q + 8, q + 16, ... of its
+// 64 particles (coalesced rows) = seg_sum's accumulator a[q], and wave 0 combines the eight in
+// seg_sum's tree: bit-identical to seg_sum, with 8x the loads in flight
+__global__ __launch_bounds__(512) void k_vv_step(VVArgs a) {
+    __shared__ double acc[8][64];
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    const int c = blockIdx.y;
+    const size_t k = (size_t)c * a.S + i;
+    const size_t stride = (size_t)3 * a.S;
+    double sq = 0.;
+    if (i < a.N)
+        for (int sl = q; sl < a.nslots; sl += 8) sq += a.slots[(size_t)sl * stride + k];
+    acc[q][lane] = sq;
+    __syncthreads();
+    if (q != 0 || i >= a.N) return;
+    const double an = ((acc[0][lane] + acc[1][lane]) + (acc[2][lane] + acc[3][lane])) +
+                      ((acc[4][lane] + acc[5][lane]) + (acc[6][lane] + acc[7][lane]));
+    double v = a.V[k] + a.dt / 2 * (a.A[k] + an);                    // :484-486 (oldA + A)
+    if (a.laser) v = laser_term(a, c, v);
+    a.V[k] = v;
+    a.A[k] = an;
+    a.Rn[k] = step_pos(a.R[k], v, an, a.dt, a.L);
 }
 
 // the collided particles of the step (:477-482): V = the host-drawn Maxwellian, then the laser term
@@ -214,7 +419,11 @@ __global__ __launch_bounds__(64) void k_collide(VVArgs a) {
     double v[3] = {e[1], e[2], e[3]};
     if (a.laser) laser_kick(a, v);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) a.V[(size_t)c * a.S + i] = v[c];
+    for (int c = 0; c < 3; ++c) {
+        const size_t k = (size_t)c * a.S + i;
+        a.V[k] = v[c];
+        a.Rn[k] = step_pos(a.R[k], v[c], a.A[k], a.dt, a.L);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -385,20 +594,39 @@ hipError_t launch_particle_potentials(const double* R, int N, int S, double L, d
     hipLaunchKernelGGL(k_particle_potentials, dim3((N + 255) / 256), dim3(256), 0, s, R, N, S, L, kappa, rCut, U);
     return hipGetLastError();
 }
+template <int NPT>
+static hipError_t launch_mc_lds(const MCArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)3 * a.N * sizeof(double);
+    hipError_t e = hipFuncSetAttribute((const void*)k_monte_carlo_lds<NPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_monte_carlo_lds<NPT>, dim3(1), dim3(MCT), lds, s, a);
+    return hipGetLastError();
+}
 hipError_t launch_monte_carlo(const MCArgs& a, hipStream_t s) {
     if (a.nsteps <= 0) return hipSuccess;
+    const int npt = (a.N + MCT - 1) / MCT;
+    switch (npt) {                                       // positions in LDS up to N = 6144 (144 KB)
+        case 1: return launch_mc_lds<1>(a, s);
+        case 2: return launch_mc_lds<2>(a, s);
+        case 3: return launch_mc_lds<3>(a, s);
+        case 4: return launch_mc_lds<4>(a, s);
+        case 5: return launch_mc_lds<5>(a, s);
+        case 6: return launch_mc_lds<6>(a, s);
+        default: break;
+    }
     hipLaunchKernelGGL(k_monte_carlo, dim3(1), dim3(MCT), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_vv_positions(double* R, const double* V, const double* A, double* Aold, int N, int S, double dt,
+hipError_t launch_vv_positions(const double* R, const double* V, const double* A, double* Rn, int N, int S, double dt,
                                double L, hipStream_t s) {
     if (N <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_vv_positions, dim3((N + 255) / 256), dim3(256), 0, s, R, V, A, Aold, N, S, dt, L);
+    hipLaunchKernelGGL(k_vv_positions, dim3((N + 255) / 256), dim3(256), 0, s, R, V, A, Rn, N, S, dt, L);
     return hipGetLastError();
 }
 hipError_t launch_vv_velocities(const VVArgs& a, hipStream_t s) {
     if (a.N <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_vv_velocities, dim3((a.N + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_vv_step, dim3((a.N + 63) / 64, 3), dim3(512), 0, s, a);
     if (a.nhits > 0) hipLaunchKernelGGL(k_collide, dim3((a.nhits + 63) / 64), dim3(64), 0, s, a);
     return hipGetLastError();
 }

@@ -184,11 +184,16 @@ struct MCArgs {
     unsigned long long* accepted;   // in/out
     int N, S, nsteps;
     double L, kappa, rCut, maxRStep, Gamma;
+    double micT;        // smallest d with fl(d / L) >= 0.5: round(d/L) without a division, |d| < 1.25 L
 };
 struct VVArgs {
     double* V;
-    const double* A;
-    const double* Aold;
+    double* A;          // in: a(t) ; out: a(t + dt) = the canonical sum of the force slots
+    const double* slots;   // [nslots][3][S] Newton-3 tile partials of a(t + dt)
+    int nslots;
+    const double* R;    // r(t + dt)
+    double* Rn;         // out: r(t + 2 dt) = stepPositions of the next MDStep (pre-advanced)
+    double L;
     const double* hits;        // [nhits][4] = (i, vx, vy, vz): this step's collisions (host-drawn)
     int nhits;
     int N, S, laser, oneAxis;
@@ -197,7 +202,7 @@ struct VVArgs {
 hipError_t launch_particle_potentials(const double* R, int N, int S, double L, double kappa, double rCut, double* U,
                                       hipStream_t s);
 hipError_t launch_monte_carlo(const MCArgs& a, hipStream_t s);
-hipError_t launch_vv_positions(double* R, const double* V, const double* A, double* Aold, int N, int S, double dt,
+hipError_t launch_vv_positions(const double* R, const double* V, const double* A, double* Rn, int N, int S, double dt,
                                double L, hipStream_t s);
 hipError_t launch_vv_velocities(const VVArgs& a, hipStream_t s);   // + the collision scatter when nhits > 0
 hipError_t launch_pair_hist(const double* R, int N, int S, double L, double step, int nbins, unsigned* hist,

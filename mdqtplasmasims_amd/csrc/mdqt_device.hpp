@@ -118,12 +118,8 @@ __device__ __forceinline__ cxd renorm_div(cxd w, double sumsq) {
 #ifndef MDQT_FAST_SINCOS
 #define MDQT_FAST_SINCOS 1
 #endif
-template <bool F>
-__device__ __forceinline__ void sincos_q(double x, double& sn, double& cs) {
-    if (!F || !MDQT_FAST_SINCOS || !(fabs(x) < 1048576.)) {
-        sincos(x, &sn, &cs);
-        return;
-    }
+// the reduction + kernels without the range check (valid for |x| < 2^20), branch-free
+__device__ __forceinline__ void sincos_fast(double x, double& sn, double& cs) {
     const double n = rint(x * 0.63661977236758134308);           // 2/pi
     double r = fma(-n, 1.57079632679489655800e+00, x);            // pi/2 = P1 + P2 + P3
     r = fma(-n, 6.12323399573676603587e-17, r);
@@ -143,6 +139,14 @@ __device__ __forceinline__ void sincos_q(double x, double& sn, double& cs) {
     const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
     sn = (q & 2) ? -s0 : s0;
     cs = ((q + 1) & 2) ? -c0 : c0;
+}
+template <bool F>
+__device__ __forceinline__ void sincos_q(double x, double& sn, double& cs) {
+    if (!F || !MDQT_FAST_SINCOS || !(fabs(x) < 1048576.)) {
+        sincos(x, &sn, &cs);
+        return;
+    }
+    sincos_fast(x, sn, cs);
 }
 
 __device__ __forceinline__ double rho_im(cxd a, cxd b) {   // Im(a * conj(b)), SpeedUp:490-502
@@ -182,6 +186,9 @@ __device__ __forceinline__ double dpp(double v) {
 #define SHL(n) (0x100 + (n))
 #define SHR(n) (0x110 + (n))
 #define BCAST(n) (0x150 + (n))
+#define ROR(n) (0x120 + (n))
+#define QP_XOR1 0xB1   // quad_perm [1, 0, 3, 2]: lane ^ 1
+#define QP_XOR2 0x4E   // quad_perm [2, 3, 0, 1]: lane ^ 2
 
 // ((T2 + T3) + T4) + T5 of the ion's lanes 2..5, in every lane of the row
 __device__ __forceinline__ double row_sum_p(double T) {

@@ -89,8 +89,9 @@ struct mdqt_ctx {
     int kdeChunks = 0;
     LaneTab tab;                   // lane-per-state QT kernel tables (host copy)
     LaneTab* dTab = nullptr;       // device copy (uploaded once at create)
-    FastTab ftab;                  // qt_math 2 row tables (host copy)
-    FastTab* dFTab = nullptr;      // device copy
+    FastTab ftab;                  // qt_math 2 row tables by state (host copy)
+    FastTab ftabL;                 // the same by lane of the lane-per-state kernel (model 0: kStateOfLane0)
+    FastTab* dFTab = nullptr;      // device copies [2]: by state, by lane
     int substep_mode = 0;          // 0 auto, 1 thread-per-ion, 2 lane-per-state
     int force_variant = 1;         // 0 exact reference operations, 1 fast reciprocal form
     int qt_math = 2;               // 0 exact reference operations, 1 FMA-contracted, 2 reassociated (option "qt_math")
@@ -367,7 +368,7 @@ static void build_constants(mdqt_ctx* s) {
     for (int k = 0; k < NS; ++k) {
         for (int j = 0; j < 3; ++j) {
             const int c = kFastCol[k][j];
-            if (c == k) continue;                  // unused slot
+            if (c == k || c >= NS) continue;       // unused slot
             const int e = static_idx(k, c);
             if (e >= 0) { f.cre[j][k] = q.Mre[e]; f.cim[j][k] = q.Mim[e]; }
         }
@@ -403,6 +404,24 @@ static void build_constants(mdqt_ctx* s) {
     if (p->qt_model != 0) build_pump_tables(p, q, f);
     f.dt2 = (0.5 * q.dtQ) * (0.5 * q.dtQ);
     for (int k = 0; k < 4; ++k) q.hdPh[k] = f.hdp[2 + k];
+    // the lane-indexed copy: model 0 moves state kStateOfLane0[l] to lane l (its slots are DPP
+    // moves, col unused: self); the pumping models keep lane = state
+    FastTab& fl = s->ftabL;
+    fl = f;
+    if (p->qt_model == 0) {
+        memset(&fl, 0, sizeof fl);
+        fl.cphi = f.cphi; fl.dt2 = f.dt2;
+        for (int l = 0; l < 16; ++l) {
+            for (int j = 0; j < 3; ++j) fl.col[j][l] = l;
+            const int k = state_of_lane0(l);
+            if (k >= NS) continue;
+            for (int j = 0; j < 3; ++j) {
+                fl.cre[j][l] = f.cre[j][k]; fl.cim[j][l] = f.cim[j][k]; fl.kw[j][l] = f.kw[j][k];
+            }
+            fl.dms[l] = f.dms[k]; fl.dmc[l] = f.dmc[k]; fl.mre[l] = f.mre[k];
+            fl.mi0[l] = f.mi0[k]; fl.mi1[l] = f.mi1[k]; fl.hdp[l] = f.hdp[k];
+        }
+    }
 }
 
 static double expDetuning_of(const mdqt_params* p, double t) {   // :447
@@ -591,7 +610,7 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
         return fail("cannot create HIP stream on device %d", p->device);
     }
     s->stream = s->own;
-    if (hipMalloc(&s->dTab, sizeof(LaneTab)) != hipSuccess || hipMalloc(&s->dFTab, sizeof(FastTab)) != hipSuccess) {
+    if (hipMalloc(&s->dTab, sizeof(LaneTab)) != hipSuccess || hipMalloc(&s->dFTab, 2 * sizeof(FastTab)) != hipSuccess) {
         mdqt_destroy(s);
         return fail("hipMalloc lane tables");
     }
@@ -620,7 +639,8 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
         }
     }
     if (hipMemcpy(s->dTab, &s->tab, sizeof(LaneTab), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(s->dFTab, &s->ftab, sizeof(FastTab), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(s->dFTab, &s->ftab, sizeof(FastTab), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s->dFTab + 1, &s->ftabL, sizeof(FastTab), hipMemcpyHostToDevice) != hipSuccess) {
         mdqt_destroy(s);
         return fail("upload of the lane table failed");
     }

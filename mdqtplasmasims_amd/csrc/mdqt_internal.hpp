@@ -59,9 +59,18 @@ struct LaneTab {
 
 // qt_math 2 (reassociated QT arithmetic, mdqt_qtfast.hip): row k of M = I - i h H as its
 // diagonal plus three off-diagonal slots with source states kFastCol[k][t] (unused slots point
-// at k itself with a zero coefficient; the time-dependent entry of rows 4, 5, 8, 9 sits in slot
-// 2).  Both QT kernels evaluate every row as the same fixed FMA chain over these slots, so the
-// thread-per-ion and lane-per-state forms stay bit-identical.
+// at k itself, or for model 0 at the zero state NS, with a zero coefficient; the time-dependent
+// entry of rows 4, 5, 8, 9 sits in slot 2).  Both QT kernels evaluate every row as the same fixed
+// FMA chain over these slots, so the thread-per-ion and lane-per-state forms stay bit-identical.
+//
+// Model 0's lane layout (lane-per-state kernel): the coupling graph (S-P and P-D edges, every P
+// level of degree 3) is bipartite and splits into three matchings; states are placed on the 16
+// lanes of an ion's row so that the matchings are lane ^ 2, lane + 8 (mod 16) and lane ^ 1 —
+// three DPP moves (quad_perm, row_ror:8, quad_perm) instead of an LDS gather:
+//   lane : 0  1  2  3  4  5  6  7  8  9  10 11 12 13 14 15
+//   state: 2  1  9  4  3  0  8  5  11 -  -  7  10 -  -  6     (- : zero lanes; 9 = y, 10 = z)
+// Slot 0 = lane ^ 2, slot 1 = lane + 8, slot 2 = lane ^ 1 (it carries the time-dependent
+// couplings 4-9 and 5-8).  The sums over lanes (dp, kick, norm) follow lane order.
 //
 // QT models (mdqt_params.qt_model): 0 = the SpeedUp Sr+ 12-level laser cooling (default);
 // the optical-pumping ("spin tagging") variants, one per reference program family:
@@ -74,8 +83,8 @@ struct LaneTab {
 constexpr int NMODELS = 4;
 constexpr int kModelStates[NMODELS] = {12, 7, 7, 5};
 constexpr int kFastColM[NMODELS][NS][3] = {
-    {{3, 5, 0}, {2, 4, 1}, {1, 9, 11}, {0, 8, 10}, {1, 7, 9}, {0, 6, 8},
-     {5, 6, 6}, {4, 7, 7}, {3, 8, 5}, {2, 9, 4}, {3, 10, 10}, {2, 11, 11}},
+    {{5, 12, 3}, {4, 12, 2}, {9, 11, 1}, {8, 10, 0}, {1, 7, 9}, {0, 6, 8},
+     {12, 5, 12}, {12, 4, 12}, {3, 12, 5}, {2, 12, 4}, {12, 3, 12}, {12, 2, 12}},
     {{2, 4, 0}, {3, 5, 1}, {0, 2, 2}, {1, 3, 3}, {0, 4, 4}, {1, 5, 5},
      {6, 6, 6}, {7, 7, 7}, {8, 8, 8}, {9, 9, 9}, {10, 10, 10}, {11, 11, 11}},
     {{4, 0, 0}, {5, 1, 1}, {2, 2, 2}, {3, 3, 3}, {0, 4, 4}, {1, 5, 5},
@@ -83,6 +92,24 @@ constexpr int kFastColM[NMODELS][NS][3] = {
     {{3, 0, 0}, {2, 1, 1}, {1, 2, 2}, {0, 3, 3}, {4, 4, 4}, {5, 5, 5},
      {6, 6, 6}, {7, 7, 7}, {8, 8, 8}, {9, 9, 9}, {10, 10, 10}, {11, 11, 11}}};
 inline constexpr const int (&kFastCol)[NS][3] = kFastColM[0];
+// model 0 lane layout (see above): state of lane l / lane of state k, as 4-bit fields (0xF: none)
+constexpr uint64_t kStateOfLane0 = 0x6FFA7FFB58034912ull;   // lanes 15..0: 6 F F A 7 F F B 5 8 0 3 4 9 1 2
+constexpr uint64_t kLaneOfState0 = 0x8C26BF734015ull;      // states 11..0: 8 C 2 6 B F 7 3 4 0 1 5
+__host__ __device__ constexpr int state_of_lane0(int l) { return (int)((kStateOfLane0 >> (4 * l)) & 0xF); }
+__host__ __device__ constexpr int lane_of_state0(int k) { return (int)((kLaneOfState0 >> (4 * k)) & 0xF); }
+constexpr bool layout0_consistent() {      // slot j of state k's lane reads the lane of kFastColM[0][k][j]
+    for (int k = 0; k < NS; ++k) {
+        const int l = lane_of_state0(k);
+        if (state_of_lane0(l) != k) return false;
+        const int part[3] = {l ^ 2, (l + 8) & 15, l ^ 1};
+        for (int j = 0; j < 3; ++j) {
+            const int ps = state_of_lane0(part[j]);
+            if ((ps >= NS ? NS : ps) != kFastColM[0][k][j]) return false;
+        }
+    }
+    return true;
+}
+static_assert(layout0_consistent(), "model 0 lane layout and kFastColM[0] disagree");
 struct FastTab {
     int col[3][16];              // kFastCol, lanes 12..15 point at themselves
     double cre[3][16], cim[3][16];   // static M entries of the slots (0 for unused / dynamic)
@@ -244,7 +271,7 @@ constexpr int kLaneKernelMaxIons = 98304;
 // fast: qt_math 1 (FMA contraction, refined rsq) instead of the reference's exact operations
 hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s);
 // qt_math 2: the reassociated kernels of mdqt_qtfast.hip (same modes as launch_substeps)
-hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s);
+hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s);   // tab[0] by state, tab[1] by lane
 // measureSpinUps (randomFrozenStartTag408Linear.cpp:600, :422Linear) / tagParticles
 // (MonteCarloFollowedByQTTagging408Linear.cpp:1022): tag[i] = 1 with probability of spin up
 hipError_t launch_tag_spin_up(const double* psi, int n, int S, uint64_t gid0, uint64_t q, const QTConst& qc,

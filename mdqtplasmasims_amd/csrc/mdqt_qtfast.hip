@@ -127,6 +127,24 @@ __device__ __forceinline__ double sq(cxd y) { return y.re * y.re + y.im * y.im; 
 // ------------------------------------------------------------------------------------------
 // thread per ion
 // ------------------------------------------------------------------------------------------
+// the P-level sum dp and the 16-lane trees in the lane kernel's order: model 0 places its states
+// on lanes by kStateOfLane0 (see mdqt_internal.hpp), the other models on lane = state
+template <int MODEL>
+__device__ __forceinline__ double sum_p(const double* Tp) {     // Tp[q] of P state 2 + q
+    if constexpr (MODEL == 0) return (Tp[0] + Tp[2]) + (Tp[1] + Tp[3]);   // lanes 0 | 3 and 4 | 7
+    return (Tp[0] + Tp[1]) + (Tp[2] + Tp[3]);
+}
+template <int MODEL>
+__device__ __forceinline__ double tree_lanes(const double* vs) {   // vs by state
+    double v[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+        const int st = MODEL == 0 ? state_of_lane0(l) : l;
+        v[l] = st < NS ? vs[st] : 0.;
+    }
+    return tree16(v);
+}
+
 template <int MODEL>
 __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab* __restrict__ tab) {
     constexpr const int(&COL)[NS][3] = kFastColM[MODEL];
@@ -148,7 +166,8 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
         }
     }
     double tPart = a.tPart[i];
-    cxd w[NS];
+    cxd w[NS + 1];                          // w[NS]: the zero state of model 0's unused slots
+    w[NS] = {0., 0.};
     if (a.do_qt) {
 #pragma unroll
         for (int k = 0; k < NS; ++k) w[k] = {a.psi[(size_t)(2 * k) * S + i], a.psi[(size_t)(2 * k + 1) * S + i]};
@@ -171,19 +190,17 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
         double Tp[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) Tp[q] = nrm2(w[2 + q]) * T.hdp[2 + q];
-        const double dp = (Tp[0] + Tp[1]) + (Tp[2] + Tp[3]);
+        const double dp = sum_p<MODEL>(Tp);
         double u1, u2;
         draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 0, u1, u2);
         double kick;
         if (u1 > dp) {
-            double kv[16];
+            double kv[NS];
 #pragma unroll
             for (int k = 0; k < NS; ++k)
                 kv[k] = kick_term(w[k], w[COL[k][0]], w[COL[k][1]], w[COL[k][2]], T.kw[0][k],
                                   T.kw[1][k], T.kw[2][k]);
-#pragma unroll
-            for (int k = NS; k < 16; ++k) kv[k] = 0.;
-            kick = tree16(kv);
+            kick = tree_lanes<MODEL>(kv);
             const double phi = (u * T.cphi) * tPart;
             double sn, cs;
             sincos_q<true>(phi, sn, cs);
@@ -193,16 +210,16 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
                 md[k] = {T.mre[k], fma(T.mi1[k], u, T.mi0[k])};
                 c2[k] = {fma(T.dms[k], sn, T.cre[2][k]), fma(T.dmc[k], cs, T.cim[2][k])};
             }
-            cxd y[NS], acc[NS];
+            cxd y[NS + 1], acc[NS];
 #pragma unroll
-            for (int k = 0; k < NS; ++k) y[k] = w[k];
+            for (int k = 0; k <= NS; ++k) y[k] = w[k];
 #pragma unroll
             for (int stg = 0; stg < 4; ++stg) {
                 double dpy = dp;
                 if (stg > 0) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) Tp[q] = nrm2(y[2 + q]) * T.hdp[2 + q];
-                    dpy = (Tp[0] + Tp[1]) + (Tp[2] + Tp[3]);
+                    dpy = sum_p<MODEL>(Tp);
                 }
                 const double pref = rsq_nr(1. - dpy);
                 cxd ws[NS];
@@ -236,12 +253,10 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
             for (int k = 0; k < NS; ++k) w[k] = {k == target ? 1. : 0., 0.};
         }
         if (qc.renorm) {                                                    // :706-712
-            double nv[16];
+            double nv[NS];
 #pragma unroll
             for (int k = 0; k < NS; ++k) nv[k] = nrm2(w[k]);
-#pragma unroll
-            for (int k = NS; k < 16; ++k) nv[k] = 0.;
-            const double r = rsq_nr(tree16(nv));
+            const double r = rsq_nr(tree_lanes<MODEL>(nv));
 #pragma unroll
             for (int k = 0; k < NS; ++k) w[k] = {w[k].re * r, w[k].im * r};
         }
@@ -265,10 +280,19 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
 }
 
 // ------------------------------------------------------------------------------------------
-// lane per state: one ion per 16-lane group (4 per wave64), lane k = state k.  The integrator
-// coordinate of a lane is x for lanes 0..11, 14, 15 (so every state lane has vx locally), y for
-// lane 12 and z for lane 13.  Lanes 12..15 carry zero amplitudes and zero coefficients.
+// lane per state: one ion per 16-lane group (4 per wave64).  DPPX (model 0): states on lanes by
+// kStateOfLane0 and the three coupling slots gathered with DPP moves (lane ^ 2, lane + 8,
+// lane ^ 1); lanes 9 / 10 hold the y / z coordinate, every other lane x.  Otherwise (the pumping
+// models): lane k = state k, slots gathered through LDS, lanes 12 / 13 hold y / z.  Lanes
+// without a state carry zero amplitudes and zero coefficients.  `tab` is indexed by lane.
 // ------------------------------------------------------------------------------------------
+// dp of model 0's layout: (T_lane0 + T_lane3) + (T_lane4 + T_lane7) = (T2 + T4) + (T3 + T5), in
+// every lane — four independent 64-bit broadcasts, then a two-level tree
+__device__ __forceinline__ double lane_sum_p8(double T) {
+    return (dpp<BCAST(0)>(T) + dpp<BCAST(3)>(T)) + (dpp<BCAST(4)>(T) + dpp<BCAST(7)>(T));
+}
+
+template <bool DPPX>
 __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
     const int k = threadIdx.x & 15;
     const int grp = threadIdx.x >> 4;
@@ -277,8 +301,10 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
     const int i = store ? iraw : a.n - 1;             // idle groups shadow the last ion
     const QTConst& qc = a.qc;
     const int S = a.S;
-    const int c = (k == 12) ? 1 : (k == 13) ? 2 : 0;
-    const bool owner = (k == 0) || (k == 12) || (k == 13);   // stores coordinate c
+    const int st = DPPX ? state_of_lane0(k) : k;      // >= NS: no state on this lane
+    const int cy = DPPX ? 9 : 12, cz = DPPX ? 10 : 13;
+    const int c = (k == cy) ? 1 : (k == cz) ? 2 : 0;
+    const bool owner = (k == 0) || (k == cy) || (k == cz);   // stores coordinate c
     const int base = threadIdx.x & ~15;
     const int l0 = base + tab->col[0][k], l1 = base + tab->col[1][k], l2 = base + tab->col[2][k];
     const cxd c0 = {tab->cre[0][k], tab->cim[0][k]}, c1 = {tab->cre[1][k], tab->cim[1][k]};
@@ -296,7 +322,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
     }
     double tPart = a.tPart[i];
     cxd w = {0., 0.};
-    if (a.do_qt && k < NS) w = {a.psi[(size_t)(2 * k) * S + i], a.psi[(size_t)(2 * k + 1) * S + i]};
+    if (a.do_qt && st < NS) w = {a.psi[(size_t)(2 * st) * S + i], a.psi[(size_t)(2 * st + 1) * S + i]};
     const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
     const uint64_t gid = a.gid0 + (uint64_t)i;
     // u1, u2 of every substep of the launch staged in LDS: Philox draws computed lane-parallel
@@ -315,72 +341,114 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
         }
     }
     __syncthreads();
-    __shared__ double2 xg[256];
+    __shared__ double2 xg[DPPX ? 1 : 256];
     auto exchange = [&](cxd y, cxd& y0, cxd& y1, cxd& y2) {
+        if constexpr (DPPX) {
+            y0 = {dpp<QP_XOR2>(y.re), dpp<QP_XOR2>(y.im)};
+            y1 = {dpp<ROR(8)>(y.re), dpp<ROR(8)>(y.im)};
+            y2 = {dpp<QP_XOR1>(y.re), dpp<QP_XOR1>(y.im)};
+            return;
+        }
         wave_sync();
         xg[threadIdx.x] = make_double2(y.re, y.im);
         wave_sync();
         const double2 t0 = xg[l0], t1 = xg[l1], t2 = xg[l2];
         y0 = {t0.x, t0.y}; y1 = {t1.x, t1.y}; y2 = {t2.x, t2.y};
     };
-    for (int s = 0; s < a.nsub; ++s) {
-        if (a.do_step) {
-            const bool moving = a.t[s] > 0;
-            p = half_drift(p, v, f, moving, DT, DT2, L);
-            v = v + dt * f;                           // step_V(dt) :398-409
-            p = half_drift(p, v, f, moving, DT, DT2, L);
-        }
-        if (!a.do_qt) continue;
-        const double u = v * qc.pv2q + a.expDet[s];        // vx on every state lane
-        tPart += qc.dtQ;
-        const double dp = lane_sum_p(nrm2(w) * hdp);
-        const double u1 = su[grp][s][0], u2 = su[grp][s][1];
-        cxd w0, w1, w2;
-        exchange(w, w0, w1, w2);
-        double kick;
-        if (u1 > dp) {
-            kick = lane_tree16(kick_term(w, w0, w1, w2, kw0, kw1, kw2));
-            const double phi = (u * cphi) * tPart;
-            double sn, cs;
-            sincos_q<true>(phi, sn, cs);
-            const cxd md = {mre, fma(mi1, u, mi0)};
-            const cxd c2 = {fma(dms, sn, c2re), fma(dmc, cs, c2im)};
-            cxd y = w, acc = {0., 0.};
-            cxd y0 = w0, y1 = w1, y2 = w2;
+    auto drift = [&](double& pp, double& vv, int sub) {   // step(): step_R, step_V, step_R (:418-430)
+        const bool moving = a.t[sub] > 0;
+        pp = half_drift(pp, vv, f, moving, DT, DT2, L);
+        vv = vv + dt * f;                             // step_V(dt) :398-409
+        pp = half_drift(pp, vv, f, moving, DT, DT2, L);
+    };
+    if (!a.do_qt) {
+        if (a.do_step)
+            for (int s = 0; s < a.nsub; ++s) drift(p, v, s);
+    } else {
+        // Software-pipelined substeps: once substep s has its kick, the drift of substep s + 1
+        // and the sin / cos of its coupling phase (:508) depend on nothing else of substep s, so
+        // they are evaluated before s's Runge-Kutta stages and overlap them.  Same operations on
+        // the same values as the plain order: bit-identical.
+        if (a.do_step) drift(p, v, 0);
+        double sn, cs;
+        sincos_q<true>(((v * qc.pv2q + a.expDet[0]) * cphi) * (tPart + qc.dtQ), sn, cs);
+        for (int s = 0; s < a.nsub; ++s) {
+            const double u = v * qc.pv2q + a.expDet[s];    // vx on every state lane
+            tPart += qc.dtQ;
+            const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp) : lane_sum_p(nrm2(w) * hdp);
+            const double u1 = su[grp][s][0], u2 = su[grp][s][1];
+            cxd w0, w1, w2;
+            exchange(w, w0, w1, w2);
+            double kick;
+            const bool nojump = u1 > dp;
+            // substep s + 1's drift and phase, placed in the same basic block as the work they
+            // overlap (straight-line: the last substep computes a harmless extra value, the
+            // |phi| >= 2^20 library fallback is applied afterwards)
+            double vn, pn, phin, snn, csn;
+            auto next_phase = [&]() {
+                vn = fma(kmask, kick, v);             // :705 (x lanes)
+                pn = p;
+                const int s1 = s + 1 < a.nsub ? s + 1 : s;
+                double pd = pn, vd = vn;
+                drift(pd, vd, s1);
+                const bool adv = a.do_step && s + 1 < a.nsub;   // no drift after the last substep
+                pn = adv ? pd : pn;
+                vn = adv ? vd : vn;
+                phin = ((vn * qc.pv2q + a.expDet[s1]) * cphi) * (tPart + qc.dtQ);
+                sincos_fast(phin, snn, csn);
+            };
+            if (nojump) {
+                kick = lane_tree16(kick_term(w, w0, w1, w2, kw0, kw1, kw2));
+                next_phase();
+                const cxd md = {mre, fma(mi1, u, mi0)};
+                const cxd c2 = {fma(dms, sn, c2re), fma(dmc, cs, c2im)};
+                cxd y = w, acc = {0., 0.};
+                cxd y0 = w0, y1 = w1, y2 = w2;
 #pragma unroll
-            for (int stg = 0; stg < 4; ++stg) {
-                double dpy = dp;
-                if (stg > 0) {
-                    dpy = lane_sum_p(nrm2(y) * hdp);
-                    exchange(y, y0, y1, y2);
+                for (int stg = 0; stg < 4; ++stg) {
+                    double dpy = dp;
+                    if (stg > 0) {
+                        dpy = DPPX ? lane_sum_p8(nrm2(y) * hdp) : lane_sum_p(nrm2(y) * hdp);
+                        exchange(y, y0, y1, y2);
+                    }
+                    const double pref = rsq_nr(1. - dpy);
+                    const cxd ws = row_r(md, y, c0, y0, c1, y1, c2, y2);
+                    const cxd d = {fma(pref, ws.re, -y.re), fma(pref, ws.im, -y.im)};
+                    if (stg == 0) acc = d;
+                    else if (stg < 3) acc = {fma(3., d.re, acc.re), fma(3., d.im, acc.im)};
+                    else acc = {acc.re + d.re, acc.im + d.im};
+                    if (stg < 2) y = {fma(0.5, d.re, w.re), fma(0.5, d.im, w.im)};
+                    else if (stg == 2) y = {w.re + d.re, w.im + d.im};
                 }
-                const double pref = rsq_nr(1. - dpy);
-                const cxd ws = row_r(md, y, c0, y0, c1, y1, c2, y2);
-                const cxd d = {fma(pref, ws.re, -y.re), fma(pref, ws.im, -y.im)};
-                if (stg == 0) acc = d;
-                else if (stg < 3) acc = {fma(3., d.re, acc.re), fma(3., d.im, acc.im)};
-                else acc = {acc.re + d.re, acc.im + d.im};
-                if (stg < 2) y = {fma(0.5, d.re, w.re), fma(0.5, d.im, w.im)};
-                else if (stg == 2) y = {w.re + d.re, w.im + d.im};
+                w = {fma(0.125, acc.re, w.re), fma(0.125, acc.im, w.im)};
+            } else {                                  // quantum jump (:573-703)
+                tPart = 0;
+                const double nk = sq(w);
+                double n3, n4, n5, n6;                    // |w|^2 of the P states 2..5
+                if constexpr (DPPX) {
+                    n3 = dpp<BCAST(0)>(nk); n4 = dpp<BCAST(4)>(nk); n5 = dpp<BCAST(3)>(nk); n6 = dpp<BCAST(7)>(nk);
+                } else {
+                    n3 = dpp<BCAST(2)>(nk); n4 = dpp<BCAST(3)>(nk); n5 = dpp<BCAST(4)>(nk); n6 = dpp<BCAST(5)>(nk);
+                }
+                double randDOrS, randDir, rand3, dummy;
+                draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
+                draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
+                (void)dummy;
+                const int target = qc.model == 0 ? jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick)
+                                                 : jump_target_pump(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
+                w = {st == target ? 1. : 0., 0.};
+                next_phase();
             }
-            w = {fma(0.125, acc.re, w.re), fma(0.125, acc.im, w.im)};
-        } else {                                      // quantum jump (:573-703)
-            tPart = 0;
-            const double nk = sq(w);
-            const double n3 = dpp<BCAST(2)>(nk), n4 = dpp<BCAST(3)>(nk), n5 = dpp<BCAST(4)>(nk), n6 = dpp<BCAST(5)>(nk);
-            double randDOrS, randDir, rand3, dummy;
-            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
-            draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
-            (void)dummy;
-            const int target = qc.model == 0 ? jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick)
-                                             : jump_target_pump(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
-            w = {k == target ? 1. : 0., 0.};
+            if (!(fabs(phin) < 1048576.)) sincos(phin, &snn, &csn);
+            if (qc.renorm) w = [&] {                      // :706-712
+                const double r = rsq_nr(lane_tree16(nrm2(w)));
+                return cxd{w.re * r, w.im * r};
+            }();
+            v = vn;
+            p = pn;
+            sn = snn;
+            cs = csn;
         }
-        if (qc.renorm) w = [&] {                      // :706-712
-            const double r = rsq_nr(lane_tree16(nrm2(w)));
-            return cxd{w.re * r, w.im * r};
-        }();
-        v = fma(kmask, kick, v);                      // :705 (x lanes)
     }
     if (store) {
         if (owner) {
@@ -390,9 +458,9 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
         }
         if (a.do_qt) {
             if (k == 0) a.tPart[i] = tPart;
-            if (k < NS) {
-                a.psi[(size_t)(2 * k) * S + i] = w.re;
-                a.psi[(size_t)(2 * k + 1) * S + i] = w.im;
+            if (st < NS) {
+                a.psi[(size_t)(2 * st) * S + i] = w.re;
+                a.psi[(size_t)(2 * st + 1) * S + i] = w.im;
             }
         }
     }
@@ -404,7 +472,10 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
     if (a.qc.model < 0 || a.qc.model >= NMODELS) return hipErrorInvalidValue;
     const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256);
-    if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes_r, gl, dim3(256), 0, s, a, tab);
+    if (mode == 2) {
+        if (a.qc.model == 0) hipLaunchKernelGGL(k_substeps_lanes_r<true>, gl, dim3(256), 0, s, a, tab + 1);
+        else hipLaunchKernelGGL(k_substeps_lanes_r<false>, gl, dim3(256), 0, s, a, tab + 1);
+    }
     else if (a.qc.model == 0) hipLaunchKernelGGL(k_substeps_r<0>, gt, dim3(256), 0, s, a, tab);
     else if (a.qc.model == 1) hipLaunchKernelGGL(k_substeps_r<1>, gt, dim3(256), 0, s, a, tab);
     else if (a.qc.model == 2) hipLaunchKernelGGL(k_substeps_r<2>, gt, dim3(256), 0, s, a, tab);

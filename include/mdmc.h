@@ -49,7 +49,8 @@ typedef struct mdmc_params {
     uint32_t seed;                /* mt19937 seed (reference: std::random_device, :52-53)       */
     uint32_t job;                 /* argv[1] (:1035)                                             */
     int device;                   /* HIP device ordinal (-1 = current)                           */
-    int force_kernel;             /* 1 = fast reciprocal pair form (default), 0 = reference ops  */
+    int force_kernel;             /* 1 (default): reciprocal pair forms (MD forces, MC energies;
+                                   * a few ulp per pair), 0: the reference's operations          */
     char saveDirectory[256];      /* :62 */
 } mdmc_params;
 

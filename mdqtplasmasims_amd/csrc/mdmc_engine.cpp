@@ -107,6 +107,13 @@ int fail_free(mdmc_ctx* c, const char* what) {
     return set_error("%s", what);
 }
 
+double sqrt_threshold(double rc) {   // smallest x with sqrt(x) >= rc: sqrt(r2) < rc iff r2 < x
+    double x = rc * rc;
+    while (x > 0 && sqrt(x) >= rc) x = nextafter(x, 0.);
+    while (sqrt(x) < rc) x = nextafter(x, INFINITY);
+    return x;
+}
+
 double mic_threshold(double L) {   // smallest d with fl(d / L) >= 0.5 (Newton-3 kernel, exact variant)
     double d = 0.5 * L;
     while (d > 0 && d / L >= 0.5) d = nextafter(d, 0.);
@@ -136,7 +143,9 @@ int accelerations(mdmc_ctx* c) {
     a.N = c->N; a.S = c->S; a.ntiles = c->nt; a.npairs = c->npairs;
     a.L = c->L; a.lDeb = 1. / c->p.kappa; a.Rcut = c->rCut; a.invlDeb = c->p.kappa;
     a.micT = mic_threshold(c->L); a.micGuard = 1.25 * c->L; a.guard = 0;
-    HIPCHK(launch_forces_n3(a, c->p.force_kernel, c->st));
+    a.rc2 = sqrt_threshold(c->rCut);
+    // force_kernel 1: variant 2 (fast values, the reference's exact pair set), 0: exact
+    HIPCHK(launch_forces_n3(a, c->p.force_kernel == 1 ? 2 : 0, c->st));
     return 0;
 }
 
@@ -303,6 +312,8 @@ extern "C" int mdmc_monte_carlo(mdmc_ctx* c, int nsteps, long long* accepted) {
     a.N = c->N; a.S = c->S;
     a.L = c->L; a.kappa = c->p.kappa; a.rCut = c->rCut; a.maxRStep = c->p.maxRStep; a.Gamma = c->p.Gamma;
     a.micT = mic_threshold(c->L);
+    a.fast = c->p.force_kernel == 1;
+    a.rc2 = sqrt_threshold(c->rCut);
     for (int done = 0; done < nsteps;) {                      // bounded launches
         a.nsteps = std::min(10000, nsteps - done);
         HIPCHK(launch_monte_carlo(a, c->st));

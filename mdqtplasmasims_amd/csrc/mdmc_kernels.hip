@@ -213,12 +213,64 @@ __device__ __forceinline__ double mt_uniform_lds(MtLds& m, MtPos& r) {
     const double u = (r2[0] + r2[1] * 4294967296.0) / 18446744073709551616.0;
     return u >= 1.0 ? 0x1.fffffffffffffp-1 : u;
 }
+__device__ __forceinline__ uint32_t mt_temper(uint32_t z) {
+    z ^= z >> 11;
+    z ^= (z << 7) & 0x9d2c5680u;
+    z ^= (z << 15) & 0xefc60000u;
+    z ^= z >> 18;
+    return z;
+}
+__device__ __forceinline__ double mt_canonical(uint32_t g1, uint32_t g2) {   // generate_canonical<double, 53>
+    const double u = ((double)g1 + (double)g2 * 4294967296.0) / 18446744073709551616.0;
+    return u >= 1.0 ? 0x1.fffffffffffffp-1 : u;
+}
+// the four uniforms of one proposal attempt (MCMD:326-331): the 8 words are read with independent
+// LDS loads (one latency instead of eight) when they lie in the current buffer
+__device__ __forceinline__ void mt_uniform4_lds(MtLds& m, MtPos& r, double* u) {
+    if (r.p + 8 <= 624) {
+        const uint32_t* src = m.w[r.cur] + r.p;
+        uint32_t g[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = src[k];
+        r.p += 8;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = mt_canonical(mt_temper(g[2 * k]), mt_temper(g[2 * k + 1]));
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = mt_uniform_lds(m, r);
+}
 __device__ __forceinline__ double mic_t(double d, double L, double T) {
     const double s = (double)(d >= T) - (double)(d <= -T);
     return d - L * s;
 }
 
-template <int NPT>
+// pair energy u(r) of one separation (calcUIJ :153-159) with the reference's pair set: the exact
+// division-free minimum image and r2 as :292-293; the lattice start puts pairs exactly on the
+// cutoff, so FAST tests r2 < rc2 (= sqrt(r2) < rCut) and only then takes the value through
+// rsq + 2 Newton steps and exp_neg (a few ulp, no division or library call).  Otherwise the
+// reference's operations (sqrt, libm exp, division).
+__device__ __forceinline__ double mic_c(double d, double L, double T) {   // = mic_t, 4 operations
+    return (fabs(d) >= T) ? d - copysign(L, d) : d;
+}
+template <bool FAST>
+__device__ __forceinline__ double mc_pair(double dx, double dy, double dz, const MCArgs& a) {
+    dx = mic_c(dx, a.L, a.micT);
+    dy = mic_c(dy, a.L, a.micT);
+    dz = mic_c(dz, a.L, a.micT);
+    const double r2 = dx * dx + dy * dy + dz * dz;                    // :292-293
+    if (FAST) {
+        double ri = __builtin_amdgcn_rsq(r2);
+        const double hr = 0.5 * r2;
+        ri = ri * fma(-hr * ri, ri, 1.5);
+        ri = ri * fma(-hr * ri, ri, 1.5);
+        const double u = exp_neg(-a.kappa * (r2 * ri)) * ri;
+        return r2 < a.rc2 ? u : 0.;                                    // = sqrt(r2) < rCut
+    }
+    return mc_uij(sqrt(r2), a.kappa, a.rCut);
+}
+
+template <int NPT, bool FAST>
 __global__ __launch_bounds__(MCT) void k_monte_carlo_lds(MCArgs a) {
     extern __shared__ double sR[];                   // [3][N]
     __shared__ MtLds mt;
@@ -227,7 +279,7 @@ __global__ __launch_bounds__(MCT) void k_monte_carlo_lds(MCArgs a) {
     __shared__ double s_part[2][MCT / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int N = a.N, S = a.S;
-    const double L = a.L, T = a.micT;
+    const double L = a.L;
     double* X = sR;
     double* Y = sR + N;
     double* Z = sR + 2 * N;
@@ -252,11 +304,13 @@ __global__ __launch_bounds__(MCT) void k_monte_carlo_lds(MCArgs a) {
         int P;
         double rx, ry, rz;
         for (;;) {
-            const double randPart = mt_uniform_lds(mt, r);
+            double u[4];
+            mt_uniform4_lds(mt, r, u);
+            const double randPart = u[0];
             P = (int)floor(randPart * N);
-            rx = a.maxRStep * (2 * mt_uniform_lds(mt, r) - 1);
-            ry = a.maxRStep * (2 * mt_uniform_lds(mt, r) - 1);
-            rz = a.maxRStep * (2 * mt_uniform_lds(mt, r) - 1);
+            rx = a.maxRStep * (2 * u[1] - 1);
+            ry = a.maxRStep * (2 * u[2] - 1);
+            rz = a.maxRStep * (2 * u[3] - 1);
             if (rx * rx + ry * ry + rz * rz < a.maxRStep * a.maxRStep) break;
         }
         s_P = P; s_d[0] = rx; s_d[1] = ry; s_d[2] = rz;
@@ -293,11 +347,8 @@ __global__ __launch_bounds__(MCT) void k_monte_carlo_lds(MCArgs a) {
             if (j >= N) continue;
             if (j == P) { s_UP = U[q]; continue; }
             const double cx = X[j], cy = Y[j], cz = Z[j];
-            const double xn = mic_t(nx - cx, L, T), yn = mic_t(ny - cy, L, T), zn = mic_t(nz - cz, L, T);
-            const double xo = mic_t(ox - cx, L, T), yo = mic_t(oy - cy, L, T), zo = mic_t(oz - cz, L, T);
-            const double dO = sqrt(xo * xo + yo * yo + zo * zo);
-            const double dN = sqrt(xn * xn + yn * yn + zn * zn);
-            const double uN = mc_uij(dN, a.kappa, a.rCut), uO = mc_uij(dO, a.kappa, a.rCut);
+            const double uN = mc_pair<FAST>(nx - cx, ny - cy, nz - cz, a);
+            const double uO = mc_pair<FAST>(ox - cx, oy - cy, oz - cz, a);
             tot = tot + uN;
             Un[q] = U[q] + (uN - uO);                                   // U[j] += (UijNew - UijOld)
             dsum = dsum + (Un[q] - U[q]);
@@ -314,11 +365,20 @@ __global__ __launch_bounds__(MCT) void k_monte_carlo_lds(MCArgs a) {
         // ---- thread 0: accept / reject (:341-381), then the next step's draws
         if (tid == 0) {
             MtPos r{mt.p, mt.cur, mt.ahead};
-            double Tt = 0., Dd = 0.;
-            for (int q = 0; q < MCT / 64; ++q) { Tt = Tt + s_part[0][q]; Dd = Dd + s_part[1][q]; }
+            double t16[MCT / 64], d16[MCT / 64];                           // fixed-shape trees: depth 4
+#pragma unroll
+            for (int q = 0; q < MCT / 64; ++q) { t16[q] = s_part[0][q]; d16[q] = s_part[1][q]; }
+#pragma unroll
+            for (int h = MCT / 128; h >= 1; h >>= 1)
+#pragma unroll
+                for (int q = 0; q < h; ++q) { t16[q] = t16[2 * q] + t16[2 * q + 1]; d16[q] = d16[2 * q] + d16[2 * q + 1]; }
+            const double Tt = t16[0], Dd = d16[0];
             const double dE = Dd + (Tt - s_UP);
             bool good = dE < 0;
-            if (!good) good = mt_uniform_lds(mt, r) < exp(-(dE / 2) * a.Gamma);
+            if (!good) {                                                     // :353-360
+                const double dice = mt_uniform_lds(mt, r);
+                good = dice < (FAST ? exp_neg(-(dE / 2) * a.Gamma) : exp(-(dE / 2) * a.Gamma));
+            }
             s_acc = good;
             s_tot = Tt;
             if (good) { X[P] = nx; Y[P] = ny; Z[P] = nz; ++acc; }
@@ -594,14 +654,18 @@ hipError_t launch_particle_potentials(const double* R, int N, int S, double L, d
     hipLaunchKernelGGL(k_particle_potentials, dim3((N + 255) / 256), dim3(256), 0, s, R, N, S, L, kappa, rCut, U);
     return hipGetLastError();
 }
+template <int NPT, bool FAST>
+static hipError_t launch_mc_lds_v(const MCArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)3 * a.N * sizeof(double);
+    hipError_t e = hipFuncSetAttribute((const void*)k_monte_carlo_lds<NPT, FAST>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_monte_carlo_lds<NPT, FAST>), dim3(1), dim3(MCT), lds, s, a);
+    return hipGetLastError();
+}
 template <int NPT>
 static hipError_t launch_mc_lds(const MCArgs& a, hipStream_t s) {
-    const size_t lds = (size_t)3 * a.N * sizeof(double);
-    hipError_t e = hipFuncSetAttribute((const void*)k_monte_carlo_lds<NPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_monte_carlo_lds<NPT>, dim3(1), dim3(MCT), lds, s, a);
-    return hipGetLastError();
+    return a.fast ? launch_mc_lds_v<NPT, true>(a, s) : launch_mc_lds_v<NPT, false>(a, s);
 }
 hipError_t launch_monte_carlo(const MCArgs& a, hipStream_t s) {
     if (a.nsteps <= 0) return hipSuccess;

@@ -195,7 +195,7 @@ extern "C" int mdqt_device_count(void) {
 // H = detunings on the P levels (-det -/+ v_q, :439) + S-P couplings -Om/2 sqrt(gs[x]) |a><b|
 // + h.c. (:438); M = I - i h H.  No optical kick, no time-dependent coupling.
 static void build_pump_tables(const mdqt_params* p, QTConst& q, FastTab& f) {
-    const double r = 0.0617, h = q.h;                          // decayRatio (:118)
+    const double r = q.r, h = q.h;                             // decayRatio (408: 0.0617 :118; 422: 0.0754 :116)
     // channel j = |a_j><b_j|: 408 a = {0,0,0,1,1,1,6,6,6,6}, 422 a = {1,1,0,0,4,4}; only b enters D
     static const int B408[10] = {2, 3, 4, 3, 4, 5, 2, 3, 4, 5};
     const double G408[10] = {1, 2. / 3, 1. / 3, 1. / 3, 2. / 3, 1, r, r, r, r};
@@ -243,11 +243,17 @@ static void build_pump_tables(const mdqt_params* p, QTConst& q, FastTab& f) {
 
 static void build_constants(mdqt_ctx* s) {
     const mdqt_params* p = &s->p;
-    s->gamToE = 174.07 / sqrt(p->density);                      // :79
-    s->ratio = (int)ceil(34.81 / sqrt(p->density));             // :83
-    s->dtQ = TIMESTEP / s->ratio;                               // :84
-    s->pv2q = 1.1821 * pow(p->density, 1. / 6);                 // :85
-    s->r = 0.0617;                                              // :146
+    // SpeedUp :79-85, :146; the pumping programs' own constants: 408 nm
+    // (randomFrozenStartTag408Linear.cpp:67-75, :118; 408Quad :69-77, :121: round, not ceil) and
+    // 422 nm (randomFrozenStartTag422Linear.cpp:66-74, :116: gamma ratio .894, velocity .967, D/S 0.0754)
+    const int m = p->qt_model;
+    s->gamToE = m == 3 ? 174.07 * .894 / sqrt(p->density) : 174.07 / sqrt(p->density);
+    s->ratio = m == 0   ? (int)ceil(34.81 / sqrt(p->density))
+               : m == 3 ? (int)round(34.81 * .894 / sqrt(p->density))
+                        : (int)round(34.81 / sqrt(p->density));
+    s->dtQ = TIMESTEP / s->ratio;
+    s->pv2q = m == 3 ? 1.1821 * pow(p->density, 1. / 6) * .967 : 1.1821 * pow(p->density, 1. / 6);
+    s->r = m == 3 ? 0.0754 : 0.0617;
     s->kRat = 0.395;                                            // :147
     s->vKick = 0.001208 / s->pv2q;                              // :148
     s->vKickDP = s->vKick * s->kRat;                            // :149
@@ -1089,6 +1095,7 @@ extern "C" int mdqt_md_steps(mdqt_ctx* s, int n) {
 static int pairs_raw(int mode, int N, double L, double lDeb, const double* R, size_t ld, double* out,
                      int nseg_req, int device, int variant) {
     if (N < 1 || !R || !out || ld < (size_t)N) return fail("pairs_raw: bad arguments");
+    if (variant < 0 || variant > 1) return fail("pairs_raw: variant must be 0 (exact) or 1 (fast)");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail("no HIP device available");
     if (device >= 0) HIPCHK(hipSetDevice(device));

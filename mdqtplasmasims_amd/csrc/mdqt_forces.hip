@@ -7,8 +7,10 @@
 //
 // VARIANT 0 keeps the reference's operations (sqrt, the three divisions, libm exp) without
 // contraction; VARIANT 1 (default) is the reciprocal form with a range-specialised exp and
-// FMA contraction — a few ulp per pair, inside the 1e-13 force gate.  Both evaluate the minimum
-// image exactly without dividing (see PairC / mic below).
+// FMA contraction — a few ulp per pair, inside the 1e-13 force gate.  VARIANT 2 (Newton-3
+// tiles; the MC + MD program, whose lattice start puts pairs exactly on the cutoff and on the
+// image boundary) has variant 1's values with variant 0's pair set: the exact minimum image and
+// the cutoff as r2 < rc2, rc2 the smallest double with sqrt(rc2) >= Rcut.
 #include "mdqt_internal.hpp"
 
 #include <math.h>
@@ -17,35 +19,12 @@ namespace mdqt {
 
 struct PairC {
     double L, T, G, Rcut, lDeb, invlDeb, invL;
+    double rc2;         // VARIANT 2: pair kept iff r2 < rc2 (= sqrt(r2) < Rcut exactly)
 };
 
 __device__ __forceinline__ const double* pos_base(const double* Rall, int g, int S) {
     const int w = g / S;
     return Rall + (size_t)w * 3 * S + (g - w * S);
-}
-
-// e^x for x = -r/lDeb in [-L/(2 lDeb), 0] (no overflow, no subnormal results for any box the
-// reference runs): Cody-Waite x = n ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial
-// (truncation < 5e-18 relative) in FMA Horner form, exponent shift.  <= 1 ulp vs glibc.
-__device__ __forceinline__ double exp_neg(double x) {
-    const double n = __builtin_rint(x * 1.4426950408889634);
-    double r = fma(-n, 0x1.62e42fefa39efp-1, x);
-    r = fma(-n, 0x1.abc9e3b39803fp-56, r);
-    double p = 1.6059043836821613e-10;               // 1/13!
-    p = fma(p, r, 2.08767569878681e-09);
-    p = fma(p, r, 2.505210838544172e-08);
-    p = fma(p, r, 2.755731922398589e-07);
-    p = fma(p, r, 2.7557319223985893e-06);
-    p = fma(p, r, 2.48015873015873e-05);
-    p = fma(p, r, 0.0001984126984126984);
-    p = fma(p, r, 0.001388888888888889);
-    p = fma(p, r, 0.008333333333333333);
-    p = fma(p, r, 0.041666666666666664);
-    p = fma(p, r, 0.16666666666666666);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    return ldexp(p, (int)n);
 }
 
 // Minimum image dx -= L*round(dx/L) (SpeedUp:218-220), exactly, without the division: for
@@ -99,6 +78,8 @@ __device__ __forceinline__ double pair_ft(double dx, double dy, double dz, const
         ri = ri * fma(-hr * ri, ri, 1.5);
         const double dr = r2 * ri;
         const double ft = ((ri + c.invlDeb) * exp_neg(-dr * c.invlDeb)) * (ri * ri);
+        if (VARIANT == 2)                        // the reference's pair set: r2 as :216, exact cutoff
+            return (dx * dx + dy * dy + dz * dz < c.rc2 && r2 > 0) ? ft : 0.;
         return (dr < c.Rcut) ? ft : 0.;          // r2 = 0 (coincident ions) gives dr = NaN: 0
     }
 }
@@ -308,7 +289,7 @@ __global__ __launch_bounds__(256) void k_pairs_n3(N3Args a) {
     __shared__ double ia[4][3][64];
     __shared__ double mj[128];
     const int2 IJ = a.pairs[blockIdx.x];
-    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L};
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
     if ((a.N & 63) && IJ.y == a.ntiles - 1) n3_tile<VARIANT, GUARD, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
     else n3_tile<VARIANT, GUARD, false>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
 }
@@ -355,7 +336,9 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
 }
 
 template <int VARIANT, bool GUARD>
-__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pairs_n3b(N3BArgs a) {
+// the fast variant fits 64 VGPRs (8 waves per SIMD); the exact one (libm exp, divisions) gets 128
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(VARIANT == 1 ? 8 : 4, VARIANT == 1 ? 8 : 4)))
+void k_pairs_n3b(N3BArgs a) {
     __shared__ double pj[3][128];
     __shared__ double mj[128];
     __shared__ double accj[BW][3][128];
@@ -486,7 +469,10 @@ hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int 
 hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s) {
     if (a.npairs <= 0) return hipSuccess;
     dim3 grid(a.npairs);
-    if (variant == 1) {
+    if (variant == 2) {
+        if (a.guard) hipLaunchKernelGGL((k_pairs_n3<2, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_pairs_n3<2, false>), grid, dim3(256), 0, s, a);
+    } else if (variant == 1) {
         if (a.guard) hipLaunchKernelGGL((k_pairs_n3<1, true>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_pairs_n3<1, false>), grid, dim3(256), 0, s, a);
     } else {

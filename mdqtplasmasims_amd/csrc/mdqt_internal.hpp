@@ -159,6 +159,30 @@ struct ForceArgs {
                         // report): range-check every pair, far separations take the division form
 };
 
+// e^x for x = -r/lDeb in [-L/(2 lDeb), 0] (no overflow, no subnormal results for any box the
+// reference runs): Cody-Waite x = n ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial
+// (truncation < 5e-18 relative) in FMA Horner form, exponent shift.  <= 1 ulp vs glibc.
+__device__ __forceinline__ double exp_neg(double x) {
+    const double n = __builtin_rint(x * 1.4426950408889634);
+    double r = fma(-n, 0x1.62e42fefa39efp-1, x);
+    r = fma(-n, 0x1.abc9e3b39803fp-56, r);
+    double p = 1.6059043836821613e-10;               // 1/13!
+    p = fma(p, r, 2.08767569878681e-09);
+    p = fma(p, r, 2.505210838544172e-08);
+    p = fma(p, r, 2.755731922398589e-07);
+    p = fma(p, r, 2.7557319223985893e-06);
+    p = fma(p, r, 2.48015873015873e-05);
+    p = fma(p, r, 0.0001984126984126984);
+    p = fma(p, r, 0.001388888888888889);
+    p = fma(p, r, 0.008333333333333333);
+    p = fma(p, r, 0.041666666666666664);
+    p = fma(p, r, 0.16666666666666666);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)n);
+}
+
 // Canonical sum of nseg partials p[0], p[stride], ... : eight interleaved accumulators
 // (partial s goes to s % 8, ascending) combined as ((a0+a1)+(a2+a3))+((a4+a5)+(a6+a7)).  One
 // fixed order wherever it is evaluated (deterministic); independent loads, short chains.
@@ -185,6 +209,7 @@ struct N3Args {
     int N, S, ntiles, npairs;
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;          // as ForceArgs::guard (exact variant only; the fast one needs no guard)
+    double rc2;         // variant 2: smallest double x with sqrt(x) >= Rcut (pair kept iff r2 < rc2)
 };
 
 // Newton-3 over block pairs (mdqt_forces.hip k_pairs_n3b): blocks of 16 tiles, cyclic half
@@ -212,6 +237,9 @@ struct MCArgs {
     int N, S, nsteps;
     double L, kappa, rCut, maxRStep, Gamma;
     double micT;        // smallest d with fl(d / L) >= 0.5: round(d/L) without a division, |d| < 1.25 L
+    int fast;           // 1: reciprocal pair energy values (rsq, exp_neg; <= 2 ulp per pair), 0: the reference's ops;
+                        //    both keep the reference's pair set: exact image, cutoff as r2 < rc2
+    double rc2;         // smallest double x with sqrt(x) >= rCut
 };
 struct VVArgs {
     double* V;

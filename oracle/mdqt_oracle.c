@@ -171,13 +171,17 @@ orc_sim* orc_create(const orc_params* p) {
     orc_sim* s = calloc(1, sizeof(orc_sim));
     if (!s) return NULL;
     s->p = *p;
-    /* SpeedUp:79-85 */
-    s->gamToE = 174.07 / sqrt(p->density);
-    s->ratio = (int)ceil(34.81 / sqrt(p->density));
+    /* SpeedUp:79-85, :146; the pumping programs: randomFrozenStartTag408Linear.cpp:67-75, :118
+       (408Quad :69-77, :121) round the ratio; randomFrozenStartTag422Linear.cpp:66-74, :116 scale
+       gamma by .894 and the velocity conversion by .967, D/S decay ratio 0.0754 */
+    const int m = p->qt_model;
+    s->gamToE = m == 3 ? 174.07 * .894 / sqrt(p->density) : 174.07 / sqrt(p->density);
+    s->ratio = m == 0 ? (int)ceil(34.81 / sqrt(p->density))
+             : m == 3 ? (int)round(34.81 * .894 / sqrt(p->density)) : (int)round(34.81 / sqrt(p->density));
     s->dtQ = TIMESTEP / s->ratio;
-    s->plasVelToQuantVel = 1.1821 * pow(p->density, 1. / 6);
+    s->plasVelToQuantVel = m == 3 ? 1.1821 * pow(p->density, 1. / 6) * .967 : 1.1821 * pow(p->density, 1. / 6);
     /* SpeedUp:146-149 */
-    s->r = 0.0617;
+    s->r = m == 3 ? 0.0754 : 0.0617;
     s->kRat = 0.395;
     s->vKick = 0.001208 / s->plasVelToQuantVel;
     s->vKickDP = s->vKick * s->kRat;

@@ -80,9 +80,14 @@ void mdref_step_positions(double* Rio, const double* Vin, const double* Ain) {
 }
 
 // ---- seeded program stages (the reference's own code; only the seed is ours) ----
-// rng as right after the program's static initialisation with seed s: mt19937 seeded, one
-// uniform drawn by `auto random_double = uni(rng);` (:52-55)
+// the program's state right after its static initialisation, with seed s: zeroed globals
+// (R, V, A, U, :110-123 — the first MDStep reads A as oldA), mt19937 seeded, one uniform drawn by
+// `auto random_double = uni(rng);` (:52-55)
 void mdref_seed(unsigned s) {
+    std::memset(R, 0, sizeof(R));
+    std::memset(V, 0, sizeof(V));
+    std::memset(A, 0, sizeof(A));
+    std::memset(U, 0, sizeof(U));
     rng.seed(s);
     uni.reset();
     velocityDistribution.reset();

@@ -11,12 +11,25 @@ import math
 
 import numpy as np
 
-from tests.dense_qt import constants
-
-decayRatio = 0.0617
 
 
-def operators(model):
+def model_constants(model, density=2.0):
+    """the pumping programs' constants: randomFrozenStartTag408Linear.cpp:67-75, :118 (408Quad
+    :69-77, :121) and randomFrozenStartTag422Linear.cpp:66-74, :116 (C round(): half away from 0)"""
+    if model == 3:
+        gamToE = 174.07 * .894 / math.sqrt(density)
+        ratio = int(math.floor(34.81 * .894 / math.sqrt(density) + 0.5))
+        pv2q = 1.1821 * density ** (1.0 / 6) * .967
+        decay = 0.0754
+    else:
+        gamToE = 174.07 / math.sqrt(density)
+        ratio = int(math.floor(34.81 / math.sqrt(density) + 0.5))
+        pv2q = 1.1821 * density ** (1.0 / 6)
+        decay = 0.0617
+    return dict(gamToE=gamToE, ratio=ratio, dtQ=0.002 / ratio, pv2q=pv2q, decayRatio=decay)
+
+
+def operators(model, decayRatio):
     n = 5 if model == 3 else 7
     ident = np.eye(n)
     w = [ident[:, k].reshape(n, 1).astype(complex) for k in range(n)]   # wvFn1.. -> w[0..]
@@ -34,8 +47,9 @@ def operators(model):
 def qstep_ion(psi12, vx, tPart, u, model, Om, detuning, density=2.0):
     """One ion through the pumping qstep; u: the uniforms in the reference's draw order.
     Returns (psi12', vx', tPart', jumped)."""
-    c = constants(density)
-    n, w, cs, gs = operators(model)
+    c = model_constants(model, density)
+    decayRatio = c["decayRatio"]
+    n, w, cs, gs = operators(model, decayRatio)
     H = lambda a: a.conj().T
     dtQuant, gamToE = c["dtQ"], c["gamToE"]
     hh = dtQuant * gamToE

@@ -106,9 +106,11 @@ def test_init_matches_reference(mc, refmc):
 
 
 @pytest.mark.gpu
-def test_monte_carlo_matches_reference(mc, refmc):
+@pytest.mark.parametrize("force_kernel", [0, 1])
+def test_monte_carlo_matches_reference(mc, refmc, force_kernel):
     with tempfile.TemporaryDirectory() as tmp:
-        ref, eng = _pair(mc, refmc, 12, tmp)
+        ref = refmc.RefMCMD(seed=12, save_directory=tmp + "/")
+        eng = mc.MonteCarloMD(seed=12, saveDirectory=tmp + "/", force_kernel=force_kernel)
         ref.init(); eng.init()
         ref.monte_carlo(1500); acc = eng.monte_carlo(1500)
         ref.monte_carlo(1500); acc += eng.monte_carlo(1500)   # the rng state handed over twice
@@ -123,11 +125,15 @@ def test_monte_carlo_matches_reference(mc, refmc):
 
 
 @pytest.mark.gpu
-def test_md_steps_with_collisions_and_laser_match_reference(mc, refmc):
+@pytest.mark.parametrize("mc_steps,force_kernel", [(500, 1), (0, 1), (0, 0)])
+def test_md_steps_with_collisions_and_laser_match_reference(mc, refmc, mc_steps, force_kernel):
+    """mc_steps 0: MD from the cubic lattice itself, where pairs sit exactly on the cutoff and on
+    the image boundary — the fast force variant must keep the reference's pair set"""
     with tempfile.TemporaryDirectory() as tmp:
-        ref, eng = _pair(mc, refmc, 13, tmp)
+        ref = refmc.RefMCMD(seed=13, save_directory=tmp + "/")
+        eng = mc.MonteCarloMD(seed=13, saveDirectory=tmp + "/", force_kernel=force_kernel)
         ref.init(); eng.init()
-        ref.monte_carlo(500); eng.monte_carlo(500)
+        ref.monte_carlo(mc_steps); eng.monte_carlo(mc_steps)
         R, V, A, U = ref.get_state()
         assert np.array_equal(R, eng.get_state()[0])
         ref.set_collision_freq(20.0); eng.set_collision_freq(20.0)     # ~10% of ions collide per step

@@ -237,11 +237,33 @@ def test_pump_kat_decay_matrix(orc):
     level schemes (408: 1 + r, 2/3 + 1/3 + r, 1/3 + 2/3 + r, 1 + r; 422: 2/3 + 1/3 + r each)"""
     from tests import dense_pump
     for model in (1, 3):
-        n, w, cs, gs = dense_pump.operators(model)
+        r = dense_pump.model_constants(model)["decayRatio"]
+        n, w, cs, gs = dense_pump.operators(model, r)
         D = sum(gs[j] * cs[j].conj().T @ cs[j] for j in range(len(cs)))
         P = range(2, 6) if model == 1 else range(2, 4)
         for k in range(n):
-            assert abs(D[k, k] - ((1 + dense_pump.decayRatio) if k in P else 0.)) < 1e-15
+            assert abs(D[k, k] - ((1 + r) if k in P else 0.)) < 1e-15
+
+
+@pytest.mark.parametrize("model,density", [(1, 2.0), (2, 2.0), (3, 2.0), (1, 0.5), (3, 3.0), (0, 2.0)])
+def test_pump_program_constants(orc, model, density):
+    """KAT of the programs' own constants: SpeedUp ceil(34.81/sqrt(d)) (:83); the 408 programs
+    round(34.81/sqrt(d)) (randomFrozenStartTag408Linear.cpp:73); the 422 program gamma x .894,
+    round(34.81*.894/sqrt(d)), velocity x .967, D/S ratio 0.0754 (randomFrozenStartTag422Linear.cpp
+    :66-74, :116).  At density 2: ratios 25, 25, 22."""
+    import math
+    from tests import dense_pump
+    s = orc.OracleSim(qt_model=model, density=density)
+    if model == 0:
+        assert s.const("plasmaToQuantumTimestepRatio") == math.ceil(34.81 / math.sqrt(density))
+        assert s.const("decayRatioD5Halves") == 0.0617
+        return
+    c = dense_pump.model_constants(model, density)
+    assert s.const("plasmaToQuantumTimestepRatio") == c["ratio"]
+    assert s.const("plasVelToQuantVel") == c["pv2q"]
+    assert s.const("decayRatioD5Halves") == c["decayRatio"]
+    if density == 2.0:
+        assert c["ratio"] == (22 if model == 3 else 25)
 
 
 def test_run_layout_and_formats(orc, tmp_path):

@@ -290,7 +290,40 @@ def mcmd_line(local, cpu=True, mc_steps=20000, md_steps=2000):
                                     "main_estimate_s": rest,
                                     "sample": "the reference's MonteCarloStep x2000 and MDStep x3 "
                                               "(oracle/_ref/libmdref.so, 1 thread)"}
+    line["qt_tagging"] = qtt_line(local)
     return line
+
+
+def qtt_line(local, steps=10):
+    """MonteCarloFollowedByQTTagging408Linear.cpp (include/mdmc.h qt_model 1) at its own
+    size, N = 4096: the pump period (plasmaToQuantumTimestepRatio QT steps + one MD step per MD step)
+    and the recorded period's tagged moments + 3 x 4001-bin velocity distributions.  The reference
+    needs Armadillo (absent): no CPU baseline."""
+    import tempfile
+    from mdqtplasmasims_amd import mdmc
+    tmp = tempfile.mkdtemp(prefix="qtt_bench_")
+    e = mdmc.MonteCarloMD(qt_model=1, device=local, seed=3, saveDirectory=tmp + "/")
+    e.init()
+    ratio = int(e.const("plasmaToQuantumTimestepRatio"))
+    e.qsteps(ratio)
+    e.md_steps(1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e.qsteps(ratio)
+        e.md_steps(1)
+    pump_ms = (time.perf_counter() - t0) / steps * 1e3
+    e.tag_qt()
+    e.tagged_moments_qt()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e.tagged_moments_qt()
+    kde_ms = (time.perf_counter() - t0) / steps * 1e3
+    N = e.N
+    e.close()
+    return {"workload": "MonteCarloFollowedByQTTagging408Linear.cpp: N=4096, n=2, pump 62 QT steps per MD step",
+            "N": N, "qsteps_per_md_step": ratio, "pump_ms_per_md_step": pump_ms,
+            "particle_qsteps_per_s": N * ratio / (pump_ms * 1e-3),
+            "tagged_moments_and_distribution_ms": kde_ms, "cpu_baseline": None}
 
 
 def sharded_run(cfg, steps, rank, world, local, dist, barrier):

@@ -14,6 +14,16 @@
  * Conventions as include/mdqt.h: opaque context, int status (0 ok, <0 error; message in
  * mdqt_last_error()), caller-owned host buffers, R/V/A as [3][N] row-major like the reference's
  * `double R[3][N]` (MCMD:110-112), device state resident between calls.
+ *
+ * The same engine runs the QT spin-tagging variants of the program ("QTT":
+ * MonteCarloFollowedByQTTagging408Linear.cpp / 408Quad.cpp / 422Linear.cpp; qt_model 1 / 2 / 3):
+ * the same MC anneal and collisional MD, then a pump period of QT steps (the optical-pumping
+ * qstep of include/mdqt.h's qt_model, QTT:555, driven by this system's velocities) between MD
+ * steps, QT tagging (QTT:1022) and collisionless MD recording the tagged ions' moments and
+ * velocity distribution (QTT:1069-1138) and the autocorrelations.  Wavefunctions start as the
+ * reference's random S superpositions from its drand48 stream (default seed, QTT:224-239); the
+ * QT jump draws use the Philox stream of include/mdqt.h (keyed by seed, job, ion, qstep index)
+ * instead of the reference's shared drand48.
  */
 #ifndef MDMC_H
 #define MDMC_H
@@ -51,15 +61,25 @@ typedef struct mdmc_params {
     int device;                   /* HIP device ordinal (-1 = current)                           */
     int force_kernel;             /* 1 (default): reciprocal pair forms (MD forces, MC energies;
                                    * a few ulp per pair), 0: the reference's operations          */
+    /* ---- QT tagging variants (QTT:84-121) ---- */
+    int qt_model;                 /* 0: MCMD (no QT); 1: 408 linear, 2: 408 quad, 3: 422 linear    */
+    double tpumpreal;             /* QTT:85 pump time (s)                                          */
+    double detuning;              /* QTT:86 pump detuning (units of gamma)                         */
+    double Om;                    /* QTT:87 Rabi frequency (units of gamma)                        */
     char saveDirectory[256];      /* :62 */
 } mdmc_params;
 
 typedef struct mdmc_ctx mdmc_ctx;
 
 void        mdmc_default_params(mdmc_params* p);              /* MCMD:62-107 defaults         */
+/* the QT tagging program's defaults (QTT:75-121: n = 2, 100000 MC steps, 1500 recorded steps,
+ * the model's pump time, detuning, Rabi frequency and save directory); model 1..3 */
+int         mdmc_default_params_qt(mdmc_params* p, int model);
 int         mdmc_create(const mdmc_params* p, mdmc_ctx** out); /* + rng (:52-55), L, rCut (:73-74) */
 void        mdmc_destroy(mdmc_ctx* c);
-double      mdmc_get_const(const mdmc_ctx* c, const char* name); /* "N", "L", "rCut", "nbins"  */
+/* "N", "L", "rCut", "nbins", "collisionFreq"; QT: "plasmaToQuantumTimestepRatio",
+ * "quantumTimestep", "gamToEinsteinFreq", "plasVelToQuantVel", "decayRatio", "pumpMDTimeSteps" */
+double      mdmc_get_const(const mdmc_ctx* c, const char* name);
 
 /* ---- the program's functions ---- */
 int mdmc_init(mdmc_ctx* c);                 /* init() :173-203 + calculatePotentialEnergyForParticles() :207-245 */
@@ -86,7 +106,18 @@ int mdmc_get_state(mdmc_ctx* c, double* R, double* V, double* A, double* U);    
 int mdmc_set_state(mdmc_ctx* c, const double* R, const double* V, const double* A, const double* U);
 int mdmc_setup_directories(mdmc_ctx* c);            /* main() :1037-1058                        */
 const char* mdmc_save_directory(const mdmc_ctx* c);
-int mdmc_run(mdmc_ctx* c, int verbose);             /* main() :1030-1167: every stage and file  */
+int mdmc_run(mdmc_ctx* c, int verbose);             /* main() :1030-1167 (QTT: :1140-1254): every stage and file */
+
+/* ---- QT tagging variants (qt_model 1..3) ---- */
+int mdmc_qsteps(mdmc_ctx* c, int n);                /* qstep() x n (QTT:555-756), velocities read from the MD state */
+/* tagParticles (QTT:1022-1067): tags [N] 0/1 (or NULL), *n_up = number tagged (or NULL) */
+int mdmc_tag_qt(mdmc_ctx* c, int* tags, int* n_up);
+/* recordTaggedParticleMoments (QTT:1069-1138): out4 = first .. fourth moment of vx over the tagged
+ * ions; dist (or NULL) = [3][4001] normalised velocity distributions of the tagged ions on the
+ * bins (j - 2000) * 0.0025 (the reference writes the x row to vel_distX_timestep%06d.dat) */
+int mdmc_tagged_moments_qt(mdmc_ctx* c, double out4[4], double* dist);
+int mdmc_get_psi(mdmc_ctx* c, double* psi);         /* [N][12][2] (re, im; states past the model's zero) */
+int mdmc_set_psi(mdmc_ctx* c, const double* psi);
 
 #ifdef __cplusplus
 }

@@ -43,6 +43,7 @@ class MdmcParams(C.Structure):
         ("applyForceAlongOneAxisOnly", C.c_int), ("beta", C.c_double),
         ("anisotropyEstablishmentTime", C.c_int), ("anisotropyFromForcesRelaxSteps", C.c_int),
         ("seed", C.c_uint32), ("job", C.c_uint32), ("device", C.c_int), ("force_kernel", C.c_int),
+        ("qt_model", C.c_int), ("tpumpreal", C.c_double), ("detuning", C.c_double), ("Om", C.c_double),
         ("saveDirectory", C.c_char * 256),
     ]
 
@@ -73,6 +74,12 @@ MDMC_SIGNATURES = [
     ("mdmc_setup_directories", C.c_int, [C.c_void_p]),
     ("mdmc_save_directory", C.c_char_p, [C.c_void_p]),
     ("mdmc_run", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdmc_default_params_qt", C.c_int, [C.POINTER(MdmcParams), C.c_int]),
+    ("mdmc_qsteps", C.c_int, [C.c_void_p, C.c_int]),
+    ("mdmc_tag_qt", C.c_int, [C.c_void_p, _ip, _ip]),
+    ("mdmc_tagged_moments_qt", C.c_int, [C.c_void_p, _dp, _dp]),
+    ("mdmc_get_psi", C.c_int, [C.c_void_p, _dp]),
+    ("mdmc_set_psi", C.c_int, [C.c_void_p, _dp]),
 ]
 
 # (name, restype, argtypes) of every symbol include/mdqt.h declares

@@ -1,7 +1,9 @@
-// mdmc — drop-in command line for MonteCarloFollowedByMDAndTempAnisotropy.cpp.
+// mdmc — drop-in command line for MonteCarloFollowedByMDAndTempAnisotropy.cpp and, with
+// --qt_model=1|2|3, for MonteCarloFollowedByQTTagging408Linear.cpp / 408Quad.cpp / 422Linear.cpp.
 //
 //   reference:  ./a.out <job>                      (MCMD:1035; parameters are globals :62-107)
-//   this:       mdmc <job> [--Name=value ...]      (same parameter names and defaults)
+//   this:       mdmc <job> [--qt_model=m] [--Name=value ...]   (same parameter names and defaults;
+//               --qt_model selects the tagging program and its defaults, QTT:75-121)
 //
 // Runs main()'s stages (MCMD:1030-1167) on the GPU through include/mdmc.h and writes the same
 // directory tree and files (pairPairCorrStepNum%d.dat, temperature.dat, VAF.dat, ...).
@@ -22,13 +24,21 @@ static void usage(void) {
             "                  [--tempPercentDiff=0.15] [--applyForceAlongOneAxisOnly=0] [--beta=26000]\n"
             "                  [--anisotropyEstablishmentTime=10] [--anisotropyFromForcesRelaxSteps=2000]\n"
             "                  [--saveDirectory=data/] [--seed=<mt19937 seed; default time(NULL)+job>]\n"
-            "                  [--device=-1] [--force_kernel=1] [--quiet=0]\n");
+            "                  [--device=-1] [--force_kernel=1] [--quiet=0]\n"
+            "                  [--qt_model=0|1|2|3] [--tpumpreal=2e-7] [--detuning=-2.5] [--Om=0.7]\n");
 }
 
 int main(int argc, char** argv) {
     if (argc < 2) { usage(); return 2; }
     mdmc_params p;
     mdmc_default_params(&p);
+    for (int i = 2; i < argc; ++i)                          // the tagging program's defaults first
+        if (!strncmp(argv[i], "--qt_model=", 11) && atoi(argv[i] + 11) != 0) {
+            if (mdmc_default_params_qt(&p, atoi(argv[i] + 11)) != 0) {
+                fprintf(stderr, "mdmc: %s\n", mdqt_last_error());
+                return 2;
+            }
+        }
     const double job = atof(argv[1]);                       // MCMD:1035
     p.job = (uint32_t)job;
     int seed_given = 0, quiet = 0;
@@ -45,10 +55,11 @@ int main(int argc, char** argv) {
 #define DPAR(name) if (!strcmp(key, #name)) { p.name = atof(v); continue; }
 #define IPAR(name) if (!strcmp(key, #name)) { p.name = atoi(v); continue; }
         DPAR(kappa) DPAR(Gamma) DPAR(n) DPAR(collisionFreq) DPAR(maxRStep) DPAR(pairPairStep) DPAR(timeStep)
-        DPAR(tempPercentDiff) DPAR(beta)
+        DPAR(tempPercentDiff) DPAR(beta) DPAR(tpumpreal) DPAR(detuning) DPAR(Om)
         IPAR(N) IPAR(monteCarloSteps) IPAR(numPreRecordMDSteps) IPAR(numVelAutoCorrsSteps)
         IPAR(numInstantaneousAnisotropySteps) IPAR(numReestablishEquilSteps) IPAR(applyForceAlongOneAxisOnly)
         IPAR(anisotropyEstablishmentTime) IPAR(anisotropyFromForcesRelaxSteps) IPAR(device) IPAR(force_kernel)
+        IPAR(qt_model)
 #undef DPAR
 #undef IPAR
         if (!strcmp(key, "quiet")) { quiet = atoi(v); continue; }

@@ -98,6 +98,19 @@ struct mdmc_ctx {
     double* hHits = nullptr;       // pinned ring of collision entries (i, vx, vy, vz), read by k_collide
     int hitCap = 0, hitOff = 0;
     std::string saveDir;
+    // QT tagging variants (qt_model 1..3)
+    int qt = 0;
+    double dtQ = 0., gamToE = 0., pv2q = 0., decayRatio = 0.;
+    int qtRatio = 0, pumpSteps = 0;
+    QTConst qc;
+    FastTab ftab;
+    FastTab* dFTab = nullptr;      // [2]: by state, by lane (the same for the pumping models)
+    double* dPsi = nullptr;        // [24][S] component-major (re0, im0, re1, ...), as include/mdqt.h's engine
+    double* dTp = nullptr;         // [S] tPart
+    int* dFlags = nullptr;
+    double *dKdePart = nullptr, *dKde = nullptr;
+    uint64_t qidx = 0;
+    unsigned short x48[3] = {0x330E, 0xABCD, 0x1234};   // drand48's default state (no srand48 in QTT)
 };
 
 namespace {
@@ -169,7 +182,24 @@ extern "C" void mdmc_default_params(mdmc_params* p) {                 // MCMD:62
     p->numReestablishEquilSteps = 500; p->tempPercentDiff = 0.15; p->applyForceAlongOneAxisOnly = 0;
     p->beta = 26000; p->anisotropyEstablishmentTime = 10; p->anisotropyFromForcesRelaxSteps = 2000;
     p->seed = 12345; p->job = 1; p->device = -1; p->force_kernel = 1;
+    p->qt_model = 0; p->tpumpreal = 0.0000002; p->detuning = -2.5; p->Om = 0.7;   // QTT 408 linear :85-87
     strcpy(p->saveDirectory, "data/");
+}
+
+extern "C" int mdmc_default_params_qt(mdmc_params* p, int model) {   // QTT:75-121
+    if (!p) return set_error("mdmc_default_params_qt: NULL argument");
+    if (model < 1 || model > 3) return set_error("mdmc_default_params_qt: model must be 1, 2 or 3");
+    mdmc_default_params(p);
+    p->n = 2;                                       // :82
+    p->monteCarloSteps = 100000;                    // :98
+    p->numVelAutoCorrsSteps = 1500;                 // :109
+    p->qt_model = model;
+    static const double tp[4] = {0, 0.0000002, 0.0000001, 0.00000005};   // 408Linear :85, 408Quad :114, 422 :85
+    static const double det[4] = {0, -2.5, 0, -1}, om[4] = {0, 0.7, 2, 1.3};
+    static const char* dir[4] = {"", "data408/", "dataSpinTagQuad/", "data422/"};
+    p->tpumpreal = tp[model]; p->detuning = det[model]; p->Om = om[model];
+    strcpy(p->saveDirectory, dir[model]);
+    return 0;
 }
 
 extern "C" void mdmc_destroy(mdmc_ctx* c) {
@@ -177,7 +207,8 @@ extern "C" void mdmc_destroy(mdmc_ctx* c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     void* ps[] = {c->dR, c->dV, c->dA, c->dRn, c->dU, c->dD, c->dSlots, c->dVS, c->dPart, c->dOut,
-                  c->dTemp, c->dMom, c->dPairs, c->dHist, c->dTags, c->dMT, c->dAcc};
+                  c->dTemp, c->dMom, c->dPairs, c->dHist, c->dTags, c->dMT, c->dAcc,
+                  c->dFTab, c->dPsi, c->dTp, c->dFlags, c->dKdePart, c->dKde};
     for (void* q : ps)
         if (q) (void)hipFree(q);
     if (c->hHits) (void)hipHostFree(c->hHits);
@@ -254,6 +285,38 @@ extern "C" int mdmc_create(const mdmc_params* p, mdmc_ctx** out) {
     if (hipHostMalloc((void**)&c->hHits, (size_t)c->hitCap * 4 * sizeof(double), hipHostMallocDefault) != hipSuccess)
         return fail_free(c, "mdmc_create: pinned allocation failed");
     c->saveDir = c->p.saveDirectory;
+    if (p->qt_model != 0) {
+        // the QT tagging program's constants: 408 (QTT408Linear:115-121) / 422 (QTT422Linear:115-121)
+        const int m = p->qt_model;
+        if (m < 1 || m > 3) return fail_free(c, "mdmc_create: qt_model must be 0 .. 3");
+        const double nn = p->n;
+        c->qt = m;
+        c->gamToE = m == 3 ? 174.07 * .894 / sqrt(nn) : 174.07 / sqrt(nn);
+        c->qtRatio = m == 3 ? (int)round(87 * .894 / sqrt(nn)) : (int)round(87 / sqrt(nn));
+        c->dtQ = p->timeStep / c->qtRatio;
+        c->pv2q = m == 3 ? 1.1821 * pow(nn, 1. / 6) * .967 : 1.1821 * pow(nn, 1. / 6);
+        c->decayRatio = m == 3 ? 0.0753 : 0.0617;
+        const double tpump = p->tpumpreal * 813490 * sqrt(nn);
+        c->pumpSteps = (int)round(tpump / p->timeStep);
+        if (c->qtRatio < 1) return fail_free(c, "mdmc_create: QT substep ratio < 1");
+        build_pump_program(m, p->detuning, p->Om, c->dtQ, c->gamToE, c->pv2q, c->decayRatio, p->seed, p->job, c->qc,
+                           c->ftab);
+        const int nch = (N + 255) / 256;
+        ok = hipMalloc(&c->dFTab, 2 * sizeof(FastTab)) == hipSuccess &&
+             hipMalloc(&c->dPsi, (size_t)24 * S * sizeof(double)) == hipSuccess &&
+             hipMalloc(&c->dTp, (size_t)S * sizeof(double)) == hipSuccess &&
+             hipMalloc(&c->dFlags, sizeof(int)) == hipSuccess &&
+             hipMalloc(&c->dKdePart, (size_t)nch * 3 * TKDE_BINS * sizeof(double)) == hipSuccess &&
+             hipMalloc(&c->dKde, (size_t)3 * TKDE_BINS * sizeof(double)) == hipSuccess;
+        if (!ok) return fail_free(c, "mdmc_create: QT allocation failed");
+        ok = hipMemcpyAsync(c->dFTab, &c->ftab, sizeof(FastTab), hipMemcpyHostToDevice, c->st) == hipSuccess &&
+             hipMemcpyAsync(c->dFTab + 1, &c->ftab, sizeof(FastTab), hipMemcpyHostToDevice, c->st) == hipSuccess &&
+             hipMemsetAsync(c->dPsi, 0, (size_t)24 * S * sizeof(double), c->st) == hipSuccess &&
+             hipMemsetAsync(c->dTp, 0, (size_t)S * sizeof(double), c->st) == hipSuccess &&
+             hipMemsetAsync(c->dFlags, 0, sizeof(int), c->st) == hipSuccess &&
+             hipStreamSynchronize(c->st) == hipSuccess;
+        if (!ok) return fail_free(c, "mdmc_create: QT initialisation failed");
+    }
     *out = c;
     return 0;
 }
@@ -265,6 +328,14 @@ extern "C" double mdmc_get_const(const mdmc_ctx* c, const char* n) {
     if (!strcmp(n, "rCut")) return c->rCut;
     if (!strcmp(n, "nbins")) return c->nbins;
     if (!strcmp(n, "collisionFreq")) return c->collisionFreq;
+    if (c->qt) {
+        if (!strcmp(n, "plasmaToQuantumTimestepRatio")) return c->qtRatio;
+        if (!strcmp(n, "quantumTimestep")) return c->dtQ;
+        if (!strcmp(n, "gamToEinsteinFreq")) return c->gamToE;
+        if (!strcmp(n, "plasVelToQuantVel")) return c->pv2q;
+        if (!strcmp(n, "decayRatio")) return c->decayRatio;
+        if (!strcmp(n, "pumpMDTimeSteps")) return c->pumpSteps;
+    }
     return NAN;
 }
 
@@ -276,6 +347,7 @@ extern "C" int mdmc_init(mdmc_ctx* c) {
     const int N = c->N, S = c->S;
     const double L = c->L;
     std::vector<double> R((size_t)3 * S, 0.), V((size_t)3 * S, 0.);
+    std::vector<double> psi(c->qt ? (size_t)24 * S : 0, 0.);
     int N0 = 0;
     for (int i = 0; i < round(pow(N, 1. / 3)); i++)
         for (int j = 0; j < round(pow(N, 1. / 3)); j++)
@@ -287,6 +359,16 @@ extern "C" int mdmc_init(mdmc_ctx* c) {
                 V[N0] = c->vd(c->rng);                              // :193-195
                 V[S + N0] = c->vd(c->rng);
                 V[2 * S + N0] = c->vd(c->rng);
+                if (c->qt) {                                         // QTT:224-239: random S superposition
+                    const double rand1 = erand48(c->x48), rand2 = erand48(c->x48);
+                    const double rand3 = erand48(c->x48);
+                    const double sign = rand3 < 0.5 ? -1 : 1;
+                    const double rand4 = erand48(c->x48);
+                    const double sign2 = rand4 < 0.5 ? -1 : 1;
+                    psi[(size_t)0 * S + N0] = sqrt(rand1);                                    // re, state 0
+                    psi[(size_t)2 * S + N0] = sign2 * sqrt(1 - rand1) * sqrt(rand2);          // re, state 1
+                    psi[(size_t)3 * S + N0] = sign * sqrt(1 - rand1) * sqrt(1 - rand2);       // im, state 1
+                }
                 N0++;
             }
     if (N0 != N) return set_error("mdmc_init: N = %d is not a perfect cube (lattice init :182-201)", N);
@@ -295,6 +377,11 @@ extern "C" int mdmc_init(mdmc_ctx* c) {
     HIPCHK(hipMemcpyAsync(c->dV, V.data(), V.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemsetAsync(c->dA, 0, (size_t)3 * S * sizeof(double), c->st));
     HIPCHK(launch_particle_potentials(c->dR, N, S, L, c->p.kappa, c->rCut, c->dU, c->st));
+    if (c->qt) {
+        HIPCHK(hipMemcpyAsync(c->dPsi, psi.data(), psi.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
+        HIPCHK(hipMemsetAsync(c->dTp, 0, (size_t)S * sizeof(double), c->st));
+        c->qidx = 0;
+    }
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
@@ -576,13 +663,121 @@ extern "C" int mdmc_set_state(mdmc_ctx* c, const double* R, const double* V, con
     return 0;
 }
 
+// ---- QT tagging variants ----
+static int need_qt(const mdmc_ctx* c, const char* what) {
+    if (!c) return set_error("NULL context");
+    if (!c->qt) return set_error("%s: the context has no QT (qt_model 0)", what);
+    return 0;
+}
+
+// qstep() x n (QTT:555-756): the pumping model's fused QT substeps on this system's velocities
+// (no drift: the MD steps move the ions), in launches of up to MAXSUB substeps
+static int qsteps_async(mdmc_ctx* c, int n) {
+    while (n > 0) {
+        const int m = n < MAXSUB ? n : MAXSUB;
+        SubstepArgs a;
+        memset(&a, 0, sizeof a);
+        a.R = c->dR; a.V = c->dV; a.F = c->dA; a.Fpart = nullptr; a.nseg = 1;
+        a.psi = c->dPsi; a.tPart = c->dTp; a.oor = c->dFlags;
+        a.n = c->N; a.S = c->S; a.gid0 = 0; a.q0 = c->qidx;
+        a.nsub = m; a.do_step = 0; a.do_qt = 1; a.U = nullptr;
+        a.L = c->L;
+        a.qc = c->qc;
+        HIPCHK(launch_substeps_r(a, c->dFTab, 0, c->st));
+        c->qidx += (uint64_t)m;
+        n -= m;
+    }
+    return 0;
+}
+
+extern "C" int mdmc_qsteps(mdmc_ctx* c, int n) {
+    if (need_qt(c, "mdmc_qsteps")) return -1;
+    HIPCHK(hipSetDevice(c->dev));
+    if (qsteps_async(c, n)) return -1;
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+// tagParticles (QTT:1022-1067 / 422:992-1034): the spin-up measurement of include/mdqt.h's
+// k_tag_spin_up (Philox draws 6, 7 of the current qstep index); the tags drive the moments
+extern "C" int mdmc_tag_qt(mdmc_ctx* c, int* tags, int* n_up) {
+    if (need_qt(c, "mdmc_tag_qt")) return -1;
+    HIPCHK(hipSetDevice(c->dev));
+    const int N = c->N;
+    HIPCHK(launch_tag_spin_up(c->dPsi, N, c->S, 0, c->qidx, c->qc, c->dTags, c->st));
+    std::vector<int> h((size_t)N);
+    HIPCHK(hipMemcpyAsync(h.data(), c->dTags, (size_t)N * sizeof(int), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    int cnt = 0;
+    for (int i = 0; i < N; ++i) cnt += h[i];
+    if (tags) memcpy(tags, h.data(), (size_t)N * sizeof(int));
+    if (n_up) *n_up = cnt;
+    return 0;
+}
+
+// recordTaggedParticleMoments (QTT:1069-1138): moments from the device sums of tag set 0,
+// distributions from k_tagged_kde (queued; dist == NULL skips them)
+static int tagged_moments_qt_queue(mdmc_ctx* c, double* sums_dev, bool dist) {
+    HIPCHK(launch_tag_moments(c->dV, c->dTags, c->N, sums_dev, c->st));
+    if (dist) HIPCHK(launch_tagged_kde(c->dV, c->dTags, c->N, c->S, c->dKdePart, c->dKde, c->st));
+    return 0;
+}
+static void moments_qt_from_sums(const double* m, double* out4) {   // :1106-1109
+    const unsigned num = (unsigned)m[4];
+    out4[0] = m[0] / num; out4[1] = m[1] / num; out4[2] = m[2] / num; out4[3] = m[3] / num;
+}
+
+extern "C" int mdmc_tagged_moments_qt(mdmc_ctx* c, double out4[4], double* dist) {
+    if (need_qt(c, "mdmc_tagged_moments_qt")) return -1;
+    if (!out4) return set_error("mdmc_tagged_moments_qt: NULL argument");
+    HIPCHK(hipSetDevice(c->dev));
+    if (tagged_moments_qt_queue(c, c->dOut, dist != nullptr)) return -1;
+    double m[20];
+    HIPCHK(hipMemcpyAsync(m, c->dOut, sizeof m, hipMemcpyDeviceToHost, c->st));
+    if (dist) HIPCHK(hipMemcpyAsync(dist, c->dKde, (size_t)3 * TKDE_BINS * sizeof(double), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    moments_qt_from_sums(m, out4);
+    return 0;
+}
+
+extern "C" int mdmc_get_psi(mdmc_ctx* c, double* psi) {             // [N][12][2]
+    if (need_qt(c, "mdmc_get_psi")) return -1;
+    if (!psi) return set_error("mdmc_get_psi: NULL argument");
+    HIPCHK(hipSetDevice(c->dev));
+    const int N = c->N, S = c->S;
+    std::vector<double> h((size_t)24 * S);
+    HIPCHK(hipMemcpyAsync(h.data(), c->dPsi, h.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (int i = 0; i < N; ++i)
+        for (int k = 0; k < 24; ++k) psi[(size_t)24 * i + k] = h[(size_t)k * S + i];
+    return 0;
+}
+
+extern "C" int mdmc_set_psi(mdmc_ctx* c, const double* psi) {
+    if (need_qt(c, "mdmc_set_psi")) return -1;
+    if (!psi) return set_error("mdmc_set_psi: NULL argument");
+    HIPCHK(hipSetDevice(c->dev));
+    const int N = c->N, S = c->S;
+    std::vector<double> h((size_t)24 * S, 0.);
+    for (int i = 0; i < N; ++i)
+        for (int k = 0; k < 24; ++k) h[(size_t)k * S + i] = psi[(size_t)24 * i + k];
+    HIPCHK(hipMemcpyAsync(c->dPsi, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
 extern "C" int mdmc_setup_directories(mdmc_ctx* c) {            // main() :1037-1058
     if (!c) return set_error("NULL context");
     std::string d = c->p.saveDirectory;
     if (mkdir_p(d.c_str())) return -1;
     char nb[256];
-    snprintf(nb, sizeof nb, "Gamma%dKappa%dNumIons%d", (unsigned)(c->p.Gamma * 100), (unsigned)(c->p.kappa * 100),
-             (unsigned)(c->N));
+    if (c->qt)                                                     // QTT:1153
+        snprintf(nb, sizeof nb, "Gamma%dKappa%dNumIons%dPumpTime%dDet%dOm%dDensity%d", (unsigned)(c->p.Gamma * 100),
+                 (unsigned)(c->p.kappa * 100), (unsigned)(c->N), (unsigned)(1000000000. * c->p.tpumpreal),
+                 (unsigned)(100. * fabs(c->p.detuning)), (unsigned)(100. * c->p.Om), (unsigned)(10. * c->p.n));
+    else
+        snprintf(nb, sizeof nb, "Gamma%dKappa%dNumIons%d", (unsigned)(c->p.Gamma * 100), (unsigned)(c->p.kappa * 100),
+                 (unsigned)(c->N));
     d += nb;
     if (mkdir_p(d.c_str())) return -1;
     snprintf(nb, sizeof nb, "/job%d/", c->p.job);
@@ -646,9 +841,75 @@ static int write_autocorrelations(mdmc_ctx* c) {                // :682-691 and 
     return 0;
 }
 
+// main() of the QT tagging programs (QTT:1140-1254)
+static int run_qtt(mdmc_ctx* c, int verbose) {
+    const mdmc_params& p = c->p;
+    if (mdmc_setup_directories(c)) return -1;                    // :1143-1167
+    if (mdmc_init(c)) return -1;                                 // steps 1-2 :1192-1196
+    for (int k = 0; k < p.monteCarloSteps;) {                    // step 3 :1198-1209
+        if (k % 10000 == 0) {
+            if (write_pair_corr(c, k)) return -1;
+            if (verbose) printf("%d\n", k);
+        }
+        const int next = std::min(p.monteCarloSteps, (k / 10000 + 1) * 10000);
+        if (mdmc_monte_carlo(c, next - k, nullptr)) return -1;
+        k = next;
+    }
+    for (int k = 0; k < p.numPreRecordMDSteps; k++) {            // step 4 :1211-1220
+        if (verbose && k % 100 == 0) printf("%d\n", k);
+        if (md_step_async(c)) return -1;
+    }
+    c->collisionFreq = 0;                                        // step 5 :1222-1233
+    if (verbose) printf("pumpMDTimeSteps=%d\nquantumStepsPerMD=%d\n", c->pumpSteps, c->qtRatio);
+    for (int k = 0; k < c->pumpSteps; k++) {
+        if (qsteps_async(c, c->qtRatio)) return -1;
+        if (md_step_async(c)) return -1;
+    }
+    if (mdmc_tag_qt(c, nullptr, nullptr)) return -1;
+    const int T = c->T;                                          // step 6 :1235-1245
+    std::vector<double> m(20), dist((size_t)3 * TKDE_BINS);
+    FILE* fm = open_in(c, "taggedMoments.dat", "a");
+    FILE* ft = open_in(c, "temperature.dat", "a");
+    if (!fm || !ft) return set_error("cannot open taggedMoments.dat / temperature.dat in %s", c->saveDir.c_str());
+    for (int k = 0; k < T; k++) {
+        if (tagged_moments_qt_queue(c, c->dOut, true)) return -1;
+        HIPCHK(hipMemcpyAsync(m.data(), c->dOut, 20 * sizeof(double), hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipMemcpyAsync(dist.data(), c->dKde, dist.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        double mom[4];
+        moments_qt_from_sums(m.data(), mom);
+        fprintf(fm, "%lg\t%lg\t%lg\t%lg\t%lg\n", k * p.timeStep, mom[0], mom[1], mom[2], mom[3]);   // :1114
+        char name[64];
+        snprintf(name, sizeof name, "vel_distX_timestep%06d.dat", k);                                     // :1128-1136
+        FILE* fd = open_in(c, name, "w");
+        if (!fd) return set_error("cannot open %s%s", c->saveDir.c_str(), name);
+        for (int j = 0; j < TKDE_BINS; j++) fprintf(fd, "%lg\t%lg\n", (double)(j - 2000) * 0.0025, dist[j]);
+        fclose(fd);
+        if (k % 100 == 0) {
+            if (verbose) printf("%d\n", k);
+            if (write_pair_corr(c, k)) return -1;
+        }
+        double t4[4];
+        HIPCHK(launch_temperatures(c->dV, c->N, c->S, c->dOut, c->st));   // recordTemperature :771-792
+        HIPCHK(hipMemcpyAsync(t4, c->dOut, sizeof t4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        double tt[4];
+        temps_from_sums(c, t4, tt);
+        fprintf(ft, "%lg\n", tt[0]);
+        if (md_step_async(c)) return -1;
+        if (mdmc_record_velocities(c, k)) return -1;
+    }
+    fclose(fm);
+    fclose(ft);
+    if (write_autocorrelations(c)) return -1;                    // step 7 :1247-1251
+    if (verbose) fflush(stdout);
+    return 0;
+}
+
 // main() :1030-1167
 extern "C" int mdmc_run(mdmc_ctx* c, int verbose) {
     if (!c) return set_error("NULL context");
+    if (c->qt) return run_qtt(c, verbose);
     const mdmc_params& p = c->p;
     if (mdmc_setup_directories(c)) return -1;                    // :1037-1058
     if (mdmc_init(c)) return -1;                                 // step 1-2 :1062-1065

@@ -646,6 +646,51 @@ __global__ __launch_bounds__(256) void k_anisotropize(double* __restrict__ V, in
 }
 
 // ------------------------------------------------------------------------------------------
+// recordTaggedParticleMoments' distributions (QT tagging programs, QTT:1097-1124): bins
+// vel_j = (j - 2000) 0.0025, P_c[j] = sum over tagged ions of exp(-V2 (vel_j - v_c)^2),
+// V2 = 1/(2 0.002^2), / (6 sqrt(2 pi 0.002^2)).  Workgroup = 256 bins x one chunk of ions (LDS
+// staged, ascending); the chunk partials are summed in chunk order by k_tagged_kde_reduce.
+// ------------------------------------------------------------------------------------------
+constexpr int TKDE_CHUNK = 256;
+
+__global__ __launch_bounds__(256) void k_tagged_kde(const double* __restrict__ V, const int* __restrict__ tags, int N,
+                                                    int S, double* __restrict__ part) {
+    __shared__ double sv[3][TKDE_CHUNK];
+    __shared__ int st[TKDE_CHUNK];
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    const int i0 = blockIdx.y * TKDE_CHUNK;
+    const int i = i0 + threadIdx.x;
+    if (i < N) {
+        sv[0][threadIdx.x] = V[i]; sv[1][threadIdx.x] = V[S + i]; sv[2][threadIdx.x] = V[2 * S + i];
+        st[threadIdx.x] = tags[i];
+    } else {
+        st[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const double vel = (double)(j - 2000) * 0.0025;                 // QTT:250
+    const double V2 = 1. / (2. * 0.002 * 0.002);                   // QTT:1072
+    double p[3] = {0., 0., 0.};
+    const int m = min(TKDE_CHUNK, N - i0);
+    for (int k = 0; k < m; ++k) {
+        if (!st[k]) continue;                                      // uniform over the workgroup
+#pragma unroll
+        for (int c = 0; c < 3; ++c) p[c] += exp(-V2 * (vel - sv[c][k]) * (vel - sv[c][k]));   // :1100-1102
+    }
+    if (j < TKDE_BINS)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) part[((size_t)blockIdx.y * 3 + c) * TKDE_BINS + j] = p[c];
+}
+
+__global__ __launch_bounds__(256) void k_tagged_kde_reduce(const double* __restrict__ part, int nch,
+                                                           double* __restrict__ out) {
+    const int k = blockIdx.x * 256 + threadIdx.x;                  // c * TKDE_BINS + j
+    if (k >= 3 * TKDE_BINS) return;
+    double s = 0.;
+    for (int q = 0; q < nch; ++q) s = s + part[(size_t)q * 3 * TKDE_BINS + k];
+    out[k] = s / (6.0 * sqrt(2 * M_PI * 0.002 * 0.002));            // :1121-1123
+}
+
+// ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
 hipError_t launch_particle_potentials(const double* R, int N, int S, double L, double kappa, double rCut, double* U,
@@ -733,6 +778,15 @@ hipError_t launch_store_velocities(const double* V, int N, int S, int T, int t, 
 hipError_t launch_anisotropize(double* V, int N, int S, double tpd, hipStream_t s) {
     if (N <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_anisotropize, dim3((N + 255) / 256), dim3(256), 0, s, V, N, S, tpd);
+    return hipGetLastError();
+}
+
+// part must hold ceil(N / 256) x 3 x TKDE_BINS doubles, out 3 x TKDE_BINS
+hipError_t launch_tagged_kde(const double* V, const int* tags, int N, int S, double* part, double* out, hipStream_t s) {
+    if (N <= 0) return hipSuccess;
+    const int nch = (N + TKDE_CHUNK - 1) / TKDE_CHUNK;
+    hipLaunchKernelGGL(k_tagged_kde, dim3((TKDE_BINS + 255) / 256, nch), dim3(256), 0, s, V, tags, N, S, part);
+    hipLaunchKernelGGL(k_tagged_kde_reduce, dim3((3 * TKDE_BINS + 255) / 256), dim3(256), 0, s, part, nch, out);
     return hipGetLastError();
 }
 

@@ -430,6 +430,30 @@ static void build_constants(mdqt_ctx* s) {
     }
 }
 
+// QT constants and FastTab of a pumping model driven by another engine (the MC + MD tagging
+// programs, include/mdmc.h): the model's couplings, decay and jump rule (build_pump_tables)
+// with the caller's quantum time step, gamma and velocity conversion
+namespace mdqt {
+void build_pump_program(int model, double detuning, double Om, double dtQ, double gamToE, double pv2q,
+                        double decayRatio, uint32_t seed, uint32_t job, QTConst& q, FastTab& f) {
+    memset(&q, 0, sizeof q);
+    q.dtQ = dtQ; q.gamToE = gamToE;
+    q.h = dtQ * gamToE;
+    q.dtHalf = dtQ * gamToE / 2;
+    q.invh = 1. / (dtQ * gamToE);
+    q.pv2q = pv2q; q.r = decayRatio;
+    q.pD = decayRatio / (decayRatio + 1);
+    q.det = detuning;
+    q.model = model; q.seed = seed; q.job = job; q.renorm = 0;
+    mdqt_params p;
+    memset(&p, 0, sizeof p);
+    p.qt_model = model; p.detuning = detuning; p.Om = Om;
+    build_pump_tables(&p, q, f);
+    f.dt2 = (0.5 * dtQ) * (0.5 * dtQ);
+    for (int k = 0; k < 4; ++k) q.hdPh[k] = f.hdp[2 + k];
+}
+}  // namespace mdqt
+
 static double expDetuning_of(const mdqt_params* p, double t) {   // :447
     return 0.0126 * p->fracOfSig * p->Te * t /
            (sqrt(p->density) * p->sig0 * sqrt(1 + 0.00014314 * t * t * p->Te / (p->density * p->sig0 * p->sig0)));

@@ -271,6 +271,13 @@ hipError_t launch_anisotropize(double* V, int N, int S, double tpd, hipStream_t 
 hipError_t launch_store_velocities(const double* V, int N, int S, int T, int t, double* vs, hipStream_t s);
 // error message of the C ABI (mdqt_last_error), shared by the mdmc_* entry points
 int set_error(const char* fmt, ...);
+// pumping-model QT tables for another engine (mdqt_engine.cpp; used by the MC + MD tagging programs)
+void build_pump_program(int model, double detuning, double Om, double dtQ, double gamToE, double pv2q,
+                        double decayRatio, uint32_t seed, uint32_t job, QTConst& q, FastTab& f);
+// recordTaggedParticleMoments' velocity distribution of the tagged ions (QT tagging programs):
+// out[c][j] = sum over tagged i (ascending) of exp(-V2 (vel_j - V[c][i])^2), vel_j = (j - 2000) 0.0025
+constexpr int TKDE_BINS = 4001;
+hipError_t launch_tagged_kde(const double* V, const int* tags, int N, int S, double* part, double* out, hipStream_t s);
 
 // drand48 in the reference's order (SpeedUp:486, :575-687: ions in index order, 1 draw per
 // ion, 4-5 for a quantum jump): one workgroup assigns every ion its uniforms from the single

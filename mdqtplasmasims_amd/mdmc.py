@@ -13,10 +13,13 @@ import numpy as np
 from ._lib import MdmcParams, check, dptr, lib
 
 
-def default_params(**over) -> MdmcParams:
-    """MCMD:62-107 defaults, with keyword overrides."""
+def default_params(qt_model: int = 0, **over) -> MdmcParams:
+    """MCMD:62-107 defaults (qt_model 1..3: the QT tagging program's, QTT:75-121), with overrides."""
     p = MdmcParams()
-    lib().mdmc_default_params(C.byref(p))
+    if qt_model:
+        check(lib().mdmc_default_params_qt(C.byref(p), int(qt_model)), "mdmc_default_params_qt")
+    else:
+        lib().mdmc_default_params(C.byref(p))
     for k, v in over.items():
         if k == "saveDirectory":
             v = v.encode() if isinstance(v, str) else v
@@ -124,5 +127,31 @@ class MonteCarloMD:
         check(lib().mdmc_setup_directories(self._h), "mdmc_setup_directories")
         return lib().mdmc_save_directory(self._h).decode()
 
-    def run(self, verbose: bool = False):            # main() :1030-1167
+    def run(self, verbose: bool = False):            # main() :1030-1167 (QTT :1140-1254)
         check(lib().mdmc_run(self._h, int(bool(verbose))), "mdmc_run")
+
+    # ---- QT tagging variants (qt_model 1..3) ----
+    def qsteps(self, n: int):                        # qstep() x n (QTT:555-756)
+        check(lib().mdmc_qsteps(self._h, int(n)), "mdmc_qsteps")
+
+    def tag_qt(self):                                # tagParticles (QTT:1022-1067) -> (tags [N], count)
+        t = np.zeros(self.N, dtype=np.int32)
+        cnt = C.c_int(0)
+        check(lib().mdmc_tag_qt(self._h, t.ctypes.data_as(C.POINTER(C.c_int)), C.byref(cnt)), "mdmc_tag_qt")
+        return t, cnt.value
+
+    def tagged_moments_qt(self, dist: bool = True):  # recordTaggedParticleMoments (QTT:1069-1138)
+        out = np.zeros(4)
+        d = np.zeros((3, 4001)) if dist else None
+        check(lib().mdmc_tagged_moments_qt(self._h, dptr(out), dptr(d)), "mdmc_tagged_moments_qt")
+        return (out, d) if dist else out
+
+    def get_psi(self) -> np.ndarray:                 # [N][12] complex
+        a = np.zeros((self.N, 12, 2))
+        check(lib().mdmc_get_psi(self._h, dptr(a)), "mdmc_get_psi")
+        return a[..., 0] + 1j * a[..., 1]
+
+    def set_psi(self, psi):
+        psi = np.asarray(psi, dtype=complex)
+        a = np.ascontiguousarray(np.stack([psi.real, psi.imag], -1), dtype=np.float64)
+        check(lib().mdmc_set_psi(self._h, dptr(a)), "mdmc_set_psi")

@@ -320,6 +320,11 @@ int orc_init(orc_sim* s) {
 int orc_get_N(const orc_sim* s) { return s->N; }
 double orc_get_time(const orc_sim* s) { return s->t; }
 void orc_set_time(orc_sim* s, double t) { s->t = t; }
+/* the QT constants of another program driving the same qstep (the MC + MD tagging programs,
+   MonteCarloFollowedByQTTagging408Linear.cpp:115-121, 422Linear.cpp:115-121) */
+void orc_set_qt_constants(orc_sim* s, double dtQ, double gamToE, double pv2q, double r) {
+    s->dtQ = dtQ; s->gamToE = gamToE; s->plasVelToQuantVel = pv2q; s->r = r;
+}
 uint64_t orc_get_qstep_index(const orc_sim* s) { return s->qidx; }
 void orc_set_qstep_index(orc_sim* s, uint64_t q) { s->qidx = q; }
 void orc_set_drand48_state(orc_sim* s, uint64_t x) { s->x48 = x & 0xFFFFFFFFFFFFull; }

@@ -81,6 +81,7 @@ void   orc_get_state(const orc_sim* s, double* R, double* V, double* F, size_t l
 void   orc_set_forces(orc_sim* s, const double* F, size_t ld);
 double orc_get_time(const orc_sim* s);
 void   orc_set_time(orc_sim* s, double t);
+void   orc_set_qt_constants(orc_sim* s, double dtQ, double gamToE, double pv2q, double r);
 uint64_t orc_get_qstep_index(const orc_sim* s);
 void   orc_set_qstep_index(orc_sim* s, uint64_t q);
 void   orc_set_drand48_state(orc_sim* s, uint64_t x);

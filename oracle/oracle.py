@@ -101,6 +101,7 @@ def lib():
         L.orc_philox_uniform.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_int]
         L.orc_qstep_ion.argtypes = [C.c_void_p, C.c_double, _dp, _dp, _dp, _dp, C.POINTER(C.c_int)]
         L.orc_tag_spin_up.restype = C.c_int
+        L.orc_set_qt_constants.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_double, C.c_double]
         L.orc_tag_spin_up.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         _lib = L
     return _lib
@@ -241,6 +242,9 @@ class OracleSim:
     @property
     def save_directory(self) -> str:
         return lib().orc_save_directory(self.h).decode()
+
+    def set_qt_constants(self, dtQ, gamToE, pv2q, r):
+        lib().orc_set_qt_constants(self.h, dtQ, gamToE, pv2q, r)
 
     def qstep_ion(self, t, psi, vx, tPart, u):
         psi = np.ascontiguousarray(psi, dtype=np.float64).copy()

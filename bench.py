@@ -39,6 +39,8 @@ CONFIGS = {
     "c3": (dict(N0=100000, Ge=1.0 / 12), 0, "C3: N0=100000 MD-only, kappa=0.5"),
     "c4": (dict(N0=1000000, Ge=1.0 / 12), 0, "C4: N0=1000000 MD-only, kappa=0.5"),
     "c5": (dict(N0=250000, detuningDP=1.0), 1, "C5: N0=250000 full MDQT, detuningDP=+1"),
+    # BASELINE.json north_star: "particle-steps/sec at N=3 500 and N=1 000 000 with QT on"
+    "c1m": (dict(N0=1000000), 1, "N0=1000000 full MDQT (C2's laser parameters, density 2)"),
 }
 
 
@@ -50,7 +52,10 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--sharded-config", default="c5", choices=["none", "c3", "c5", "c4"])
+    ap.add_argument("--sharded-config", default="c5", choices=["none", "c3", "c5", "c4", "c1m"])
+    ap.add_argument("--million-config", default="c1m", choices=["none", "c1m", "c4"],
+                    help="the N=1M line of the metric (QT on), one system sharded over all ranks")
+    ap.add_argument("--million-steps", type=int, default=2)
     ap.add_argument("--sharded-steps", type=int, default=3)
     ap.add_argument("--qt-math", type=int, default=2, choices=[0, 1, 2],
                     help="0: the reference's exact QT operations, 1: FMA-contracted, 2: reassociated "
@@ -205,6 +210,10 @@ def main():
         sh = sharded_run(args.sharded_config, args.sharded_steps, rank, world, local, dist, barrier)
         if rank == 0:
             out["sharded"] = sh
+    if args.million_config != "none":
+        sh = sharded_run(args.million_config, args.million_steps, rank, world, local, dist, barrier)
+        if rank == 0:
+            out["sharded_1m"] = sh
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

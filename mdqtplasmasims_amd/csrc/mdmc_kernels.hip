@@ -248,7 +248,7 @@ __device__ __forceinline__ double mic_t(double d, double L, double T) {
 // pair energy u(r) of one separation (calcUIJ :153-159) with the reference's pair set: the exact
 // division-free minimum image and r2 as :292-293; the lattice start puts pairs exactly on the
 // cutoff, so FAST tests r2 < rc2 (= sqrt(r2) < rCut) and only then takes the value through
-// rsq + 2 Newton steps and exp_neg (a few ulp, no division or library call).  Otherwise the
+// rsq3 and exp_neg (a few ulp, no division or library call).  Otherwise the
 // reference's operations (sqrt, libm exp, division).
 __device__ __forceinline__ double mic_c(double d, double L, double T) {   // = mic_t, 4 operations
     return (fabs(d) >= T) ? d - copysign(L, d) : d;
@@ -260,10 +260,7 @@ __device__ __forceinline__ double mc_pair(double dx, double dy, double dz, const
     dz = mic_c(dz, a.L, a.micT);
     const double r2 = dx * dx + dy * dy + dz * dz;                    // :292-293
     if (FAST) {
-        double ri = __builtin_amdgcn_rsq(r2);
-        const double hr = 0.5 * r2;
-        ri = ri * fma(-hr * ri, ri, 1.5);
-        ri = ri * fma(-hr * ri, ri, 1.5);
+        const double ri = rsq3(r2);
         const double u = exp_neg(-a.kappa * (r2 * ri)) * ri;
         return r2 < a.rc2 ? u : 0.;                                    // = sqrt(r2) < rCut
     }

@@ -6,7 +6,7 @@
 //   k_reduce_segments        canonical sum of the partials when a caller asks for F
 //
 // VARIANT 0 keeps the reference's operations (sqrt, the three divisions, libm exp) without
-// contraction; VARIANT 1 (default) is the reciprocal form with a range-specialised exp and
+// contraction; VARIANT 1 (default) is the reciprocal form (rsq3) with a range-specialised exp and
 // FMA contraction — a few ulp per pair, inside the 1e-13 force gate.  VARIANT 2 (Newton-3
 // tiles; the MC + MD program, whose lattice start puts pairs exactly on the cutoff and on the
 // image boundary) has variant 1's values with variant 0's pair set: the exact minimum image and
@@ -72,10 +72,7 @@ __device__ __forceinline__ double pair_ft(double dx, double dy, double dz, const
         return (dr > 0 && dr < c.Rcut) ? ft : 0.;
     } else {
         const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
-        double ri = __builtin_amdgcn_rsq(r2);
-        const double hr = 0.5 * r2;
-        ri = ri * fma(-hr * ri, ri, 1.5);
-        ri = ri * fma(-hr * ri, ri, 1.5);
+        const double ri = rsq3(r2);
         const double dr = r2 * ri;
         const double ft = ((ri + c.invlDeb) * exp_neg(-dr * c.invlDeb)) * (ri * ri);
         if (VARIANT == 2)                        // the reference's pair set: r2 as :216, exact cutoff
@@ -93,10 +90,7 @@ __device__ __forceinline__ double pair_u(double dx, double dy, double dz, const 
         return (dr > 0 && dr < c.Rcut) ? u : 0.;
     } else {
         const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
-        double ri = __builtin_amdgcn_rsq(r2);
-        const double hr = 0.5 * r2;
-        ri = ri * fma(-hr * ri, ri, 1.5);
-        ri = ri * fma(-hr * ri, ri, 1.5);
+        const double ri = rsq3(r2);
         const double dr = r2 * ri;
         const double u = exp_neg(-dr * c.invlDeb) * ri;
         return (dr < c.Rcut) ? u : 0.;           // r2 = 0 gives dr = NaN: 0
@@ -207,9 +201,13 @@ __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi,
     ft *= m;
     const double px = dx * ft, py = dy * ft, pz = dz * ft;
     fx += px; fy += py; fz += pz;
+#if defined(MDQT_EXPT_NOJACC)
+    (void)ax; (void)ay; (void)az;
+#else
     __hip_atomic_fetch_add(&ax[idx], px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
 }
 
 template <int VARIANT, bool GUARD, bool RAGGED>
@@ -247,8 +245,17 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     const bool diag = I == J;
     if (!diag) {
         const int b = l + 16 * q;
+#if defined(MDQT_EXPT_2X)
 #pragma unroll
         for (int t = 0; t < 16; ++t) step(b + t, 1.);
+        const double xs = xi * 1.0000000001;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            n3_step<VARIANT, GUARD, RAGGED>(b + t, 1., xs, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+#else
+#pragma unroll
+        for (int t = 0; t < 16; ++t) step(b + t, 1.);
+#endif
     } else {
         const int b = l + 1 + 8 * q;
 #pragma unroll

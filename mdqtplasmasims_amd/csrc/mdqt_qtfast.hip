@@ -21,13 +21,7 @@
 
 namespace mdqt {
 
-__device__ __forceinline__ double rsq_nr(double x) {   // 1/sqrt(x): v_rsq_f64 + 2 Newton steps
-    double r = __builtin_amdgcn_rsq(x);
-    const double hx = 0.5 * x;
-    r = r * fma(-hx * r, r, 1.5);
-    r = r * fma(-hx * r, r, 1.5);
-    return r;
-}
+__device__ __forceinline__ double rsq_nr(double x) { return rsq3(x); }   // 1/sqrt(x), mdqt_internal.hpp
 __device__ __forceinline__ double nrm2(cxd y) { return fma(y.re, y.re, y.im * y.im); }
 __device__ __forceinline__ double rho_im_r(cxd a, cxd b) { return fma(a.im, b.re, -(a.re * b.im)); }
 

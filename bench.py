@@ -56,6 +56,13 @@ def parse():
     ap.add_argument("--million-config", default="c1m", choices=["none", "c1m", "c4"],
                     help="the N=1M line of the metric (QT on), one system sharded over all ranks")
     ap.add_argument("--million-steps", type=int, default=2)
+    ap.add_argument("--md-only-config", default="c3", choices=["none", "c1", "c3", "c4"],
+                    help="MD-only line (force-kernel FP64 roofline run; BASELINE configs[2] = C3)")
+    ap.add_argument("--no-e2e-line", action="store_true",
+                    help="skip the end-to-end line (reference cadence: output() every sampleFreq MD steps)")
+    ap.add_argument("--e2e-md-steps", type=int, default=400)
+    ap.add_argument("--secondary-deadline", type=float, default=420.0,
+                    help="seconds allowed for all secondary line items together")
     ap.add_argument("--sharded-steps", type=int, default=3)
     ap.add_argument("--qt-math", type=int, default=2, choices=[0, 1, 2],
                     help="0: the reference's exact QT operations, 1: FMA-contracted, 2: reassociated "
@@ -205,15 +212,24 @@ def main():
         if world == 1 and not args.no_mcmd_lines:
             out["mcmd"] = mcmd_line(local, cpu=not args.no_cpu_baseline)
     sim.close()
+    # The secondary line items below run after the headline number is final.  A watchdog on every
+    # rank bounds them: if one of them fails or does not finish in time, rank 0 prints the line
+    # with what it has (and the reason) and every rank leaves, so the headline is never lost.
+    out = out if rank == 0 else None
+    dog = Watchdog(args.secondary_deadline, rank, out)
+    if world == 1 and not args.no_e2e_line:
+        dog.run("end_to_end", lambda: end_to_end_line(local, args.config, args.e2e_md_steps))
+    if args.md_only_config != "none":
+        dog.run("md_only_" + args.md_only_config,
+                lambda: sharded_run(args.md_only_config, args.sharded_steps, rank, world, local, dist, barrier))
     # secondary line item: one large system sharded over all ranks (RCCL all-gather per MD step)
     if args.sharded_config != "none":
-        sh = sharded_run(args.sharded_config, args.sharded_steps, rank, world, local, dist, barrier)
-        if rank == 0:
-            out["sharded"] = sh
+        dog.run("sharded", lambda: sharded_run(args.sharded_config, args.sharded_steps, rank, world, local,
+                                               dist, barrier))
     if args.million_config != "none":
-        sh = sharded_run(args.million_config, args.million_steps, rank, world, local, dist, barrier)
-        if rank == 0:
-            out["sharded_1m"] = sh
+        dog.run("sharded_1m", lambda: sharded_run(args.million_config, args.million_steps, rank, world, local,
+                                                  dist, barrier))
+    dog.finish()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -335,6 +351,80 @@ def qtt_line(local, steps=10):
             "tagged_moments_and_distribution_ms": kde_ms, "cpu_baseline": None}
 
 
+class Watchdog:
+    """Bounds the secondary line items: exceptions are recorded in the line, and if the deadline
+    passes (e.g. a collective that never completes) rank 0 prints what it has and every rank exits."""
+
+    def __init__(self, seconds, rank, out):
+        import threading
+        self.rank, self.out, self.lock = rank, out, threading.Lock()
+        self.done = threading.Event()
+        self.current = None
+        self.t = threading.Thread(target=self._wait, args=(seconds,), daemon=True)
+        self.t.start()
+
+    def _wait(self, seconds):
+        if self.done.wait(seconds):
+            return
+        with self.lock:
+            if self.rank == 0:
+                self.out.setdefault("secondary_errors", {})[self.current or "?"] = \
+                    f"did not finish within {seconds:.0f} s (watchdog)"
+                print(json.dumps(self.out), flush=True)
+            sys.stdout.flush()
+            os._exit(0)
+
+    def run(self, name, fn):
+        self.current = name
+        try:
+            res = fn()
+        except Exception as e:                       # noqa: BLE001 - reported in the line
+            res, err = None, f"{type(e).__name__}: {e}"
+        else:
+            err = None
+        with self.lock:
+            if self.rank == 0:
+                if err is None:
+                    self.out[name] = res
+                else:
+                    self.out.setdefault("secondary_errors", {})[name] = err
+
+    def finish(self):
+        self.done.set()
+
+
+def end_to_end_line(local, cfg, md_steps):
+    """mdqt_run() (SpeedUp main() loop :1248-1383) with the reference cadence: output() every
+    sampleFreq = 40 MD steps (energies, KDE velocity distributions, state populations files),
+    writeConditions at the end, files written.  mdqt_run() starts with init() (newRun = 1), so the
+    rate is differential: two runs to different tmax, value = extra particle-qsteps / extra wall."""
+    import tempfile
+    import mdqtplasmasims_amd as M
+    params, qt, desc = CONFIGS[cfg]
+
+    def one(steps):
+        with tempfile.TemporaryDirectory() as d:
+            sim = M.Simulation(device=local, seed=12346, job=1, qt_enabled=qt, tmax=steps * 0.002,
+                               saveDirectory=d + "/", **params)    # one MD step = 0.002 (SpeedUp:79-85)
+            t0 = time.perf_counter()
+            sim.run()
+            sim.synchronize()
+            el = time.perf_counter() - t0
+            res = dict(N=sim.N, q=sim.qstep_index, c0=sim.counters()["c0"], wall=el,
+                       files=sum(len(fs) for _, _, fs in os.walk(d)))
+            sim.close()
+        return res
+
+    one(40)                                              # warm-up (module load, first allocations)
+    a, b = one(40), one(40 + md_steps)
+    el, dq = b["wall"] - a["wall"], b["q"] - a["q"]
+    return {"workload": desc + f", mdqt_run() with output() every 40 MD steps (files written): "
+                               f"run to {b['c0']} MD steps minus run to {a['c0']}",
+            "N": b["N"], "md_steps": b["c0"] - a["c0"], "qsteps": dq, "outputs": b["c0"] // 40 - a["c0"] // 40,
+            "files_long_run": b["files"], "wall_s": el, "wall_s_long_run_incl_init": b["wall"],
+            "value": b["N"] * dq / el, "unit": "particle-qsteps/s"}
+
+
 def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     """C5 (or C3/C4) as ONE system whose ions are sharded over the world: strong scaling."""
     import torch
@@ -352,11 +442,14 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     ratio = int(sim.const("plasmaToQuantumTimestepRatio"))
     sim.md_steps(1)
     barrier()
+    sim.enable_timing(1)
     t0 = time.perf_counter()
     sim.md_steps(steps)
     sim.synchronize()
     barrier()
     el = time.perf_counter() - t0
+    f_ms, nf, s_ms, ns = sim.kernel_time_totals()
+    sim.enable_timing(False)
     tt = torch.tensor([el], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -364,12 +457,19 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     N = sim.N
     sim.close()
     unit_steps = ratio if qt else 1
+    f_avg = f_ms / max(nf, 1) * 1e-3
+    pairs = N * (N - 1) / 2.0
+    force = {"avg_ms": f_avg * 1e3, "launches": nf, "pairs_per_s": pairs / f_avg if f_avg else None,
+             "fp64_tflops": W_F_PER_PAIR * pairs / f_avg / 1e12 if f_avg else None,
+             "fp64_frac": W_F_PER_PAIR * pairs / f_avg / 1e12 / FP64_PEAK_TFS if f_avg else None,
+             "note": "this rank's forces() incl. all-gather/reduce-scatter; flops = 30 x N(N-1)/2 (SURVEY 8d)"}
     return {"workload": desc + ", one system sharded over all ranks (RCCL position all-gather; "
                            "Newton-3 block-pair forces reduce-scattered)",
             "N": N, "n_gpus": world, "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
-            "scaling": "strong", "init_s": t_init}
+            "scaling": "strong", "init_s": t_init, "force": force,
+            "substeps_ms_per_md_step": s_ms / max(ns, 1) if ns else None}
 
 
 if __name__ == "__main__":

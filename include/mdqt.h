@@ -134,6 +134,11 @@ int         mdqt_output(mdqt_ctx* c);                        /* output(),  Speed
 int         mdqt_write_conditions(mdqt_ctx* c, int c0);      /* writeConditions, :725-784       */
 int         mdqt_read_conditions(mdqt_ctx* c, int c0);       /* readConditions,  :785-916       */
 int         mdqt_run(mdqt_ctx* c);                           /* main() time loop, :1139-1383    */
+/* Output files are formatted ("%lg", byte-identical to fprintf) and written by background threads
+ * of the context.  mdqt_output / mdqt_write_conditions / mdqt_run return after their files are on
+ * disk (inside mdqt_run the per-output files are written while the loop goes on, joined at the
+ * end); mdqt_flush_files waits for any still in flight and reports the first I/O error. */
+int         mdqt_flush_files(mdqt_ctx* c);
 /* optical-pumping models: tag every ion spin-up with probability |<up|psi>|^2 —
  * measureSpinUps (randomFrozenStartTag408Linear.cpp:600, randomFrozenStartTag422Linear.cpp:568)
  * = tagParticles (MonteCarloFollowedByQTTagging408Linear.cpp:1022).  tags: [N] (may be NULL;

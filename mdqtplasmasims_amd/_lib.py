@@ -119,6 +119,7 @@ SIGNATURES = [
     ("mdqt_write_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_read_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_run", C.c_int, [C.c_void_p]),
+    ("mdqt_flush_files", C.c_int, [C.c_void_p]),
     ("mdqt_tag_spin_up", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("mdqt_set_option", C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     ("mdqt_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),

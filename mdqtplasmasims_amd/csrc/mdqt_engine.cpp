@@ -15,12 +15,14 @@
 
 #include <string>
 #include <algorithm>
+#include <memory>
 #include <vector>
 
 #include <rccl/rccl.h>
 
 #include "../../include/mdqt.h"
 #include "mdqt_internal.hpp"
+#include "mdqt_writer.hpp"
 
 using namespace mdqt;
 
@@ -126,6 +128,7 @@ struct mdqt_ctx {
     uint64_t x48 = 0;
     std::vector<double> Vholder;   // [13][3][N] VZERO_* files (SpeedUp:752-763, :898-913)
     char saveDirectory[1024];
+    std::unique_ptr<FileWriter> writer;   // background formatting/writing of the output files
     // timing
     // per-launch HIP events of the hot kernels (kind 0 = force, 1 = substeps), recorded on
     // the launch stream while timing is on; summed by mdqt_kernel_time_totals
@@ -685,6 +688,7 @@ extern "C" int mdqt_create(const mdqt_params* p, mdqt_ctx** out) {
 
 extern "C" void mdqt_destroy(mdqt_ctx* s) {
     if (!s) return;
+    s->writer.reset();                                   // joins the file writers
     (void)hipSetDevice(s->dev);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     free_device(s);
@@ -1313,53 +1317,82 @@ extern "C" int mdqt_setup_directories(mdqt_ctx* s) {       // SpeedUp:1145-1160
     return 0;
 }
 
-extern "C" int mdqt_output(mdqt_ctx* s) {                 // output(), SpeedUp:917-1032
+static FileWriter& writer_of(mdqt_ctx* s) {
+    if (!s->writer) s->writer.reset(new FileWriter(4));
+    return *s->writer;
+}
+
+static std::string path_in(const mdqt_ctx* s, const char* name) { return std::string(s->saveDirectory) + name; }
+
+// wait for the background writers; reports the first file error
+static int flush_files(mdqt_ctx* s) {
+    if (!s->writer) return 0;
+    std::string e;
+    if (s->writer->flush(&e)) return fail("%s", e.c_str());
+    return 0;
+}
+
+// output(), SpeedUp:917-1032.  The observables are computed on the device and snapshotted here;
+// the files are formatted by the background writers (the caller flushes: mdqt_output at once,
+// mdqt_run at the end of the run).
+static int output_async(mdqt_ctx* s) {
     const int N = s->N;
     double o[7];
-    std::vector<double> P((size_t)3 * NBINS), pops((size_t)3 * (N > 0 ? N : 1)), V((size_t)3 * (N > 0 ? N : 1));
-    if (mdqt_observables(s, o, P.data(), pops.data())) return -1;
-    std::fill(V.begin(), V.end(), 0.);
-    if (mdqt_get_state(s, nullptr, V.data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
-    if (mdqt_allreduce_sum(s, V.data(), (size_t)N)) return -1;      // vx column, zero-padded gather
+    auto P = std::make_shared<std::vector<double>>((size_t)3 * NBINS);
+    auto pops = std::make_shared<std::vector<double>>((size_t)3 * (N > 0 ? N : 1));
+    auto V = std::make_shared<std::vector<double>>((size_t)3 * (N > 0 ? N : 1), 0.);
+    if (mdqt_observables(s, o, P->data(), pops->data())) return -1;
+    if (mdqt_get_state(s, nullptr, V->data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
+    if (mdqt_allreduce_sum(s, V->data(), (size_t)N)) return -1;      // vx column, zero-padded gather
     if (s->p.rank != 0) { s->counter++; return 0; }                 // files are rank 0's
-    FILE* fa = open_in(s, "energies.dat", "a");
+    FILE* fa = open_in(s, "energies.dat", "a");                      // appended in order: here
     if (!fa) return -1;
     fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\t%lg\n", o[0], o[1], o[2], o[3], o[4], o[5], o[6]);   // :954
     fclose(fa);
-    char b1[64], b2[64], b3[64];
-    snprintf(b1, sizeof b1, "vel_distX_time%06d.dat", s->counter);
-    snprintf(b2, sizeof b2, "vel_distY_time%06d.dat", s->counter);
-    snprintf(b3, sizeof b3, "vel_distZ_time%06d.dat", s->counter);
-    FILE *f1 = open_in(s, b1, "w"), *f2 = open_in(s, b2, "w"), *f3 = open_in(s, b3, "w");
-    if (!f1 || !f2 || !f3) {
-        if (f1) fclose(f1);
-        if (f2) fclose(f2);
-        if (f3) fclose(f3);
-        return -1;
+    FileWriter& w = writer_of(s);
+    const double* vel = s->vel;                                      // constant bin centres
+    const char* axes[3] = {"X", "Y", "Z"};
+    for (int a = 0; a < 3; ++a) {                                                        // :983-1006
+        char b[64];
+        snprintf(b, sizeof b, "vel_dist%s_time%06d.dat", axes[a], s->counter);
+        const double shift = a == 0 ? o[6] : 0.;
+        w.submit(path_in(s, b), "w", [P, vel, a, shift](LgText& t) {
+            const double* p = P->data() + (size_t)a * NBINS;
+            for (int i = 0; i < NBINS; i++) {
+                t.num(vel[i] + shift); t.ch('\t'); t.num(p[i]); t.ch('\n');
+            }
+        });
     }
-    for (int i = 0; i < NBINS; i++) {                                                    // :983-1006
-        fprintf(f1, "%lg\t%lg\n", s->vel[i] + o[6], P[i]);
-        fprintf(f2, "%lg\t%lg\n", s->vel[i], P[NBINS + i]);
-        fprintf(f3, "%lg\t%lg\n", s->vel[i], P[2 * NBINS + i]);
-    }
-    fclose(f1); fclose(f2); fclose(f3);
-    snprintf(b1, sizeof b1, "statePopulationsVsVTime%06d.dat", s->counter);
-    fa = open_in(s, b1, "w");
-    if (!fa) return -1;
-    for (int i = 0; i < N; i++)                                                          // :1010-1024
-        fprintf(fa, "%lg\t%lg\t%lg\t%lg\n", V[i], pops[3 * i], pops[3 * i + 1], pops[3 * i + 2]);
-    fclose(fa);
+    char b[64];
+    snprintf(b, sizeof b, "statePopulationsVsVTime%06d.dat", s->counter);
+    w.submit(path_in(s, b), "w", [V, pops, N](LgText& t) {                              // :1010-1024
+        const double *v = V->data(), *q = pops->data();
+        for (int i = 0; i < N; i++) {
+            t.num(v[i]); t.ch('\t'); t.num(q[3 * i]); t.ch('\t'); t.num(q[3 * i + 1]); t.ch('\t');
+            t.num(q[3 * i + 2]); t.ch('\n');
+        }
+    });
     s->counter++;                                                                        // :1027
     return 0;
 }
 
-extern "C" int mdqt_write_conditions(mdqt_ctx* s, int c0) {   // writeConditions, :725-784
+extern "C" int mdqt_output(mdqt_ctx* s) {                 // output(), SpeedUp:917-1032
+    if (!s) return fail("NULL context");
+    if (output_async(s)) return -1;
+    return flush_files(s);
+}
+
+// writeConditions, SpeedUp:725-784 (files formatted by the background writers)
+static int write_conditions_async(mdqt_ctx* s, int c0) {
     const int N = s->N;
-    std::vector<double> R((size_t)3 * (N > 0 ? N : 1), 0.), V(R.size(), 0.), psi((size_t)24 * (N > 0 ? N : 1), 0.);
+    const size_t n1 = (size_t)(N > 0 ? N : 1);
+    auto R = std::make_shared<std::vector<double>>(3 * n1, 0.);
+    auto V = std::make_shared<std::vector<double>>(3 * n1, 0.);
+    auto psi = std::make_shared<std::vector<double>>(24 * n1, 0.);
     if (mdqt_allgather_positions(s)) return -1;           // collective when sharded
-    if (mdqt_get_state(s, R.data(), V.data(), nullptr, N, psi.data(), nullptr, nullptr)) return -1;
-    if (mdqt_allreduce_sum(s, V.data(), V.size())) return -1;
-    if (mdqt_allreduce_sum(s, psi.data(), psi.size())) return -1;
+    if (mdqt_get_state(s, R->data(), V->data(), nullptr, N, psi->data(), nullptr, nullptr)) return -1;
+    if (mdqt_allreduce_sum(s, V->data(), V->size())) return -1;
+    if (mdqt_allreduce_sum(s, psi->data(), psi->size())) return -1;
     if (s->p.rank != 0) return 0;
     char b[96];
     snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
@@ -1367,34 +1400,52 @@ extern "C" int mdqt_write_conditions(mdqt_ctx* s, int c0) {   // writeConditions
     if (!fa) return -1;
     fprintf(fa, "%i\t%i", N, s->counter);                                                // :737
     fclose(fa);
+    FileWriter& w = writer_of(s);
     snprintf(b, sizeof b, "conditions_timestep%06d.dat", c0);
-    fa = open_in(s, b, "w");
-    if (!fa) return -1;
-    for (int i = 0; i < N; i++)                                                          // :747
-        fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\t\n", R[i], R[(size_t)N + i], R[(size_t)2 * N + i], V[i],
-                V[(size_t)N + i], V[(size_t)2 * N + i]);
-    fclose(fa);
+    w.submit(path_in(s, b), "w", [R, V, N](LgText& t) {                                 // :747
+        const double *r = R->data(), *v = V->data();
+        for (int i = 0; i < N; i++) {
+            for (int k = 0; k < 3; ++k) { t.num(r[(size_t)k * N + i]); t.ch('\t'); }
+            for (int k = 0; k < 3; ++k) { t.num(v[(size_t)k * N + i]); t.ch('\t'); }
+            t.ch('\n');
+        }
+    });
+    auto vholder = std::make_shared<std::vector<double>>(s->Vholder);
     for (int v = 0; v < NINTERVALV; v++) {                                              // :752-763
         snprintf(b, sizeof b, "VZERO_timestep%06d_interval%d.dat", c0, v);
-        fa = open_in(s, b, "w");
-        if (!fa) return -1;
-        const double* vh = s->Vholder.data() + (size_t)v * 3 * N;
-        for (int i = 0; i < N; i++) fprintf(fa, "%lg\t%lg\t%lg\n", vh[i], vh[(size_t)N + i], vh[(size_t)2 * N + i]);
-        fclose(fa);
+        w.submit(path_in(s, b), "w", [vholder, v, N](LgText& t) {
+            const double* vh = vholder->data() + (size_t)v * 3 * N;
+            for (int i = 0; i < N; i++) {
+                t.num(vh[i]); t.ch('\t'); t.num(vh[(size_t)N + i]); t.ch('\t'); t.num(vh[(size_t)2 * N + i]);
+                t.ch('\n');
+            }
+        });
     }
     snprintf(b, sizeof b, "wvFns_timestep%06d.dat", c0);
-    fa = open_in(s, b, "w");
-    if (!fa) return -1;
-    for (int j = 0; j < N; j++) {                                                        // :777-779
-        const double* ps = psi.data() + (size_t)24 * j;
-        for (int k = 0; k < NS; k++) fprintf(fa, "%lg\t%lg\t", ps[2 * k], ps[2 * k + 1]);
-        fprintf(fa, "\n");
-    }
-    fclose(fa);
+    w.submit(path_in(s, b), "w", [psi, N](LgText& t) {                                  // :777-779
+        for (int j = 0; j < N; j++) {
+            const double* ps = psi->data() + (size_t)24 * j;
+            for (int k = 0; k < NS; k++) { t.num(ps[2 * k]); t.ch('\t'); t.num(ps[2 * k + 1]); t.ch('\t'); }
+            t.ch('\n');
+        }
+    });
     return 0;
 }
 
+extern "C" int mdqt_write_conditions(mdqt_ctx* s, int c0) {   // writeConditions, :725-784
+    if (!s) return fail("NULL context");
+    if (write_conditions_async(s, c0)) return -1;
+    return flush_files(s);
+}
+
+extern "C" int mdqt_flush_files(mdqt_ctx* s) {
+    if (!s) return fail("NULL context");
+    return flush_files(s);
+}
+
 extern "C" int mdqt_read_conditions(mdqt_ctx* s, int c0) {    // readConditions, :785-916
+    if (!s) return fail("NULL context");
+    if (flush_files(s)) return -1;                       // the files may still be being written
     s->t = ((double)c0 - 9.) * TIMESTEP + 0.02;                                         // :789
     char b[96];
     snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
@@ -1468,7 +1519,7 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
     int tsc = ratio;                                                                    // :1235
     while (s->t <= tend) {                                                              // :1248
         if ((s->c0 + 1) % sf == 0 && tsc == 1)                                          // :1365
-            if (mdqt_output(s)) return -1;
+            if (output_async(s)) return -1;             // files formatted while the loop goes on
         if (tsc == ratio) {                                                             // :1369
             if (mdqt_allgather_positions(s)) return -1;                                 // §8e
             if (mdqt_forces(s)) return -1;
@@ -1484,7 +1535,7 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
         if (mdqt_substeps(s, n)) return -1;                                            // :1376-1377
         tsc += n;
     }
-    return mdqt_write_conditions(s, s->c0);                                            // :1381
+    return mdqt_write_conditions(s, s->c0);             // :1381; also joins the writers
 }
 
 // ---------------------------------------------------------------------------------------------

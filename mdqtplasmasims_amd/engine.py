@@ -250,6 +250,10 @@ class Simulation:
     def run(self):
         check(lib().mdqt_run(self.h), "run")
 
+    def flush_files(self):
+        """wait for the background file writers (mdqt_flush_files)"""
+        check(lib().mdqt_flush_files(self.h), "flush_files")
+
     def set_option(self, name: str, value: int):
         check(lib().mdqt_set_option(self.h, name.encode(), int(value)), "set_option")
 

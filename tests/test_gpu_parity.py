@@ -498,6 +498,30 @@ def test_run_writes_reference_layout(eng, orc, tmp_path):
         assert np.allclose(xa, xb, rtol=2e-5, atol=1e-9 * max(1.0, np.abs(xb).max())), f
 
 
+def test_run_files_are_lg_of_the_final_state(eng, tmp_path):
+    """mdqt_run's files come from the background writers (mdqt_writer.hpp): byte for byte the
+    "%lg" text of the state the run ends with (SpeedUp:747, :777-779)."""
+    kw = dict(N0=300, tmax=0.1, sampleFreq=10, seed=21, job=2, rng_mode=1)
+    s = eng.Simulation(saveDirectory=str(tmp_path) + "/", **kw)
+    s.run()
+    s.flush_files()
+    st = s.get_state()
+    c0 = s.counters()["c0"]
+    R, V, psi = st["R"], st["V"], st["psi"]
+    N = s.N
+    d = s.save_directory
+    want = "".join("".join("%g\t" % R[k, i] for k in range(3)) + "".join("%g\t" % V[k, i] for k in range(3)) + "\n"
+                   for i in range(N))
+    assert open(os.path.join(d, "conditions_timestep%06d.dat" % c0)).read() == want
+    P = psi.reshape(N, -1)
+    want = "".join("".join("%g\t" % v for v in P[i]) + "\n" for i in range(N))
+    assert open(os.path.join(d, "wvFns_timestep%06d.dat" % c0)).read() == want
+    assert open(os.path.join(d, "ions_timestep%06d.dat" % c0)).read() == "%d\t%d" % (N, s.counters()["counter"])
+    # one velocity distribution per output, each 2001 rows
+    for n in range(s.counters()["counter"]):
+        assert len(open(os.path.join(d, "vel_distZ_time%06d.dat" % n)).read().splitlines()) == 2001
+
+
 def test_resume_roundtrip(eng, tmp_path):
     kw = dict(N0=60, tmax=0.05, sampleFreq=1000, seed=5, job=1, saveDirectory=str(tmp_path) + "/")
     s = eng.Simulation(**kw)

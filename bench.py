@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-e2e-line", action="store_true",
                     help="skip the end-to-end line (reference cadence: output() every sampleFreq MD steps)")
     ap.add_argument("--e2e-md-steps", type=int, default=400)
+    ap.add_argument("--no-replicas-line", action="store_true",
+                    help="skip the jobs-per-GPU line (k independent C2 jobs sharing one GPU)")
     ap.add_argument("--secondary-deadline", type=float, default=420.0,
                     help="seconds allowed for all secondary line items together")
     ap.add_argument("--sharded-steps", type=int, default=3)
@@ -217,6 +219,8 @@ def main():
     # with what it has (and the reason) and every rank leaves, so the headline is never lost.
     out = out if rank == 0 else None
     dog = Watchdog(args.secondary_deadline, rank, out)
+    if not args.no_replicas_line:
+        dog.run("jobs_per_gpu", lambda: replicas_line(local, args.config))
     if world == 1 and not args.no_e2e_line:
         dog.run("end_to_end", lambda: end_to_end_line(local, args.config, args.e2e_md_steps))
     if args.md_only_config != "none":
@@ -391,6 +395,40 @@ class Watchdog:
 
     def finish(self):
         self.done.set()
+
+
+def replicas_line(local, cfg, counts=(2, 4, 8), steps=100):
+    """The reference's production pattern is an array of independent jobs (exampleSlurmFile.slurm:3,
+    job = 1..8).  Here k of them share ONE MI355X, each context on its own HIP stream, MD steps
+    issued round-robin from one host thread: one system's latency-bound QT launch overlaps another's
+    force launch.  value = sum over jobs of N x qsteps / wall.  A capacity figure for the
+    job-array workload, not the single-system headline."""
+    import mdqtplasmasims_amd as M
+    params, qt, desc = CONFIGS[cfg]
+    res = []
+    for k in counts:
+        sims = [M.Simulation(device=local, seed=12345 + j, job=j, qt_enabled=qt, **params).init()
+                for j in range(1, k + 1)]
+        ratio = int(sims[0].const("plasmaToQuantumTimestepRatio"))
+        for _ in range(5):
+            for x in sims:
+                x.md_steps(1)
+        for x in sims:
+            x.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            for x in sims:
+                x.md_steps(1)
+        for x in sims:
+            x.synchronize()
+        el = time.perf_counter() - t0
+        ntot = sum(x.N for x in sims)
+        for x in sims:
+            x.close()
+        res.append({"jobs": k, "N_total": ntot, "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
+                    "value": ntot * ratio * steps / el, "unit": "particle-qsteps/s"})
+    return {"workload": desc + ": k independent jobs (seed 12345+job) on one GPU, one stream each",
+            "lines": res}
 
 
 def end_to_end_line(local, cfg, md_steps):

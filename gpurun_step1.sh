@@ -9,8 +9,8 @@ echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 10 > gpurun_out/bench.log 2>&1 || exit $?
-timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --sharded-config none --million-config none --qt-math 0 --no-pump-lines --no-mcmd-lines > gpurun_out/bench_exact.log 2>&1 || exit $?
+timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --sharded-config none --million-config none --qt-math 0 --no-pump-lines --no-mcmd-lines --md-only-config none --no-e2e-line --no-replicas-line > gpurun_out/bench_exact.log 2>&1 || exit $?
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof1" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline --sharded-config none --million-config none --no-pump-lines --no-mcmd-lines > "$GRAFT_REPO_ROOT/gpurun_out/prof1.log" 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_c5" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --sharded-config c5 --sharded-steps 2 --million-config none --no-pump-lines --no-mcmd-lines > "$GRAFT_REPO_ROOT/gpurun_out/prof_c5.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof1" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline --sharded-config none --million-config none --no-pump-lines --no-mcmd-lines --md-only-config none --no-e2e-line --no-replicas-line > "$GRAFT_REPO_ROOT/gpurun_out/prof1.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_c5" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --sharded-config c5 --sharded-steps 2 --million-config none --no-pump-lines --no-mcmd-lines --md-only-config none --no-e2e-line --no-replicas-line > "$GRAFT_REPO_ROOT/gpurun_out/prof_c5.log" 2>&1
 echo "prof rc=$?" >> "$GRAFT_REPO_ROOT/gpurun_out/prof1.log"

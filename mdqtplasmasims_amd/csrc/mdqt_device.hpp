@@ -1,6 +1,7 @@
 // Device helpers shared by the gfx950 QT kernels (mdqt_kernels.hip, mdqt_qtfast.hip):
 // Philox stream, complex helpers, the QT arithmetic modes, sincos, DPP/LDS lane moves.
 #pragma once
+
 #include "mdqt_internal.hpp"
 
 #include <math.h>

@@ -979,12 +979,28 @@ static int mark(mdqt_ctx* s, int k) {
     return 0;
 }
 
+// a start/stop pair from the pool of kind k, for a launch that records them itself
+static int take_events(mdqt_ctx* s, int k, hipEvent_t* e0, hipEvent_t* e1) {
+    auto& pool = s->evpool[k];
+    while ((int)pool.size() < s->evused[k] + 2) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        pool.push_back(e);
+    }
+    *e0 = pool[s->evused[k]++];
+    *e1 = pool[s->evused[k]++];
+    return 0;
+}
+
 extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:192-236
     if (!s) return fail("NULL context");
     if (s->nloc == 0) return 0;
     HIPCHK(hipSetDevice(s->dev));
     const bool tm = s->timing && (s->tcount[0]++ % s->tperiod == 0);
-    if (tm && mark(s, 0)) return -1;
+    // timing: the Newton-3 tile kernel (one launch) records its own timestamps; the other
+    // schemes (several kernels, collectives) are bracketed by events on the stream
+    const bool tm_marks = tm && !s->use_n3;
+    if (tm_marks && mark(s, 0)) return -1;
     if (s->use_n3) {
         N3Args a;
         a.R = s->dR; a.P = s->dFpart; a.pairs = s->dPairs;
@@ -993,7 +1009,9 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
         a.micGuard = c.micGuard;
         a.guard = c.guard;
-        HIPCHK(launch_forces_n3(a, s->force_variant, s->stream));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (tm && take_events(s, 0, &e0, &e1)) return -1;
+        HIPCHK(launch_forces_n3(a, s->force_variant, s->stream, e0, e1));
         s->f_pending = true;       // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots;
     } else if (s->use_n3b) {
@@ -1021,7 +1039,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         s->f_pending = true;       // summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nseg;
     }
-    if (tm && mark(s, 0)) return -1;
+    if (tm_marks && mark(s, 0)) return -1;
     return 0;
 }
 
@@ -1061,10 +1079,10 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             a.U = s->dU;
         }
         const bool tm = s->timing && (s->tcount[1]++ % s->tperiod == 0);
-        if (tm && mark(s, 1)) return -1;
-        if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->substep_mode, s->stream));
-        else HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream));
-        if (tm && mark(s, 1)) return -1;
+        hipEvent_t e0 = nullptr, e1 = nullptr;       // timing: the kernel's own timestamps
+        if (tm && (take_events(s, 1, &e0, &e1))) return -1;
+        if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->substep_mode, s->stream, e0, e1));
+        else HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream, e0, e1));
         if (advance_t) {
             s->t = t;
             s->qidx += (uint64_t)m;

@@ -210,6 +210,20 @@ __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi,
 #endif
 }
 
+#ifndef MDQT_N3_WAVES
+#define MDQT_N3_WAVES 4
+#endif
+constexpr int N3W = MDQT_N3_WAVES;                  // waves per tile pair (2, 4 or 8)
+static_assert(N3W == 2 || N3W == 4 || N3W == 8, "waves per tile pair");
+
+// the j accumulators of the N3W waves, both halves of each, combined in wave order
+__device__ __forceinline__ double n3_jsum(const double (*accj)[3][128], int k, int l) {
+    double w = accj[0][k][l] + accj[0][k][l + 64];
+#pragma unroll
+    for (int q = 1; q < N3W; ++q) w += accj[q][k][l] + accj[q][k][l + 64];
+    return w;
+}
+
 template <int VARIANT, bool GUARD, bool RAGGED>
 __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
@@ -244,23 +258,14 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     };
     const bool diag = I == J;
     if (!diag) {
-        const int b = l + 16 * q;
-#if defined(MDQT_EXPT_2X)
+        const int b = l + (64 / N3W) * q;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) step(b + t, 1.);
-        const double xs = xi * 1.0000000001;
-#pragma unroll
-        for (int t = 0; t < 16; ++t)
-            n3_step<VARIANT, GUARD, RAGGED>(b + t, 1., xs, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
-#else
-#pragma unroll
-        for (int t = 0; t < 16; ++t) step(b + t, 1.);
-#endif
+        for (int t = 0; t < 64 / N3W; ++t) step(b + t, 1.);
     } else {
-        const int b = l + 1 + 8 * q;
+        const int b = l + 1 + (32 / N3W) * q;
 #pragma unroll
-        for (int t = 0; t < 7; ++t) step(b + t, 1.);
-        step(b + 7, (q == 3 && l >= 32) ? 0. : 1.);  // lane distance 32: once per pair
+        for (int t = 0; t < 32 / N3W - 1; ++t) step(b + t, 1.);
+        step(b + 32 / N3W - 1, (q == N3W - 1 && l >= 32) ? 0. : 1.);  // lane distance 32: once per pair
     }
     ia[q][0][l] = fx; ia[q][1][l] = fy; ia[q][2][l] = fz;
     __syncthreads();
@@ -269,12 +274,10 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         double* Pi = a.P + (size_t)J * slab3;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            double v = ((ia[0][k][l] + ia[1][k][l]) + ia[2][k][l]) + ia[3][k][l];
-            if (diag) {
-                const double w = (((accj[0][k][l] + accj[0][k][l + 64]) + (accj[1][k][l] + accj[1][k][l + 64])) +
-                                  (accj[2][k][l] + accj[2][k][l + 64])) + (accj[3][k][l] + accj[3][k][l + 64]);
-                v = v - w;
-            }
+            double v = ia[0][k][l];
+#pragma unroll
+            for (int w = 1; w < N3W; ++w) v += ia[w][k][l];
+            if (diag) v = v - n3_jsum(accj, k, l);
             if (i < S) Pi[(size_t)k * S + i] = v;
         }
     } else if (q == 1 && !diag) {                   // rows of J -> slot I
@@ -282,24 +285,47 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         const int j = J * 64 + l;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const double w = (((accj[0][k][l] + accj[0][k][l + 64]) + (accj[1][k][l] + accj[1][k][l + 64])) +
-                              (accj[2][k][l] + accj[2][k][l + 64])) + (accj[3][k][l] + accj[3][k][l + 64]);
+            const double w = n3_jsum(accj, k, l);
             if (j < S) Pj[(size_t)k * S + j] = -w;
         }
     }
 }
 
+#if defined(MDQT_EXPT_STAMPS)
+// diagnostic build only: per-workgroup start/end (s_memrealtime, 100 MHz) and placement
+__device__ unsigned long long g_n3_stamps[4 * 8192];
+#endif
+
 template <int VARIANT, bool GUARD>
-__global__ __launch_bounds__(256) void k_pairs_n3(N3Args a) {
+__global__ __launch_bounds__(64 * N3W) void k_pairs_n3(N3Args a) {
     __shared__ double pj[3][128];
-    __shared__ double accj[4][3][128];
-    __shared__ double ia[4][3][64];
+    __shared__ double accj[N3W][3][128];
+    __shared__ double ia[N3W][3][64];
     __shared__ double mj[128];
+#if defined(MDQT_EXPT_STAMPS)
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const int2 IJ = a.pairs[blockIdx.x];
     const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
     if ((a.N & 63) && IJ.y == a.ntiles - 1) n3_tile<VARIANT, GUARD, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
     else n3_tile<VARIANT, GUARD, false>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+#if defined(MDQT_EXPT_STAMPS)
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        g_n3_stamps[4 * blockIdx.x] = t_start;
+        g_n3_stamps[4 * blockIdx.x + 1] = t_end;
+        g_n3_stamps[4 * blockIdx.x + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        g_n3_stamps[4 * blockIdx.x + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+    }
+#endif
 }
+
+#if defined(MDQT_EXPT_STAMPS)
+extern "C" int mdqt_expt_n3_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_n3_stamps), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Newton-3 over BLOCK pairs (large N, one GPU or sharded): blocks of 16 tiles (1024 ions); a
@@ -473,18 +499,18 @@ hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int 
     return hipGetLastError();
 }
 
-hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s) {
+hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (a.npairs <= 0) return hipSuccess;
     dim3 grid(a.npairs);
     if (variant == 2) {
-        if (a.guard) hipLaunchKernelGGL((k_pairs_n3<2, true>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_pairs_n3<2, false>), grid, dim3(256), 0, s, a);
+        if (a.guard) launch_timed(k_pairs_n3<2, true>, grid, dim3(64 * N3W), s, ev0, ev1, a);
+        else launch_timed(k_pairs_n3<2, false>, grid, dim3(64 * N3W), s, ev0, ev1, a);
     } else if (variant == 1) {
-        if (a.guard) hipLaunchKernelGGL((k_pairs_n3<1, true>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_pairs_n3<1, false>), grid, dim3(256), 0, s, a);
+        if (a.guard) launch_timed(k_pairs_n3<1, true>, grid, dim3(64 * N3W), s, ev0, ev1, a);
+        else launch_timed(k_pairs_n3<1, false>, grid, dim3(64 * N3W), s, ev0, ev1, a);
     } else {
-        if (a.guard) hipLaunchKernelGGL((k_pairs_n3<0, true>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_pairs_n3<0, false>), grid, dim3(256), 0, s, a);
+        if (a.guard) launch_timed(k_pairs_n3<0, true>, grid, dim3(64 * N3W), s, ev0, ev1, a);
+        else launch_timed(k_pairs_n3<0, false>, grid, dim3(64 * N3W), s, ev0, ev1, a);
     }
     return hipGetLastError();
 }

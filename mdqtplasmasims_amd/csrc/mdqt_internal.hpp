@@ -3,6 +3,9 @@
 // globals: several contexts with different parameters may live in one process).
 #pragma once
 #include <hip/hip_runtime.h>
+#if defined(__HIP__)
+#include <hip/hip_ext.h>
+#endif
 #include <stdint.h>
 
 namespace mdqt {
@@ -309,7 +312,8 @@ hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s);
 
 // ---- launchers (mdqt_kernels.hip) ----
 hipError_t launch_forces(const ForceArgs& a, hipStream_t s);
-hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s);
+hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEvent_t ev0 = nullptr,
+                            hipEvent_t ev1 = nullptr);
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
                                   hipStream_t s);
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[seg][0][i]
@@ -317,9 +321,24 @@ hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[
 //       1 = thread-per-ion, 2 = lane-per-state.  Both are bit-identical.
 constexpr int kLaneKernelMaxIons = 98304;
 // fast: qt_math 1 (FMA contraction, refined rsq) instead of the reference's exact operations
-hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s);
+#if defined(__HIP__)
+// Launch with the kernel's own dispatch timestamps written to (ev0, ev1) when timing is on
+// (hipExtLaunchKernelGGL): the measured interval is the kernel itself, without the event
+// packets' queue time that a pair of hipEventRecord calls around the launch adds.
+template <typename... Args, typename F = void (*)(Args...)>
+inline void launch_timed(F kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                         Args... args) {
+    if (ev0) hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ev0, ev1, 0, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+}
+#endif
+
+// ev0/ev1 (optional): the kernel's own start/stop timestamps (hipExtLaunchKernelGGL)
+hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s,
+                           hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // qt_math 2: the reassociated kernels of mdqt_qtfast.hip (same modes as launch_substeps)
-hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s);   // tab[0] by state, tab[1] by lane
+hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s,
+                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);   // tab[0] by state, tab[1] by lane
 // measureSpinUps (randomFrozenStartTag408Linear.cpp:600, :422Linear) / tagParticles
 // (MonteCarloFollowedByQTTagging408Linear.cpp:1022): tag[i] = 1 with probability of spin up
 hipError_t launch_tag_spin_up(const double* psi, int n, int S, uint64_t gid0, uint64_t q, const QTConst& qc,

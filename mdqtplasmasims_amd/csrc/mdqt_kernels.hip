@@ -577,16 +577,17 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
     }
 }
 
-hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s) {
+hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s,
+                           hipEvent_t ev0, hipEvent_t ev1) {
     if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
-    const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256);
+    const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256), b(256);
     if (fast) {
-        if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes<true>, gl, dim3(256), 0, s, a, tab);
-        else hipLaunchKernelGGL(k_substeps<true>, gt, dim3(256), 0, s, a);
+        if (mode == 2) launch_timed(k_substeps_lanes<true>, gl, b, s, ev0, ev1, a, tab);
+        else launch_timed(k_substeps<true>, gt, b, s, ev0, ev1, a);
     } else {
-        if (mode == 2) hipLaunchKernelGGL(k_substeps_lanes<false>, gl, dim3(256), 0, s, a, tab);
-        else hipLaunchKernelGGL(k_substeps<false>, gt, dim3(256), 0, s, a);
+        if (mode == 2) launch_timed(k_substeps_lanes<false>, gl, b, s, ev0, ev1, a, tab);
+        else launch_timed(k_substeps<false>, gt, b, s, ev0, ev1, a);
     }
     return hipGetLastError();
 }

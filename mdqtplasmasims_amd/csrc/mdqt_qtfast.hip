@@ -460,20 +460,21 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
     }
 }
 
-hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s) {
+hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s, hipEvent_t ev0,
+                             hipEvent_t ev1) {
     if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
     if (a.nsub > MAXSUB) return hipErrorInvalidValue;
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
     if (a.qc.model < 0 || a.qc.model >= NMODELS) return hipErrorInvalidValue;
-    const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256);
+    const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256), b(256);
     if (mode == 2) {
-        if (a.qc.model == 0) hipLaunchKernelGGL(k_substeps_lanes_r<true>, gl, dim3(256), 0, s, a, tab + 1);
-        else hipLaunchKernelGGL(k_substeps_lanes_r<false>, gl, dim3(256), 0, s, a, tab + 1);
+        if (a.qc.model == 0) launch_timed(k_substeps_lanes_r<true>, gl, b, s, ev0, ev1, a, tab + 1);
+        else launch_timed(k_substeps_lanes_r<false>, gl, b, s, ev0, ev1, a, tab + 1);
     }
-    else if (a.qc.model == 0) hipLaunchKernelGGL(k_substeps_r<0>, gt, dim3(256), 0, s, a, tab);
-    else if (a.qc.model == 1) hipLaunchKernelGGL(k_substeps_r<1>, gt, dim3(256), 0, s, a, tab);
-    else if (a.qc.model == 2) hipLaunchKernelGGL(k_substeps_r<2>, gt, dim3(256), 0, s, a, tab);
-    else hipLaunchKernelGGL(k_substeps_r<3>, gt, dim3(256), 0, s, a, tab);
+    else if (a.qc.model == 0) launch_timed(k_substeps_r<0>, gt, b, s, ev0, ev1, a, tab);
+    else if (a.qc.model == 1) launch_timed(k_substeps_r<1>, gt, b, s, ev0, ev1, a, tab);
+    else if (a.qc.model == 2) launch_timed(k_substeps_r<2>, gt, b, s, ev0, ev1, a, tab);
+    else launch_timed(k_substeps_r<3>, gt, b, s, ev0, ev1, a, tab);
     return hipGetLastError();
 }
 

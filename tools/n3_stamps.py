@@ -1,0 +1,44 @@
+"""Diagnostic (variant build with -DMDQT_EXPT_STAMPS): per-workgroup start/end times and placement
+of the Newton-3 tile kernel at C2.  MDQT_LIB=expt/stamps/lib/libmdqt.so python tools/n3_stamps.py"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import mdqtplasmasims_amd as M  # noqa: E402
+from mdqtplasmasims_amd._lib import lib  # noqa: E402
+
+s = M.Simulation(N0=int(sys.argv[1]) if len(sys.argv) > 1 else 3500, seed=12346).init()
+for _ in range(3):
+    s.md_steps(1)
+s.synchronize()
+s.forces()
+s.synchronize()
+n = s.counters and 1596
+ntiles = (s.N + 63) // 64
+n = ntiles * (ntiles + 1) // 2
+buf = (C.c_ulonglong * (4 * n))()
+assert lib().mdqt_expt_n3_stamps(buf, n) == 0
+a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.int64)
+t0 = a[:, 0].min()
+st = (a[:, 0] - t0) * 10e-3      # us (100 MHz)
+en = (a[:, 1] - t0) * 10e-3
+life = en - st
+hw = a[:, 2]
+cu = (hw >> 8) & 15
+sh = (hw >> 12) & 1
+se = (hw >> 13) & 7
+xcc = a[:, 3] & 15
+print(f"N={s.N} WGs={n} kernel span {en.max():.2f} us")
+print("start  pct 0/10/50/90/100:", np.percentile(st, [0, 10, 50, 90, 100]).round(2))
+print("end    pct 0/10/50/90/100:", np.percentile(en, [0, 10, 50, 90, 100]).round(2))
+print("life   pct 0/10/50/90/100:", np.percentile(life, [0, 10, 50, 90, 100]).round(2))
+key = xcc * 1000 + se * 100 + sh * 16 + cu
+u, cnt = np.unique(key, return_counts=True)
+print("distinct CUs used:", len(u), " WGs per CU min/mean/max:", cnt.min(), round(cnt.mean(), 2), cnt.max())
+print("per-XCC WGs:", np.bincount(xcc, minlength=8))
+diag = np.array([0])
+hist = np.histogram(st, bins=10)[0]
+print("start histogram (10 bins over span):", hist)

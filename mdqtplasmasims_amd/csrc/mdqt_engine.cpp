@@ -16,6 +16,7 @@
 #include <string>
 #include <algorithm>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -23,6 +24,7 @@
 #include "../../include/mdqt.h"
 #include "mdqt_internal.hpp"
 #include "mdqt_writer.hpp"
+#include "mdqt_init_sample.hpp"
 
 using namespace mdqt;
 
@@ -63,12 +65,7 @@ inline cx cx_add(cx a, cx b) { return {a.re + b.re, a.im + b.im}; }
 inline cx cx_sub(cx a, cx b) { return {a.re - b.re, a.im - b.im}; }
 inline cx cx_conj(cx a) { return {a.re, -a.im}; }
 
-// glibc drand48 (SpeedUp:303-333, srand48 :1219), bit-exact.
-inline uint64_t srand48_state(uint32_t seed) { return (((uint64_t)seed) << 16) | 0x330Eull; }
-inline double drand48_next(uint64_t* x) {
-    *x = (0x5DEECE66Dull * (*x) + 0xBull) & 0xFFFFFFFFFFFFull;
-    return ldexp((double)(*x), -48);
-}
+// glibc drand48 (SpeedUp:303-333, srand48 :1219): mdqt_init_sample.hpp
 
 }  // namespace
 
@@ -129,6 +126,7 @@ struct mdqt_ctx {
     std::vector<double> Vholder;   // [13][3][N] VZERO_* files (SpeedUp:752-763, :898-913)
     char saveDirectory[1024];
     std::unique_ptr<FileWriter> writer;   // background formatting/writing of the output files
+    int init_threads = 0;          // init() sampling threads (option "init_threads"; 0 auto, 1 sequential)
     // timing
     // per-launch HIP events of the hot kernels (kind 0 = force, 1 = substeps), recorded on
     // the launch stream while timing is on; summed by mdqt_kernel_time_totals
@@ -856,34 +854,39 @@ extern "C" int mdqt_get_counters(const mdqt_ctx* s, int* c0, unsigned* counter, 
 // init (SpeedUp:289-348): drand48 rejection sampling, bit-exact with the reference stream
 // ---------------------------------------------------------------------------------------------
 
+// ---------------------------------------------------------------------------------------------
+// init() (SpeedUp:289-348): rejection sampling of N9L candidate triples from ONE drand48 stream;
+// a kept triple consumes 4 more draws for its wavefunction.
+//
+// Sequentially that is 3 N9L + 4 N draws (2.2e9 at N0 = 1M: ~13 s on one core).  In parallel,
+// with the same stream and the same result bit for bit: a candidate starting at draw index p is
+// kept iff ok(u_p) && ok(u_p+1) && ok(u_p+2), independently of the walk, so (1) threads scan
+// disjoint ranges of draw indices (LCG jump-ahead to each range start) and list every p that
+// WOULD be kept (rate 1/729); (2) one pass walks the candidates: from p the walk visits p, p+3,
+// ... until the first listed p' in the same residue class mod 3, takes it and continues at
+// p' + 7 (so the class shifts by one per kept ion), counting candidates up to N9L; (3) the kept
+// ions' 7 draws are regenerated by jump-ahead, in parallel.  If the walk runs past the scanned
+// range (more ions than the bound allows) it finishes sequentially from there.
+// ---------------------------------------------------------------------------------------------
+
 extern "C" int mdqt_init(mdqt_ctx* s) {
     if (!s) return fail("NULL context");
     const double L = s->L;
     const double N9L = (unsigned)(9. * 9. * 9. * (L * L * L) * 3. / (4. * M_PI));   // :299
-    std::vector<double> X, Y, Z, psi;
-    const size_t guess = (size_t)s->p.N0 + 1000;
-    X.reserve(guess); Y.reserve(guess); Z.reserve(guess); psi.reserve(guess * 24);
-    s->x48 = srand48_state(s->p.seed);                                                // :1219
-    for (long i = 0; i < N9L; i++) {                                                  // :303
-        const double x = 9. * L * drand48_next(&s->x48) - 4. * L;
-        const double y = 9. * L * drand48_next(&s->x48) - 4. * L;
-        const double z = 9. * L * drand48_next(&s->x48) - 4. * L;
-        if (x <= L && y <= L && z <= L && x > 0 && y > 0 && z > 0) {                 // :308
-            X.push_back(x); Y.push_back(y); Z.push_back(z);
-            const double rand1 = drand48_next(&s->x48);                                // :317-328
-            const double rand2 = drand48_next(&s->x48);
-            const double rand3 = drand48_next(&s->x48);
-            double sign = 1;
-            if (rand3 < 0.5) sign = -1;
-            const double rand4 = drand48_next(&s->x48);
-            double sign2 = 1;
-            if (rand4 < 0.5) sign2 = -1;
-            double w[24] = {0};                                                        // :329-332
-            w[0] = sqrt(rand1);
-            w[2] = sign2 * sqrt(1 - rand1) * sqrt(rand2);
-            w[3] = sign * sqrt(1 - rand1) * sqrt(1 - rand2);
-            psi.insert(psi.end(), w, w + 24);
-        }
+    int threads = s->init_threads;
+    if (threads <= 0) {
+        const unsigned hc = std::thread::hardware_concurrency();
+        threads = (int)std::min(16u, hc ? hc : 1u);
+    }
+    const long Nbound = (long)s->p.N0 + 1000 + (long)(20. * sqrt((double)s->p.N0 + 1.));
+    uint64_t xend = 0;
+    const std::vector<InitIon> ions =
+        init_sample(srand48_state(s->p.seed), L, (long)N9L, Nbound, threads, &xend);   // :1219, :303-335
+    s->x48 = xend;
+    std::vector<double> X, Y, Z, psi((size_t)24 * ions.size(), 0.);
+    for (size_t k = 0; k < ions.size(); ++k) {
+        X.push_back(ions[k].x); Y.push_back(ions[k].y); Z.push_back(ions[k].z);
+        psi[24 * k] = ions[k].w0; psi[24 * k + 2] = ions[k].w2; psi[24 * k + 3] = ions[k].w3;
     }
     const int N = (int)X.size();
     std::vector<double> R((size_t)3 * N), V((size_t)3 * N, 0.), tp((size_t)N, 0.);
@@ -1585,6 +1588,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     if (!strcmp(name, "force_kernel")) {
         if (value < 0 || value > 1) return fail("force_kernel must be 0 (exact) or 1 (fast)");
         s->force_variant = value;
+        return 0;
+    }
+    if (!strcmp(name, "init_threads")) {                // init() sampling: 0 auto, 1 sequential, k threads
+        if (value < 0 || value > 256) return fail("init_threads must be in [0, 256]");
+        s->init_threads = value;
         return 0;
     }
     if (!strcmp(name, "substep_kernel")) {

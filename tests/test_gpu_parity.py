@@ -498,6 +498,22 @@ def test_run_writes_reference_layout(eng, orc, tmp_path):
         assert np.allclose(xa, xb, rtol=2e-5, atol=1e-9 * max(1.0, np.abs(xb).max())), f
 
 
+def test_init_parallel_sampling_matches_sequential(eng):
+    """init()'s drand48 rejection sampling in parallel (option init_threads, default auto) equals
+    the sequential walk (init_threads 1) bit for bit, incl. the stream state qsteps continue from"""
+    out = []
+    for th in (1, 6):
+        s = eng.Simulation(N0=3500, seed=12346, rng_mode=0)
+        s.set_option("init_threads", th)
+        s.init()
+        st = s.get_state()
+        out.append((s.N, st["R"], st["psi"], s.drand48_state))
+        s.close()
+    (n1, R1, p1, x1), (n2, R2, p2, x2) = out
+    assert n1 == n2 == 3573
+    assert np.array_equal(R1, R2) and np.array_equal(p1, p2) and x1 == x2
+
+
 def test_run_files_are_lg_of_the_final_state(eng, tmp_path):
     """mdqt_run's files come from the background writers (mdqt_writer.hpp): byte for byte the
     "%lg" text of the state the run ends with (SpeedUp:747, :777-779)."""

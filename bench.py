@@ -65,6 +65,11 @@ def parse():
                     help="skip the jobs-per-GPU line (k independent C2 jobs sharing one GPU)")
     ap.add_argument("--secondary-deadline", type=float, default=420.0,
                     help="seconds allowed for all secondary line items together")
+    ap.add_argument("--sharded-in-child", type=int, default=-1,
+                    help="run the sharded lines in child processes (own RCCL group) so that a fault "
+                         "there cannot take the headline line with it: 1 yes, 0 no, -1 auto (world > 1)")
+    ap.add_argument("--child-sharded", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--child-steps", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--sharded-steps", type=int, default=3)
     ap.add_argument("--qt-math", type=int, default=2, choices=[0, 1, 2],
                     help="0: the reference's exact QT operations, 1: FMA-contracted, 2: reassociated "
@@ -116,8 +121,65 @@ def cpu_baseline(params, qt, seconds, seed, job):
                       f"restatement, OpenMP {threads} threads, {el:.1f} s"}
 
 
+def child_main(args):
+    """one rank of a sharded line in its own process and RCCL group (see sharded_in_children)"""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    res = sharded_run(args.child_sharded, args.child_steps, rank, world, local, dist, barrier)
+    if rank == 0:
+        print("CHILD_JSON " + json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+_CHILD_PORT_OFFSET = [0]
+
+
+def sharded_in_children(cfg, steps, rank, world, timeout):
+    """Every rank starts one child process that runs the sharded line with the other ranks'
+    children (a fresh RCCL group on another port); the parent only waits.  A child that faults
+    or hangs costs this line only (reported in secondary_errors), never the headline."""
+    import subprocess
+    _CHILD_PORT_OFFSET[0] += 1
+    env = dict(os.environ)
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)       # the child group runs its own store
+    env["MASTER_ADDR"] = env.get("MASTER_ADDR", "127.0.0.1")
+    env["MASTER_PORT"] = str(int(env.get("MASTER_PORT", "29500")) + 97 + _CHILD_PORT_OFFSET[0])
+    env.setdefault("RANK", str(rank)); env.setdefault("WORLD_SIZE", str(world))
+    env.setdefault("LOCAL_RANK", os.environ.get("LOCAL_RANK", "0"))
+    cmd = [sys.executable, os.path.abspath(__file__), "--child-sharded", cfg, "--child-steps", str(steps)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        raise RuntimeError(f"sharded child did not finish within {timeout:.0f} s")
+    if r.returncode != 0:
+        raise RuntimeError(f"sharded child exited {r.returncode}: {r.stderr.strip()[-400:]}")
+    if rank != 0:
+        return None
+    for line in r.stdout.splitlines():
+        if line.startswith("CHILD_JSON "):
+            return json.loads(line[len("CHILD_JSON "):])
+    raise RuntimeError("sharded child printed no result")
+
+
 def main():
     args = parse()
+    if args.child_sharded:
+        return child_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -223,16 +285,24 @@ def main():
         dog.run("jobs_per_gpu", lambda: replicas_line(local, args.config))
     if world == 1 and not args.no_e2e_line:
         dog.run("end_to_end", lambda: end_to_end_line(local, args.config, args.e2e_md_steps))
+    # one large system sharded over all ranks (RCCL all-gather / reduce-scatter per MD step)
+    in_child = args.sharded_in_child == 1 or (args.sharded_in_child == -1 and world > 1)
+
+    def sharded(cfg, steps):
+        if in_child:
+            try:
+                return sharded_in_children(cfg, steps, rank, world, timeout=150.0)
+            finally:
+                if world > 1:
+                    dist.barrier()
+        return sharded_run(cfg, steps, rank, world, local, dist, barrier)
+
     if args.md_only_config != "none":
-        dog.run("md_only_" + args.md_only_config,
-                lambda: sharded_run(args.md_only_config, args.sharded_steps, rank, world, local, dist, barrier))
-    # secondary line item: one large system sharded over all ranks (RCCL all-gather per MD step)
+        dog.run("md_only_" + args.md_only_config, lambda: sharded(args.md_only_config, args.sharded_steps))
     if args.sharded_config != "none":
-        dog.run("sharded", lambda: sharded_run(args.sharded_config, args.sharded_steps, rank, world, local,
-                                               dist, barrier))
+        dog.run("sharded", lambda: sharded(args.sharded_config, args.sharded_steps))
     if args.million_config != "none":
-        dog.run("sharded_1m", lambda: sharded_run(args.million_config, args.million_steps, rank, world, local,
-                                                  dist, barrier))
+        dog.run("sharded_1m", lambda: sharded(args.million_config, args.million_steps))
     dog.finish()
     if rank == 0:
         print(json.dumps(out), flush=True)

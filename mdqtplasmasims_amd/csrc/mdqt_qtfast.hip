@@ -21,6 +21,13 @@
 
 namespace mdqt {
 
+// threads per workgroup of the lane-per-state kernels (16 lanes per ion)
+#ifndef MDQT_LANE_WG
+#define MDQT_LANE_WG 256
+#endif
+constexpr int kLaneWG = MDQT_LANE_WG;
+static_assert(kLaneWG % 64 == 0 && kLaneWG <= 256, "lane kernel workgroup: whole waves, <= 256 threads");
+
 __device__ __forceinline__ double rsq_nr(double x) { return rsq3(x); }   // 1/sqrt(x), mdqt_internal.hpp
 __device__ __forceinline__ double nrm2(cxd y) { return fma(y.re, y.re, y.im * y.im); }
 __device__ __forceinline__ double rho_im_r(cxd a, cxd b) { return fma(a.im, b.re, -(a.re * b.im)); }
@@ -290,7 +297,7 @@ template <bool DPPX>
 __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
     const int k = threadIdx.x & 15;
     const int grp = threadIdx.x >> 4;
-    const int iraw = blockIdx.x * 16 + grp;
+    const int iraw = blockIdx.x * (kLaneWG / 16) + grp;
     const bool store = iraw < a.n;
     const int i = store ? iraw : a.n - 1;             // idle groups shadow the last ion
     const QTConst& qc = a.qc;
@@ -321,7 +328,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
     const uint64_t gid = a.gid0 + (uint64_t)i;
     // u1, u2 of every substep of the launch staged in LDS: Philox draws computed lane-parallel
     // (lane k: substeps k, k + 16), or the rng_mode 0 uniforms of the single substep
-    __shared__ double su[16][MAXSUB][2];
+    __shared__ double su[kLaneWG / 16][MAXSUB][2];
     if (a.do_qt) {
         if (a.U) {
             if (k == 0) { su[grp][0][0] = a.U[i]; su[grp][0][1] = a.U[(size_t)S + i]; }
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
         }
     }
     __syncthreads();
-    __shared__ double2 xg[DPPX ? 1 : 256];
+    __shared__ double2 xg[DPPX ? 1 : kLaneWG];
     auto exchange = [&](cxd y, cxd& y0, cxd& y1, cxd& y2) {
         if constexpr (DPPX) {
             y0 = {dpp<QP_XOR2>(y.re), dpp<QP_XOR2>(y.im)};
@@ -466,10 +473,10 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
     if (a.nsub > MAXSUB) return hipErrorInvalidValue;
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
     if (a.qc.model < 0 || a.qc.model >= NMODELS) return hipErrorInvalidValue;
-    const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256), b(256);
+    const dim3 gl((a.n + kLaneWG / 16 - 1) / (kLaneWG / 16)), bl(kLaneWG), gt((a.n + 255) / 256), b(256);
     if (mode == 2) {
-        if (a.qc.model == 0) launch_timed(k_substeps_lanes_r<true>, gl, b, s, ev0, ev1, a, tab + 1);
-        else launch_timed(k_substeps_lanes_r<false>, gl, b, s, ev0, ev1, a, tab + 1);
+        if (a.qc.model == 0) launch_timed(k_substeps_lanes_r<true>, gl, bl, s, ev0, ev1, a, tab + 1);
+        else launch_timed(k_substeps_lanes_r<false>, gl, bl, s, ev0, ev1, a, tab + 1);
     }
     else if (a.qc.model == 0) launch_timed(k_substeps_r<0>, gt, b, s, ev0, ev1, a, tab);
     else if (a.qc.model == 1) launch_timed(k_substeps_r<1>, gt, b, s, ev0, ev1, a, tab);

@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash gpurun_tests.sh || exit $?
+bash tools/gpu/gpurun_tests.sh || exit $?
 timeout -k 10 200 python -u tools/mdmc_timing.py > gpurun_out/mdmc_timing.log 2>&1 || { cat gpurun_out/mdmc_timing.log; exit 1; }
 cat gpurun_out/mdmc_timing.log
 timeout -k 10 300 python bench.py --no-cpu-baseline --sharded-config none --million-config none --no-mcmd-lines --md-only-config none --no-e2e-line \

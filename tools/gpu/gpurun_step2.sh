@@ -1,5 +1,5 @@
 #!/bin/bash
 # tests + bench + kernel trace, then PMC passes (counters only)
 cd "$GRAFT_REPO_ROOT" || exit 1
-bash gpurun_step1.sh || exit $?
-bash gpurun_pmc.sh
+bash tools/gpu/gpurun_step1.sh || exit $?
+bash tools/gpu/gpurun_pmc.sh

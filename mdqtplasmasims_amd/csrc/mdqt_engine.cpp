@@ -970,12 +970,18 @@ static int settle_forces(mdqt_ctx* s) {
     return 0;
 }
 
+// Timing events only measure: no system-scope release/acquire when they complete.  With the
+// default flags every timed launch ended in an L2 write-back + invalidate that cost the MD step
+// ~20 us (kernel trace of the driver's bench command: gaps of 6.5 / 8.9 / 4.8 us around each
+// timed pair of launches, none elsewhere).
+static constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
+
 // record the next timing event of kind k (start/stop alternate)
 static int mark(mdqt_ctx* s, int k) {
     auto& pool = s->evpool[k];
     if (s->evused[k] == (int)pool.size()) {
         hipEvent_t e;
-        HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
         pool.push_back(e);
     }
     HIPCHK(hipEventRecord(pool[s->evused[k]++], s->stream));
@@ -987,7 +993,7 @@ static int take_events(mdqt_ctx* s, int k, hipEvent_t* e0, hipEvent_t* e1) {
     auto& pool = s->evpool[k];
     while ((int)pool.size() < s->evused[k] + 2) {
         hipEvent_t e;
-        HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
         pool.push_back(e);
     }
     *e0 = pool[s->evused[k]++];
@@ -1068,9 +1074,13 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         a.L = s->L;
         a.qc = s->qc;
         double t = s->t;
+        a.movmask = 0;
+        a.expdet_zero = 1;
         for (int k = 0; k < m; ++k) {
             a.t[k] = t;
             a.expDet[k] = expDetuning_of(&s->p, t);
+            if (t > 0) a.movmask |= 1u << k;
+            if (a.expDet[k] != 0.) a.expdet_zero = 0;
             if (advance_t) t += s->dtQ;                    // qstep: t += dtQuant (:716)
         }
         if (d48 && s->nloc > 0) {
@@ -1645,9 +1655,10 @@ extern "C" int mdqt_kernel_time_totals(mdqt_ctx* s, double* force_ms, int* nforc
 }
 
 // ---------------------------------------------------------------------------------------------
-// RCCL: one communicator per context over world_size ranks (one process per GPU).  The only
-// data-path collective is the per-MD-step all-gather of the position slabs;
-// output steps all-reduce a few scalars, the KDE bins and the per-ion file columns.
+// RCCL: one communicator per context over world_size ranks (one process per GPU).  Data-path
+// collectives per MD step: the all-gather of the position slabs and, for Newton-3
+// block pairs (N > 65,536), the reduce-scatter of the per-rank dense partial forces; output
+// steps all-reduce a few scalars, the KDE bins and the per-ion file columns.
 // ---------------------------------------------------------------------------------------------
 
 

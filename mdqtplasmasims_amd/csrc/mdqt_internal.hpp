@@ -144,6 +144,8 @@ struct SubstepArgs {
     double L;
     double t[MAXSUB];       // global time at each substep (t before qstep advances it)
     double expDet[MAXSUB];  // expDetuning(t) (:447)
+    uint32_t movmask;       // bit s: t[s] > 0 (step_R's moving branch, :360); set by the host
+    int expdet_zero;        // every expDet[s] == 0 (fracOfSig = 0, the default)
     QTConst qc;
 };
 

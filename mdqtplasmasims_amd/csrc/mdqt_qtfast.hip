@@ -293,8 +293,22 @@ __device__ __forceinline__ double lane_sum_p8(double T) {
     return (dpp<BCAST(0)>(T) + dpp<BCAST(3)>(T)) + (dpp<BCAST(4)>(T) + dpp<BCAST(7)>(T));
 }
 
+#if defined(MDQT_EXPT_QTSTAMPS)
+// diagnostic build only: per-wave s_memtime at entry, loop start, loop end, exit + s_memrealtime
+// at entry and exit (tools/qt_stamps.py)
+__device__ unsigned long long g_qt_stamps[6 * 4096];
+#define QT_STAMP(slot, v) (st_[slot] = (v))
+#else
+#define QT_STAMP(slot, v) ((void)0)
+#endif
+
 template <bool DPPX>
 __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
+#if defined(MDQT_EXPT_QTSTAMPS)
+    unsigned long long st_[6];
+#endif
+    QT_STAMP(0, __builtin_amdgcn_s_memtime());
+    QT_STAMP(4, __builtin_amdgcn_s_memrealtime());
     const int k = threadIdx.x & 15;
     const int grp = threadIdx.x >> 4;
     const int iraw = blockIdx.x * (kLaneWG / 16) + grp;
@@ -326,6 +340,22 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
     if (a.do_qt && st < NS) w = {a.psi[(size_t)(2 * st) * S + i], a.psi[(size_t)(2 * st + 1) * S + i]};
     const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
     const uint64_t gid = a.gid0 + (uint64_t)i;
+    // per-substep constants in registers, not kernel-argument loads inside the substep loop (a
+    // scalar load indexed by the substep waits ~100+ cycles in every iteration): the moving flags
+    // as a bit mask, expDetuning(t) of substep s in lane s & 15 of the row (s < 16: ed0, else ed1)
+    const uint32_t movmask = a.movmask;
+    const bool edz = a.expdet_zero != 0;
+    const double ed0 = edz ? 0. : a.expDet[k], ed1 = edz ? 0. : a.expDet[k + 16];
+    // (read ed0 / ed1 themselves, written with every lane active: a value selected per lane
+    // inside a divergent branch would be stale in the inactive lane the read picks)
+    auto rl = [](double e, int l) {
+        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(e), l),
+                                __builtin_amdgcn_readlane(__double2loint(e), l));
+    };
+    auto expdet = [&](int s) -> double {
+        if (edz) return 0.;
+        return s < 16 ? rl(ed0, s & 15) : rl(ed1, s & 15);
+    };
     // u1, u2 of every substep of the launch staged in LDS: Philox draws computed lane-parallel
     // (lane k: substeps k, k + 16), or the rng_mode 0 uniforms of the single substep
     __shared__ double su[kLaneWG / 16][MAXSUB][2];
@@ -357,11 +387,12 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
         y0 = {t0.x, t0.y}; y1 = {t1.x, t1.y}; y2 = {t2.x, t2.y};
     };
     auto drift = [&](double& pp, double& vv, int sub) {   // step(): step_R, step_V, step_R (:418-430)
-        const bool moving = a.t[sub] > 0;
+        const bool moving = (movmask >> sub) & 1u;
         pp = half_drift(pp, vv, f, moving, DT, DT2, L);
         vv = vv + dt * f;                             // step_V(dt) :398-409
         pp = half_drift(pp, vv, f, moving, DT, DT2, L);
     };
+    QT_STAMP(1, __builtin_amdgcn_s_memtime());
     if (!a.do_qt) {
         if (a.do_step)
             for (int s = 0; s < a.nsub; ++s) drift(p, v, s);
@@ -372,9 +403,9 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
         // the same values as the plain order: bit-identical.
         if (a.do_step) drift(p, v, 0);
         double sn, cs;
-        sincos_q<true>(((v * qc.pv2q + a.expDet[0]) * cphi) * (tPart + qc.dtQ), sn, cs);
+        sincos_q<true>(((v * qc.pv2q + expdet(0)) * cphi) * (tPart + qc.dtQ), sn, cs);
         for (int s = 0; s < a.nsub; ++s) {
-            const double u = v * qc.pv2q + a.expDet[s];    // vx on every state lane
+            const double u = v * qc.pv2q + expdet(s);      // vx on every state lane
             tPart += qc.dtQ;
             const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp) : lane_sum_p(nrm2(w) * hdp);
             const double u1 = su[grp][s][0], u2 = su[grp][s][1];
@@ -395,7 +426,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
                 const bool adv = a.do_step && s + 1 < a.nsub;   // no drift after the last substep
                 pn = adv ? pd : pn;
                 vn = adv ? vd : vn;
-                phin = ((vn * qc.pv2q + a.expDet[s1]) * cphi) * (tPart + qc.dtQ);
+                phin = ((vn * qc.pv2q + expdet(s1)) * cphi) * (tPart + qc.dtQ);
                 sincos_fast(phin, snn, csn);
             };
             if (nojump) {
@@ -451,6 +482,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
             cs = csn;
         }
     }
+    QT_STAMP(2, __builtin_amdgcn_s_memtime());
     if (store) {
         if (owner) {
             a.R[(size_t)c * S + i] = p;
@@ -465,7 +497,26 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
             }
         }
     }
+#if defined(MDQT_EXPT_QTSTAMPS)
+    __builtin_amdgcn_s_waitcnt(0);
+    st_[3] = __builtin_amdgcn_s_memtime();
+    st_[5] = __builtin_amdgcn_s_memrealtime();
+    const int wv = (int)(blockIdx.x * (kLaneWG / 64) + (threadIdx.x >> 6));
+    if ((threadIdx.x & 63) < 6 && wv < 4096) {              // vector stores, one slot per lane
+        const int q = threadIdx.x & 63;
+        unsigned long long v = st_[0];
+#pragma unroll
+        for (int m = 1; m < 6; ++m) v = (q == m) ? st_[m] : v;
+        g_qt_stamps[6 * wv + q] = v;
+    }
+#endif
 }
+
+#if defined(MDQT_EXPT_QTSTAMPS)
+extern "C" int mdqt_expt_qt_stamps(unsigned long long* out, int nwaves) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 6 * nwaves) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s, hipEvent_t ev0,
                              hipEvent_t ev1) {

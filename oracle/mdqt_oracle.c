@@ -63,6 +63,8 @@ struct orc_sim {
     uint64_t x48;                     /* drand48 state */
     uint64_t qidx;                    /* number of qstep() calls (Philox counter) */
     char saveDirectory[1024];
+    uint64_t* ion_ids;                /* Philox ion key of local ion i (NULL: i); sampled-ion checks */
+    int n_ion_ids;
 };
 
 /* ------------------------------------------------------------------------------------------ */
@@ -252,6 +254,7 @@ orc_sim* orc_create(const orc_params* p) {
 void orc_destroy(orc_sim* s) {
     if (!s) return;
     free(s->R); free(s->V); free(s->F); free(s->psi); free(s->tPart); free(s->Vholder);
+    free(s->ion_ids);
     free(s);
 }
 
@@ -409,6 +412,54 @@ void orc_forces_rows(int N, int lo, int hi, double L, double lDeb, const double*
         F[i] = Fx; F[ld + i] = Fy; F[2 * ld + i] = Fz;
     }
     (void)nthreads;
+}
+
+/* rows idx[0..nidx) of the same pair terms (every j), F is [3][nidx], summed with Neumaier
+ * compensation: at N ~ 1e6 a plain ascending sum carries ~N eps of rounding of its own, so the
+ * large-N GPU checks compare sampled ions against these nearly exact rows. */
+void orc_forces_index(int N, double L, double lDeb, const double* R, size_t ld, const int* idx, int nidx,
+                      double* F, int nthreads) {
+    const double Rcut = L / 2.;
+    const double* X = R; const double* Y = R + ld; const double* Z = R + 2 * ld;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int k = 0; k < nidx; k++) {
+        const int i = idx[k];
+        double S[3] = {0., 0., 0.}, C[3] = {0., 0., 0.};   /* Neumaier sum and its compensation */
+        double rx = X[i], ry = Y[i], rz = Z[i];
+        for (int j = 0; j < N; j++) {                                            /* SpeedUp:211-230 */
+            if (j == i) continue;
+            double dx = rx - X[j];
+            double dy = ry - Y[j];
+            double dz = rz - Z[j];
+            dx -= L * round(dx / L);
+            dy -= L * round(dy / L);
+            dz -= L * round(dz / L);
+            double dr = sqrt(dx * dx + dy * dy + dz * dz);
+            if (dr > 0 && dr < Rcut) {
+                double ftotal = (1. / dr + 1. / lDeb) * exp(-dr / lDeb) / (dr * dr);
+                const double t[3] = {dx * ftotal, dy * ftotal, dz * ftotal};
+                for (int c = 0; c < 3; ++c) {
+                    const double u = S[c] + t[c];
+                    C[c] += (fabs(S[c]) >= fabs(t[c])) ? (S[c] - u) + t[c] : (t[c] - u) + S[c];
+                    S[c] = u;
+                }
+            }
+        }
+        F[k] = S[0] + C[0]; F[nidx + k] = S[1] + C[1]; F[2 * (size_t)nidx + k] = S[2] + C[2];
+    }
+    (void)nthreads;
+}
+
+void orc_set_ion_ids(orc_sim* s, const uint64_t* ids, int n) {
+    free(s->ion_ids);
+    s->ion_ids = NULL;
+    s->n_ion_ids = 0;
+    if (!ids || n <= 0) return;
+    s->ion_ids = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+    memcpy(s->ion_ids, ids, sizeof(uint64_t) * (size_t)n);
+    s->n_ion_ids = n;
 }
 
 void orc_forces_raw(int N, double L, double lDeb, const double* R, size_t ld, double* F, int nthreads) {
@@ -881,7 +932,8 @@ void orc_qstep(orc_sim* s) {
 #endif
             for (int i = 0; i < s->N; i++) {
                 rngsrc g; memset(&g, 0, sizeof(g));
-                g.mode = 1; g.seed = s->p.seed; g.job = s->p.job; g.ion = (uint64_t)i; g.qidx = s->qidx;
+                g.mode = 1; g.seed = s->p.seed; g.job = s->p.job; g.qidx = s->qidx;
+                g.ion = (s->ion_ids && i < s->n_ion_ids) ? s->ion_ids[i] : (uint64_t)i;
                 if (s->p.qt_model != 0) qstep_ion_pump(s, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
                 else qstep_ion(s, s->t, expDet, s->psi + (size_t)24 * i, &s->V[i], &s->tPart[i], &g);
             }

@@ -96,6 +96,13 @@ void   orc_forces_raw(int N, double L, double lDeb, const double* R, size_t ld, 
 /* owner-computes slab [lo,hi) of the same (for the sharding partition-invariance tests) */
 void   orc_forces_rows(int N, int lo, int hi, double L, double lDeb, const double* R, size_t ld,
                        double* F, int nthreads);
+/* rows idx[0..nidx) of the same pair terms, compensated (Neumaier) sum, F is [3][nidx] (sampled-ion
+ * checks at large N) */
+void   orc_forces_index(int N, double L, double lDeb, const double* R, size_t ld, const int* idx, int nidx,
+                        double* F, int nthreads);
+/* Philox ion key of local ion i = ids[i] (default i): a subset of a large system's ions run by the
+ * oracle draws the same uniforms as the full system */
+void   orc_set_ion_ids(orc_sim* s, const uint64_t* ids, int n);
 /* SpeedUp:244-281 Epotential() (serial, reference order) */
 double orc_epotential(orc_sim* s);
 double orc_epotential_raw(int N, double L, double lDeb, const double* R, size_t ld);

@@ -75,6 +75,9 @@ def lib():
         L.orc_forces_raw.argtypes = [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t, _dp, C.c_int]
         L.orc_forces_rows.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, _dp,
                                       C.c_size_t, _dp, C.c_int]
+        L.orc_forces_index.argtypes = [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t,
+                                       C.POINTER(C.c_int), C.c_int, _dp, C.c_int]
+        L.orc_set_ion_ids.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
         L.orc_epotential.restype = C.c_double
         L.orc_epotential.argtypes = [C.c_void_p]
         L.orc_epotential_raw.restype = C.c_double
@@ -246,6 +249,12 @@ class OracleSim:
     def set_qt_constants(self, dtQ, gamToE, pv2q, r):
         lib().orc_set_qt_constants(self.h, dtQ, gamToE, pv2q, r)
 
+    def set_ion_ids(self, ids):
+        """Philox ion key of local ion i = ids[i]: a sampled subset of a larger system draws the
+        uniforms its ions draw in the full system"""
+        self._ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        lib().orc_set_ion_ids(self.h, self._ids.ctypes.data_as(C.POINTER(C.c_uint64)), len(self._ids))
+
     def qstep_ion(self, t, psi, vx, tPart, u):
         psi = np.ascontiguousarray(psi, dtype=np.float64).copy()
         vxc = C.c_double(vx); tp = C.c_double(tPart)
@@ -268,6 +277,16 @@ def forces_rows(R, lo, hi, L, lDeb, nthreads=1):
     N = R.shape[1]
     F = np.zeros((3, N))
     lib().orc_forces_rows(N, lo, hi, L, lDeb, _p(R), N, _p(F), nthreads)
+    return F
+
+
+def forces_index(R, idx, L, lDeb, nthreads=1):
+    """F[3][len(idx)] of the ions idx over all j (SpeedUp:192-236), for sampled-row checks"""
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    N = R.shape[1]
+    ii = np.ascontiguousarray(idx, dtype=np.int32)
+    F = np.zeros((3, len(ii)))
+    lib().orc_forces_index(N, L, lDeb, _p(R), N, ii.ctypes.data_as(C.POINTER(C.c_int)), len(ii), _p(F), nthreads)
     return F
 
 

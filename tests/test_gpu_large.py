@@ -1,0 +1,121 @@
+"""The HIP path at BASELINE.json's large configurations (C3, C4, C5), checked against
+the oracle on sampled ions (the full O(N^2) oracle is hours at N = 1e6).
+
+  C3  N0 = 100,000  MD-only, Ge = 1/12 (kappa = 0.5)      Newton-3 block pairs, one GPU
+  C4  N0 = 1,000,000 MD-only, Ge = 1/12                  Newton-3 block pairs, one GPU (~12 GB of slots)
+  C5  N0 = 250,000  full MDQT, detuningDP = +1           Newton-3 block pairs + one fused 25-substep launch
+
+Per config:
+  * forces() on the reference's init() state (C5: after 20 MD steps, so that the interval below
+    has quantum jumps): GPU F of ~1,000 sampled ions (one per 1,024-ion
+    block, the ragged last tile, both sides of the NB/2 half-shell boundary, random others) against
+    the oracle's rows over all j (orc_forces_index: the reference's pair terms, compensated sum so
+    that the check sees the GPU's rounding, not N eps of the oracle's own);
+    gate: max |dF| <= 1e-12 x max |F| over the sample (stated tolerance: the GPU sums N/2 terms per
+    ion through ~NB/2 block slots; measured ~1e-14);
+  * momentum: |sum_i F_i| <= 1e-9 x mean |F_i| (each distinct pair is evaluated once, +f and -f;
+    only the summation rounding of ~N^2/2 terms remains);
+  * MD-only (C3, C4): one MD step's 25 drift substeps with F frozen are exact arithmetic (step(),
+    SpeedUp:356-430): sampled ions equal the oracle's step() bit for bit;
+  * C5: one fused 25-substep launch (step()+qstep(), SpeedUp:356-717) with the GPU's F frozen on the
+    sampled ions against the oracle run on those ions alone (ions are independent between force
+    calls; the oracle draws the same Philox uniforms keyed by the global ion id):
+    tPart (jump pattern) and R, V, psi within the per-qstep gates.
+"""
+import os
+
+import numpy as np
+import pytest
+
+CONFIGS = {
+    "C3": dict(N0=100000, Ge=1.0 / 12, qt_enabled=0),
+    "C5": dict(N0=250000, detuningDP=1.0, qt_enabled=1),
+    "C4": dict(N0=1000000, Ge=1.0 / 12, qt_enabled=0),
+}
+SEED = 12346
+
+
+def threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def sample_ions(N, nsamp, rng):
+    """one ion per 1,024-ion block, the ragged last tile, the blocks around NB/2, random others"""
+    NB = (N + 1023) // 1024
+    idx = [b * 1024 + int(rng.integers(0, min(1024, N - b * 1024))) for b in range(NB)]
+    idx += list(range(max(0, N - 64), N))                          # ragged last tile
+    for b in (NB // 2 - 1, NB // 2, NB // 2 + 1, NB - 1, 0):       # half-shell boundary blocks
+        if 0 <= b < NB:
+            lo = b * 1024
+            idx += list(range(lo, min(N, lo + 8))) + list(range(max(lo, min(N, lo + 1024) - 8), min(N, lo + 1024)))
+    rest = nsamp - len(set(idx))
+    if rest > 0:
+        idx += list(rng.integers(0, N, rest))
+    return np.array(sorted(set(int(i) for i in idx)), dtype=np.int64)
+
+
+def test_forces_index_matches_full_rows(orc):
+    """CPU: the indexed, compensated rows equal the plain rows to rounding (no GPU)"""
+    rng = np.random.default_rng(3)
+    L = 24.474785
+    R = rng.uniform(0, L, (3, 900))
+    idx = np.array([0, 1, 63, 64, 450, 899])
+    A = orc.forces_index(R, idx, L, 1.8257418583505538, nthreads=2)
+    B = orc.forces_raw(R, L, 1.8257418583505538)[:, idx]
+    assert np.abs(A - B).max() <= 1e-13 * np.abs(B).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["C3", "C5", "C4"])
+def test_large_config_forces_and_interval(cfg, orc):
+    import mdqtplasmasims_amd as M
+    if M.device_count() < 1:
+        pytest.fail("no GPU visible to the gpu-marked tests")
+    kw = dict(CONFIGS[cfg])
+    qt = kw["qt_enabled"]
+    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **kw).init()
+    if qt:
+        s.md_steps(20)                                  # P populations build up: quantum jumps occur
+    N = s.N
+    assert s.const("force_scheme") == 3                 # Newton-3 block pairs above 65,536 ions
+    L, lDeb = s.const("L"), s.const("lDeb")
+    s.forces()
+    st = s.get_state()
+    R, F = st["R"], st["F"]
+    rng = np.random.default_rng(11)
+    idx = sample_ions(N, 1024 if N < 500000 else 640, rng)
+    G = orc.forces_index(R, idx, L, lDeb, nthreads=threads())
+    err = np.abs(F[:, idx] - G).max() / np.abs(G).max()
+    print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}")
+    assert err <= 1e-12
+    mom = np.abs(F.sum(axis=1)).max() / (np.abs(F).sum() / N)
+    print(f"{cfg}: |sum F| / mean|F| = {mom:.3e}")
+    assert mom <= 1e-9
+    # one MD interval (25 substeps) with F frozen, sampled ions vs the oracle on those ions alone
+    ratio = int(s.const("plasmaToQuantumTimestepRatio"))
+    q0 = s.qstep_index
+    s.substeps(ratio)
+    after = s.get_state()
+    o = orc.OracleSim(seed=SEED, job=1, rng_mode=1, nthreads=threads(), **kw)
+    assert o.const("L") == L
+    n = len(idx)
+    o.set_state(R[:, idx], st["V"][:, idx], st["psi"][idx], st["tPart"][idx], st["t"])
+    o.set_forces(F[:, idx])
+    o.set_ion_ids(idx)
+    o.qstep_index = q0
+    o.substeps(ratio)
+    b = o.get_state()
+    assert b["t"] == after["t"]
+    if not qt:
+        assert np.array_equal(after["R"][:, idx], b["R"]) and np.array_equal(after["V"][:, idx], b["V"])
+    else:
+        assert np.abs(after["tPart"][idx] - b["tPart"]).max() <= 1e-15        # same jump substeps
+        dR = np.abs(after["R"][:, idx] - b["R"]).max()
+        dV = np.abs(after["V"][:, idx] - b["V"]).max()
+        dpsi = np.abs(after["psi"][idx] - b["psi"]).max()
+        print(f"{cfg}: interval of {ratio} substeps on {n} ions: max|dR| {dR:.2e} |dV| {dV:.2e} |dpsi| {dpsi:.2e}, "
+              f"ions that jumped {int((b['tPart'] < 0.999 * ratio * s.const('quantumTimestep')).sum())}")
+        assert dR <= 1e-12 and dV <= 1e-13 and dpsi <= 1e-11
+        assert (b["tPart"] < 0.999 * ratio * s.const("quantumTimestep")).sum() >= 3   # the jump branch ran
+    o.close()
+    s.close()

@@ -103,6 +103,15 @@ struct mdqt_ctx {
     double* dSlots = nullptr;      // its slots [nd + R][3][Npad]
     size_t capSlots = 0;
     double* dFr = nullptr;         // sharded n3b: this rank's dense partial forces [world][3][S]
+    // spatial order of the n3b scheme (mdqt_sort.hip; option "force_sort", default on)
+    int sort_mode = 1;             // 0 off, 1 sorted + tile-pair skipping, 2 sorted, nothing skipped (tests)
+    uint32_t* dKeys = nullptr;     // [2][N] Morton keys, sorted keys
+    int* dIon = nullptr;           // [2][N] identity, sorted index -> ion
+    void* dSortTmp = nullptr;
+    size_t sortTmpBytes = 0;
+    double* dRs = nullptr;         // [3][Npad] positions in sorted order
+    double* dBoxes = nullptr;      // [6][T] tile boxes
+    int capSortN = 0;
     bool rs_pending = false;       // in-process group: F = sum of the ranks' dFr chunks, not formed yet
     const double** dPeerParts = nullptr;   // device array of the group's dFr pointers
     int nslots = 0, npairs = 0, capPairs = 0;
@@ -542,6 +551,21 @@ static int ensure_aux(mdqt_ctx* s) {
         }
         if (s->p.world_size > 1 && !s->dFr)
             HIPCHK(hipMalloc(&s->dFr, (size_t)s->capS * 3 * s->p.world_size * sizeof(double)));
+        if (s->sort_mode && s->N > s->capSortN) {
+            for (void* q : {(void*)s->dKeys, (void*)s->dIon, s->dSortTmp, (void*)s->dRs, (void*)s->dBoxes})
+                if (q) HIPCHK(hipFree(q));
+            s->dKeys = nullptr; s->dIon = nullptr; s->dSortTmp = nullptr; s->dRs = nullptr; s->dBoxes = nullptr;
+            const int Nc = s->N;
+            const int Tc = (Nc + 63) / 64;
+            HIPCHK(hipMalloc(&s->dKeys, (size_t)2 * Nc * sizeof(uint32_t)));
+            HIPCHK(hipMalloc(&s->dIon, (size_t)2 * Nc * sizeof(int)));
+            s->sortTmpBytes = spatial_order_tmp_bytes(Nc);
+            if (!s->sortTmpBytes) return fail("radix sort scratch size query failed");
+            HIPCHK(hipMalloc(&s->dSortTmp, s->sortTmpBytes));
+            HIPCHK(hipMalloc(&s->dRs, (size_t)3 * Tc * 64 * sizeof(double)));
+            HIPCHK(hipMalloc(&s->dBoxes, (size_t)6 * Tc * sizeof(double)));
+            s->capSortN = Nc;
+        }
     }
     if (s->use_n3 && s->npairs > 0) {
         if (s->npairs > s->capPairs) {
@@ -570,6 +594,10 @@ static void free_device(mdqt_ctx* s) {
     s->capPairs = 0;
     if (s->dSlots) (void)hipFree(s->dSlots);
     if (s->dFr) (void)hipFree(s->dFr);
+    for (void* q : {(void*)s->dKeys, (void*)s->dIon, s->dSortTmp, (void*)s->dRs, (void*)s->dBoxes})
+        if (q) (void)hipFree(q);
+    s->dKeys = nullptr; s->dIon = nullptr; s->dSortTmp = nullptr; s->dRs = nullptr; s->dBoxes = nullptr;
+    s->capSortN = 0;
     if (s->dPeerParts) (void)hipFree((void*)s->dPeerParts);
     s->dSlots = nullptr; s->dFr = nullptr; s->dPeerParts = nullptr;
     s->capSlots = 0;
@@ -715,6 +743,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "kRat")) return s->kRat;
     if (!strcmp(n, "force_segments")) return s->nseg;
     if (!strcmp(n, "force_scheme")) return s->use_n3b ? 3 : s->use_n3 ? 2 : 1;
+    if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
     return NAN;
@@ -1029,6 +1058,15 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         a.Rall = s->dR; a.slots = s->dSlots; a.S = s->S;
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
         a.micGuard = c.micGuard; a.guard = c.guard;
+        a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr;
+        if (s->sort_mode) {                        // Morton order + tile boxes (mdqt_sort.hip)
+            SortArgs o;
+            o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
+            o.keys = s->dKeys; o.keys2 = s->dKeys + s->N; o.ion = s->dIon; o.perm = s->dIon + s->N;
+            o.tmp = s->dSortTmp; o.tmp_bytes = s->sortTmpBytes; o.Rs = s->dRs; o.boxes = s->dBoxes;
+            HIPCHK(launch_spatial_order(o, s->stream));
+            a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes;
+        }
         const int W = s->p.world_size;
         HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream));
         if (W > 1) {
@@ -1582,6 +1620,12 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (settle_forces(s)) return -1;
         s->scheme_opt = value;
         choose_segments(s);
+        return ensure_aux(s);
+    }
+    if (!strcmp(name, "force_sort")) {                 // Newton-3 blocks: Morton order + tile-pair skipping
+        if (value < 0 || value > 2) return fail("force_sort must be 0 (off), 1 (on) or 2 (sorted, no skipping)");
+        if (settle_forces(s)) return -1;
+        s->sort_mode = value;
         return ensure_aux(s);
     }
     if (!strcmp(name, "qt_enabled")) {                 // pump window of the tagging programs

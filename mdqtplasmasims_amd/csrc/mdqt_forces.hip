@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restric
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int c = blockIdx.y;
     if (i >= nrows || c >= ncomp) return;
-    F[(size_t)c * S + i] = seg_sum(Fpart + (size_t)c * S + i, (size_t)3 * S, nseg);
+    F[(size_t)c * S + i] = slot_sum16(Fpart + (size_t)c * S + i, (size_t)3 * S, nseg);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -385,11 +385,33 @@ void k_pairs_n3b(N3BArgs a) {
     const int I = P * BW + q;
     const bool vI = I < T;
     const int i = I * 64 + l;
+    // positions: the sorted copy [3][Npad] (spatial order) or the gathered slabs
+    const bool srt = a.use_sort != 0;
+    const int PS = srt ? a.Npad : S;
+    auto tile_ptr = [&](int tile) { return srt ? a.Rs + tile * 64 : tile_base(a.Rall, tile, S); };
     double xi = 0., yi = 0., zi = 0., mi = 0.;
     if (vI && i < N) {
-        const double* p = tile_base(a.Rall, I, S) + l;
-        xi = p[0]; yi = p[S]; zi = p[2 * S]; mi = 1.;
+        const double* p = tile_ptr(I) + l;
+        xi = p[0]; yi = p[PS]; zi = p[2 * PS]; mi = 1.;
     }
+    // tile I's box (spatial order): a tile pair whose boxes are >= L/2 apart in the minimum image
+    // has no pair inside the cutoff (SpeedUp:222) and adds exact zeros: skipped whole
+    double bc[3] = {0., 0., 0.}, bh[3] = {0., 0., 0.};
+    if (srt && vI)
+#pragma unroll
+        for (int c3 = 0; c3 < 3; ++c3) { bc[c3] = a.boxes[(size_t)c3 * T + I]; bh[c3] = a.boxes[(size_t)(3 + c3) * T + I]; }
+    const double rc2 = a.Rcut * a.Rcut;
+    auto far_apart = [&](int J) {
+        double g2 = 0.;
+#pragma unroll
+        for (int c3 = 0; c3 < 3; ++c3) {
+            double d = bc[c3] - a.boxes[(size_t)c3 * T + J];
+            d = fma(-__builtin_rint(d * c.invL), a.L, d);
+            const double gap = fabs(d) - (bh[c3] + a.boxes[(size_t)(3 + c3) * T + J]);
+            g2 = gap > 0. ? fma(gap, gap, g2) : g2;
+        }
+        return g2 > rc2;
+    };
     double fx = 0., fy = 0., fz = 0.;
     double* ax = accj[q][0];
     double* ay = accj[q][1];
@@ -398,14 +420,15 @@ void k_pairs_n3b(N3BArgs a) {
     for (int db = d0; db < d1; ++db) {
         if (!(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2) continue;   // the other half covers it
         const int Q = (P + db) % a.NB;
+        double bx = 0., by = 0., bz = 0.;          // this block distance's i partial (3-level blocking)
         for (int b = 0; b < BW; ++b) {
             const int J = Q * BW + b;
             if (J >= T) break;
             if (q == 0) {                           // stage J (twice over)
                 const int j = J * 64 + l;
                 const bool vj = j < N;
-                const double* p = tile_base(a.Rall, J, S) + l;
-                const double xj = vj ? p[0] : 0., yj = vj ? p[S] : 0., zj = vj ? p[2 * S] : 0.;
+                const double* p = tile_ptr(J) + l;
+                const double xj = vj ? p[0] : 0., yj = vj ? p[PS] : 0., zj = vj ? p[2 * PS] : 0.;
                 pj[0][l] = xj; pj[0][l + 64] = xj;
                 pj[1][l] = yj; pj[1][l + 64] = yj;
                 pj[2][l] = zj; pj[2][l + 64] = zj;
@@ -414,12 +437,18 @@ void k_pairs_n3b(N3BArgs a) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
             __syncthreads();
-            if (vI && (db > 0 || J >= I)) {
+            if (vI && (db > 0 || J >= I) && !(a.use_sort == 1 && far_apart(J))) {
                 const bool diag = (db == 0 && J == I);
+                // blocked i accumulation: the tile pair's 64 steps into a fresh sum, those into the
+                // block distance's sum, those into the run's (a run is ~1e5 pair terms at N = 1e6;
+                // in spatial order they arrive in coherent groups, and one serial chain would
+                // carry their rounding: momentum |sum F| / mean |F| 1.8e-8 -> 1e-10 at C4)
+                double tx = 0., ty = 0., tz = 0.;
                 if (ragN && (I == T - 1 || J == T - 1))
-                    n3b_pair<VARIANT, GUARD, true>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+                    n3b_pair<VARIANT, GUARD, true>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
                 else
-                    n3b_pair<VARIANT, GUARD, false>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+                    n3b_pair<VARIANT, GUARD, false>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
+                bx += tx; by += ty; bz += tz;
             }
             __syncthreads();
             if (q < 3) {                            // j side of J's rows -> j-slot db
@@ -430,6 +459,7 @@ void k_pairs_n3b(N3BArgs a) {
             }
             __syncthreads();
         }
+        fx += bx; fy += by; fz += bz;
     }
     if (vI) {                                       // i side -> i-slot nd + run
         double* o = a.slots + (size_t)(a.nd + run) * plane + i;
@@ -454,8 +484,9 @@ __global__ __launch_bounds__(256) void k_n3b_reduce(N3BArgs a, double* __restric
     }
     if (B >= a.Plo && B < a.Phi)
         for (int r = 0; r < a.R; ++r) acc = acc + p[(size_t)(a.nd + r) * plane];
-    const int w = g / a.S;
-    out[(size_t)w * 3 * a.S + (size_t)k * a.S + (g - w * a.S)] = acc;
+    const int ion = a.use_sort ? a.perm[g] : g;     // spatial order: scatter back to the ion's place
+    const int w = ion / a.S;
+    out[(size_t)w * 3 * a.S + (size_t)k * a.S + (ion - w * a.S)] = acc;
 }
 
 // in-process rank group (tests): F of rank `rank` = sum over ranks r = 0.. of part[r]'s chunk

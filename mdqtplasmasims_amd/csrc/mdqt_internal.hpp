@@ -178,24 +178,24 @@ __device__ __forceinline__ double rsq3(double x) {
 }
 
 // e^x for x = -r/lDeb in [-L/(2 lDeb), 0] (no overflow, no subnormal results for any box the
-// reference runs): Cody-Waite x = n ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial
-// (truncation < 5e-18 relative) in FMA Horner form, exponent shift.  <= 1 ulp vs glibc.
+// reference runs): Cody-Waite x = n ln2 + r, |r| <= ln2/2, then the degree-11 minimax polynomial
+// of e^r on [-ln2/2, ln2/2] (relative approximation error 3.1e-18; Remez exchange in 60-digit
+// arithmetic, coefficients rounded to double) in FMA Horner form, exponent shift: <= 1.1 ulp vs
+// the exact value over the range (two FMAs fewer per pair than a degree-13 Taylor polynomial).
 __device__ __forceinline__ double exp_neg(double x) {
     const double n = __builtin_rint(x * 1.4426950408889634);
     double r = fma(-n, 0x1.62e42fefa39efp-1, x);
     r = fma(-n, 0x1.abc9e3b39803fp-56, r);
-    double p = 1.6059043836821613e-10;               // 1/13!
-    p = fma(p, r, 2.08767569878681e-09);
-    p = fma(p, r, 2.505210838544172e-08);
-    p = fma(p, r, 2.755731922398589e-07);
-    p = fma(p, r, 2.7557319223985893e-06);
-    p = fma(p, r, 2.48015873015873e-05);
-    p = fma(p, r, 0.0001984126984126984);
-    p = fma(p, r, 0.001388888888888889);
-    p = fma(p, r, 0.008333333333333333);
-    p = fma(p, r, 0.041666666666666664);
-    p = fma(p, r, 0.16666666666666666);
-    p = fma(p, r, 0.5);
+    double p = 2.4994304884817207e-08;
+    p = fma(p, r, 2.7632293279459877e-07);
+    p = fma(p, r, 2.7557622530872255e-06);
+    p = fma(p, r, 2.4801486521427463e-05);
+    p = fma(p, r, 0.00019841269432679237);
+    p = fma(p, r, 0.0013888888951223987);
+    p = fma(p, r, 0.00833333333355927);
+    p = fma(p, r, 0.04166666666649277);
+    p = fma(p, r, 0.1666666666666617);
+    p = fma(p, r, 0.5000000000000018);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
     return ldexp(p, (int)n);
@@ -215,6 +215,29 @@ __device__ __forceinline__ double seg_sum(const double* __restrict__ p, size_t s
     for (int q = 0; q < 8; ++q)
         if (s + q < nseg) a[q] += p[(size_t)(s + q) * stride];
     return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// THE canonical sum of the nseg force partials of one ion component (MDQT engine): sixteen
+// strided partial sums, q_k = (((0 + p[k]) + p[k + 16]) + p[k + 32]) + ... (k = 0..15, the
+// slots < nseg), combined by the lane kernel's DPP tree
+//   (((q0 + q1) + (q2 + q3)) + ((q4 + q5) + (q6 + q7))) + (((q8 + q9) + ...) + ((q12 + q13) + (q14 + q15))).
+// The lane-per-state QT kernel evaluates it distributed over an ion's 16 lanes (lane k: q_k, all
+// of its loads in flight at once), the thread-per-ion kernels and k_reduce_segments serially:
+// the same operations, so every consumer of the partials sees the same F bit for bit.
+__device__ __forceinline__ double slot_sum16_partial(const double* __restrict__ p, size_t stride, int nseg, int k) {
+    double q = 0.;
+    for (int s = k; s < nseg; s += 16) q = q + p[(size_t)s * stride];
+    return q;
+}
+__device__ __forceinline__ double tree16_sum(const double* q) {
+    return (((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]))) +
+           (((q[8] + q[9]) + (q[10] + q[11])) + ((q[12] + q[13]) + (q[14] + q[15])));
+}
+__device__ __forceinline__ double slot_sum16(const double* __restrict__ p, size_t stride, int nseg) {
+    double q[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) q[k] = slot_sum16_partial(p, stride, nseg, k);
+    return tree16_sum(q);
 }
 
 // Newton-3 tile-pair scheme (world_size 1): one workgroup of 4 waves per 64x64 tile pair
@@ -241,7 +264,26 @@ struct N3BArgs {
     int Plo, Phi;       // this rank's blocks
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;
+    // spatial order (mdqt_sort.hip): tiles are 64 consecutive ions of the Morton order
+    int use_sort;       // 1: positions from Rs, slots by sorted index, tile pairs beyond L/2 skipped;
+                        // 2: the same order, nothing skipped (tests: bit-identical to 1)
+    const double* Rs;   // [3][Npad] positions in sorted order
+    const int* perm;    // sorted index -> ion
+    const double* boxes;// [6][T]: tile center (x, y, z), half extents (x, y, z)
 };
+struct SortArgs {
+    const double* Rall; // gathered positions [world][3][S]
+    int N, S, Npad;
+    double L;
+    uint32_t *keys, *keys2;  // [N] Morton keys, sorted keys
+    int *ion, *perm;         // [N] identity, sorted index -> ion
+    void* tmp;               // hipCUB radix-sort scratch
+    size_t tmp_bytes;
+    double* Rs;              // out [3][Npad]
+    double* boxes;           // out [6][T]
+};
+hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s);
+size_t spatial_order_tmp_bytes(int N);
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 

@@ -284,10 +284,10 @@ __global__ __launch_bounds__(256) void k_substeps(SubstepArgs a) {
     double x = a.R[i], y = a.R[S + i], z = a.R[2 * S + i];
     double vx = a.V[i], vy = a.V[S + i], vz = a.V[2 * S + i];
     double fx, fy, fz;
-    if (a.nseg > 1) {        // forces() left segment partials: canonical sum (seg_sum)
-        fx = seg_sum(a.Fpart + i, (size_t)3 * S, a.nseg);
-        fy = seg_sum(a.Fpart + S + i, (size_t)3 * S, a.nseg);
-        fz = seg_sum(a.Fpart + 2 * S + i, (size_t)3 * S, a.nseg);
+    if (a.nseg > 1) {        // forces() left segment partials: canonical sum (slot_sum16)
+        fx = slot_sum16(a.Fpart + i, (size_t)3 * S, a.nseg);
+        fy = slot_sum16(a.Fpart + S + i, (size_t)3 * S, a.nseg);
+        fz = slot_sum16(a.Fpart + 2 * S + i, (size_t)3 * S, a.nseg);
         a.F[i] = fx; a.F[S + i] = fy; a.F[2 * S + i] = fz;
     } else {
         fx = a.F[i]; fy = a.F[S + i]; fz = a.F[2 * S + i];
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
     if (a.nseg > 1) {        // lanes 0..2 sum component k of the segment partials, then share
         double fk = 0.;
         if (k < 3) {
-            fk = seg_sum(a.Fpart + (size_t)k * S + i, (size_t)3 * S, a.nseg);
+            fk = slot_sum16(a.Fpart + (size_t)k * S + i, (size_t)3 * S, a.nseg);
             if (store) a.F[(size_t)k * S + i] = fk;
         }
         fx = gat(fk, g0 + 0); fy = gat(fk, g0 + 1); fz = gat(fk, g0 + 2);

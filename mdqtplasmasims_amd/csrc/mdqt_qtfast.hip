@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
         P[c] = a.R[(size_t)c * S + i];
         Vv[c] = a.V[(size_t)c * S + i];
         if (a.nseg > 1) {
-            Fv[c] = seg_sum(a.Fpart + (size_t)c * S + i, (size_t)3 * S, a.nseg);
+            Fv[c] = slot_sum16(a.Fpart + (size_t)c * S + i, (size_t)3 * S, a.nseg);
             a.F[(size_t)c * S + i] = Fv[c];
         } else {
             Fv[c] = a.F[(size_t)c * S + i];
@@ -302,8 +302,16 @@ __device__ unsigned long long g_qt_stamps[6 * 4096];
 #define QT_STAMP(slot, v) ((void)0)
 #endif
 
+#ifndef MDQT_LANE_WPE
+#define MDQT_LANE_WPE 0
+#endif
+#if MDQT_LANE_WPE > 0
+#define LANE_WPE_ATTR __attribute__((amdgpu_waves_per_eu(MDQT_LANE_WPE, MDQT_LANE_WPE)))
+#else
+#define LANE_WPE_ATTR
+#endif
 template <bool DPPX>
-__global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
+__global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
 #if defined(MDQT_EXPT_QTSTAMPS)
     unsigned long long st_[6];
 #endif
@@ -328,16 +336,36 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
     const double kw0 = tab->kw[0][k], kw1 = tab->kw[1][k], kw2 = tab->kw[2][k];
     const double cphi = tab->cphi, DT2 = tab->dt2;
     const double kmask = (c == 0) ? 1. : 0.;
+    // Prologue: every load is issued before any is consumed (one memory round trip), and the
+    // lane-parallel Philox draws below run while they are in flight.
     double p = a.R[(size_t)c * S + i], v = a.V[(size_t)c * S + i], f;
-    if (a.nseg > 1) {
-        f = seg_sum(a.Fpart + (size_t)c * S + i, (size_t)3 * S, a.nseg);
-        if (store && owner) a.F[(size_t)c * S + i] = f;
-    } else {
-        f = a.F[(size_t)c * S + i];
-    }
     double tPart = a.tPart[i];
     cxd w = {0., 0.};
     if (a.do_qt && st < NS) w = {a.psi[(size_t)(2 * st) * S + i], a.psi[(size_t)(2 * st + 1) * S + i]};
+    const int nseg = a.nseg;
+    // F: the canonical slot_sum16 distributed over the ion's 16 lanes — lane k forms the strided
+    // partial q_k of all three components (its loads issued together, 4 slots per round), the
+    // DPP tree combines them in slot_sum16's order
+    double qf[3] = {0., 0., 0.};
+    if (nseg > 1) {
+        const double* base_p = a.Fpart + i;
+        const size_t plane = (size_t)3 * S;
+        for (int s0 = k; s0 < nseg; s0 += 64) {
+            double t[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int sl = s0 + 16 * u;
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) t[u][cc] = sl < nseg ? base_p[(size_t)sl * plane + (size_t)cc * S] : 0.;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) qf[cc] = qf[cc] + t[u][cc];
+        }
+    } else {
+        f = a.F[(size_t)c * S + i];
+    }
     const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
     const uint64_t gid = a.gid0 + (uint64_t)i;
     // per-substep constants in registers, not kernel-argument loads inside the substep loop (a
@@ -370,6 +398,11 @@ __global__ __launch_bounds__(256) void k_substeps_lanes_r(SubstepArgs a, const F
                 su[grp][s][1] = x1;
             }
         }
+    }
+    if (nseg > 1) {
+        const double fx = lane_tree16(qf[0]), fy = lane_tree16(qf[1]), fz = lane_tree16(qf[2]);
+        f = c == 0 ? fx : c == 1 ? fy : fz;
+        if (store && owner) a.F[(size_t)c * S + i] = f;
     }
     __syncthreads();
     __shared__ double2 xg[DPPX ? 1 : kLaneWG];

@@ -99,26 +99,84 @@ def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r01_v11_c2_p
     return None
 
 
+def cpu_threads():
+    """the GPU box's CPU share (16 per GPU; os.cpu_count() reports the whole machine there)"""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def cpu_baseline(params, qt, seconds, seed, job):
-    """The oracle (CPU restatement, race-free OpenMP) on a bounded sample of the same workload."""
+    """The oracle (CPU restatement, race-free OpenMP) on a bounded sample of the same workload, at
+    the box's CPU share (16 threads) and on one thread (BASELINE.md §3 asks for both)."""
     from oracle import oracle as O
     if not os.path.exists(O.LIB_PATH):
         O.build()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    o = O.OracleSim(rng_mode=1, nthreads=threads, qt_enabled=qt, seed=seed, job=job, **params).init()
-    ratio = int(o.const("plasmaToQuantumTimestepRatio"))
-    o.md_steps(1)                                  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        o.md_steps(1)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 400:
-            break
-    rate = o.N * ratio * n / el
+
+    def timed(threads, budget, cap):
+        o = O.OracleSim(rng_mode=1, nthreads=threads, qt_enabled=qt, seed=seed, job=job, **params).init()
+        ratio = int(o.const("plasmaToQuantumTimestepRatio"))
+        o.md_steps(1)                              # warm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            o.md_steps(1)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= cap:
+                break
+        N = o.N
+        o.close()
+        return N * ratio * n / el, n, ratio, N, el
+
+    threads = cpu_threads()
+    rate, n, ratio, N, el = timed(threads, seconds, 400)
+    r1, n1, _, _, el1 = timed(1, max(2.0, seconds / 3), 100)
     return {"value": rate, "unit": "particle-qsteps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} MD steps x {ratio} qsteps of the same workload (N={o.N}), oracle C "
-                      f"restatement, OpenMP {threads} threads, {el:.1f} s"}
+            "sample": f"{n} MD steps x {ratio} qsteps of the same workload (N={N}), oracle C "
+                      f"restatement, OpenMP {threads} threads, {el:.1f} s",
+            "single_thread": {"value": r1, "unit": "particle-qsteps/s", "cores": 1,
+                              "sample": f"{n1} MD steps x {ratio} qsteps, 1 thread, {el1:.1f} s"}}
+
+
+def cpu_baseline_large(cfg, seconds=6.0):
+    """CPU baseline of a large line (C3 / C5 / N = 1M; BASELINE.md §3: time a part of one MD interval
+    and extrapolate).  The race-free CPU restatement computes owner rows (each pair from both
+    sides: N(N-1) pair terms per forces()): forces_rows over a block of rows, timed, scaled to all N
+    rows; with QT on, plus one MD interval of qsteps on a sample of ions (ions are independent
+    between force calls), scaled to N.  Inputs: the reference's init() positions are replaced by
+    uniform positions of the same N and box (the cost does not depend on them)."""
+    import numpy as np
+    from oracle import oracle as O
+    if not os.path.exists(O.LIB_PATH):
+        O.build()
+    params, qt, desc = CONFIGS[cfg]
+    threads = cpu_threads()
+    o = O.OracleSim(rng_mode=1, nthreads=threads, qt_enabled=qt, seed=12346, job=1, **params)
+    L, lDeb, ratio = o.const("L"), o.const("lDeb"), int(o.const("plasmaToQuantumTimestepRatio"))
+    N = int(params["N0"])
+    R = np.random.default_rng(5).uniform(0, L, (3, N))
+    rows = max(threads * 4, int(threads * 3.7e7 * seconds / 2 / N))   # ~half the budget
+    rows = min(rows, N)
+    t0 = time.perf_counter()
+    O.forces_rows(R, 0, rows, L, lDeb, nthreads=threads)
+    t_rows = time.perf_counter() - t0
+    t_force = t_rows * N / rows
+    t_qt, nq = 0.0, 0
+    if qt:
+        nq = min(N, 20000)
+        V = np.zeros((3, nq))
+        psi = np.zeros((nq, 12, 2)); psi[:, 0, 0] = 1.0
+        o.set_state(R[:, :nq], V, psi, np.zeros(nq), 0.0)
+        o.set_forces(np.zeros((3, nq)))
+        t0 = time.perf_counter()
+        o.substeps(ratio)
+        t_qt = (time.perf_counter() - t0) * N / nq
+    o.close()
+    per_md_step = t_force + t_qt
+    units = ratio if qt else 1
+    return {"value": N * units / per_md_step, "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
+            "cores": threads, "kind": "port", "s_per_md_step": per_md_step,
+            "sample": f"forces_rows over {rows} of {N} rows ({rows * (N - 1):.3g} pair terms, {t_rows:.1f} s)"
+                      + (f" + {ratio} qsteps on {nq} ions" if qt else "")
+                      + f", extrapolated to one MD step of N={N}; oracle C restatement, OpenMP {threads} threads"}
 
 
 def child_main(args):
@@ -229,17 +287,21 @@ def main():
         f_avg = f_ms / max(nf, 1) * 1e-3
         s_avg = s_ms / max(ns, 1) * 1e-3
         if qt and s_ms >= f_ms:
-            nsub_per_launch = ratio                 # one fused launch per MD interval (ratio <= 32)
+            # substeps per fused launch: the MD interval split at MAXSUB = 32 (mdqt_internal.hpp)
+            launches = -(-ratio // 32)
+            nsub_per_launch = ratio / launches
             bytes_launch = B_Q_PER_ION * N
             ach = bytes_launch / s_avg / 1e9
             flops = F_Q_PER_QSTEP * N * nsub_per_launch
-            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(("k_substeps_lanes" if N < 98304 else "k_substeps") +
-                                                                     ("_r" if args.qt_math == 2 else "")),
-                    "kernel": ("k_substeps_lanes" if N < 98304 else "k_substeps") +
-                              ("_r" if args.qt_math == 2 else "") + " (fused 25 x step+qstep)",
+            kname = ("k_substeps_lanes" if N < 98304 else "k_substeps") + ("_r" if args.qt_math == 2 else "")
+            # The fused QT launch is bound by neither roof: one wave per SIMD runs a dependent chain of
+            # ~330 VALU instructions per substep — "latency", with both fractions given.
+            roof = {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname),
+                    "kernel": f"{kname} (fused {nsub_per_launch:g} x step+qstep)",
                     "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
-                    "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS}
+                    "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS,
+                    "hbm_frac": ach / HBM_PEAK_GBS}
         else:
             pairs = N * (N - 1) / 2.0
             flops = W_F_PER_PAIR * pairs
@@ -263,7 +325,9 @@ def main():
             "data": "synthetic (reference init(): drand48 positions + random S superposition, seed 12345+job)",
             "config": {"workload": desc, "N": N, "md_steps": args.steps, "qsteps_per_md_step": ratio,
                        "particle_md_steps_per_s": value / ratio,
-                       "parallelism": "replicas" if world > 1 else "single",
+                       "parallelism": ("replicas: one independent C2 system per GPU (job = rank + 1, like the "
+                                       "reference's SLURM array); not one sharded system — that is the "
+                                       "'sharded' / 'sharded_1m' lines") if world > 1 else "single",
                        "rng": "philox4x32-10", "kernel_ms": {"force_total": f_ms, "force_launches": nf,
                                                             "substeps_total": s_ms, "substep_launches": ns}},
             "roofline": roof,
@@ -297,12 +361,20 @@ def main():
                     dist.barrier()
         return sharded_run(cfg, steps, rank, world, local, dist, barrier)
 
+    cpu_large = world == 1 and not args.no_cpu_baseline
+
+    def with_cpu(cfg, res):
+        if cpu_large and rank == 0 and res is not None:
+            res["cpu_baseline"] = cpu_baseline_large(cfg)
+        return res
+
     if args.md_only_config != "none":
-        dog.run("md_only_" + args.md_only_config, lambda: sharded(args.md_only_config, args.sharded_steps))
+        dog.run("md_only_" + args.md_only_config,
+                lambda: with_cpu(args.md_only_config, sharded(args.md_only_config, args.sharded_steps)))
     if args.sharded_config != "none":
-        dog.run("sharded", lambda: sharded(args.sharded_config, args.sharded_steps))
+        dog.run("sharded", lambda: with_cpu(args.sharded_config, sharded(args.sharded_config, args.sharded_steps)))
     if args.million_config != "none":
-        dog.run("sharded_1m", lambda: sharded(args.million_config, args.million_steps))
+        dog.run("sharded_1m", lambda: with_cpu(args.million_config, sharded(args.million_config, args.million_steps)))
     dog.finish()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -1059,7 +1059,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
         a.micGuard = c.micGuard; a.guard = c.guard;
         a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr;
-        if (s->sort_mode) {                        // Morton order + tile boxes (mdqt_sort.hip)
+        if (s->sort_mode) {                        // Hilbert order + tile boxes (mdqt_sort.hip)
             SortArgs o;
             o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
             o.keys = s->dKeys; o.keys2 = s->dKeys + s->N; o.ion = s->dIon; o.perm = s->dIon + s->N;
@@ -1622,7 +1622,7 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         choose_segments(s);
         return ensure_aux(s);
     }
-    if (!strcmp(name, "force_sort")) {                 // Newton-3 blocks: Morton order + tile-pair skipping
+    if (!strcmp(name, "force_sort")) {                 // Newton-3 blocks: Hilbert order + tile-pair skipping
         if (value < 0 || value > 2) return fail("force_sort must be 0 (off), 1 (on) or 2 (sorted, no skipping)");
         if (settle_forces(s)) return -1;
         s->sort_mode = value;

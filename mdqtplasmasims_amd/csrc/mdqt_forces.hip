@@ -375,7 +375,8 @@ void k_pairs_n3b(N3BArgs a) {
     __shared__ double pj[3][128];
     __shared__ double mj[128];
     __shared__ double accj[BW][3][128];
-    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __shared__ double irun[BW][3][64];
+    const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;   // q: wave-uniform
     const int P = a.Plo + (int)blockIdx.x / a.R;
     const int run = (int)blockIdx.x % a.R;
     const int d0 = run * a.runlen, d1 = min(a.nd, d0 + a.runlen);
@@ -412,7 +413,10 @@ void k_pairs_n3b(N3BArgs a) {
         }
         return g2 > rc2;
     };
-    double fx = 0., fy = 0., fz = 0.;
+    // the run's i accumulator lives in LDS (read and written once per block distance) so that
+    // the three-level blocking fits the 64-VGPR budget of two 16-wave workgroups per CU
+    double* fi = irun[q][0];
+    fi[l] = 0.; fi[64 + l] = 0.; fi[128 + l] = 0.;
     double* ax = accj[q][0];
     double* ay = accj[q][1];
     double* az = accj[q][2];
@@ -459,11 +463,11 @@ void k_pairs_n3b(N3BArgs a) {
             }
             __syncthreads();
         }
-        fx += bx; fy += by; fz += bz;
+        fi[l] += bx; fi[64 + l] += by; fi[128 + l] += bz;   // one wave's own LDS words: in order
     }
     if (vI) {                                       // i side -> i-slot nd + run
         double* o = a.slots + (size_t)(a.nd + run) * plane + i;
-        o[0] = fx; o[a.Npad] = fy; o[2 * (size_t)a.Npad] = fz;
+        o[0] = fi[l]; o[a.Npad] = fi[64 + l]; o[2 * (size_t)a.Npad] = fi[128 + l];
     }
 }
 

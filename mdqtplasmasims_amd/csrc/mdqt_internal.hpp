@@ -264,7 +264,7 @@ struct N3BArgs {
     int Plo, Phi;       // this rank's blocks
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;
-    // spatial order (mdqt_sort.hip): tiles are 64 consecutive ions of the Morton order
+    // spatial order (mdqt_sort.hip): tiles are 64 consecutive ions of the Hilbert order
     int use_sort;       // 1: positions from Rs, slots by sorted index, tile pairs beyond L/2 skipped;
                         // 2: the same order, nothing skipped (tests: bit-identical to 1)
     const double* Rs;   // [3][Npad] positions in sorted order

@@ -123,7 +123,7 @@ def test_large_config_forces_and_interval(cfg, orc):
 
 @pytest.mark.gpu
 def test_spatial_order_tile_skipping_is_exact(orc):
-    """Newton-3 blocks in Morton order (mdqt_sort.hip): skipping tile pairs whose boxes are >= L/2
+    """Newton-3 blocks in Hilbert order (mdqt_sort.hip): skipping tile pairs whose boxes are >= L/2
     apart changes nothing (they add exact zeros) — bit for bit against the same order without
     skipping; against the unsorted order the forces agree to rounding (1e-13 of max |F|)"""
     import mdqtplasmasims_amd as M

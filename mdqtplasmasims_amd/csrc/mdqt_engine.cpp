@@ -140,7 +140,8 @@ struct mdqt_ctx {
     // per-launch HIP events of the hot kernels (kind 0 = force, 1 = substeps), recorded on
     // the launch stream while timing is on; summed by mdqt_kernel_time_totals
     bool timing = false;
-    unsigned tperiod = 1, tcount[2] = {0, 0};   // bracket every tperiod-th launch of each kind
+    unsigned tperiod = 1, tcount[2] = {0, 0};   // bracket launches k = tperiod/2 mod tperiod of each kind
+                                                // (mid-period: not the first launch after a sync)
     std::vector<hipEvent_t> evpool[2];
     int evused[2] = {0, 0};
 };
@@ -413,9 +414,12 @@ static void build_constants(mdqt_ctx* s) {
     const KW kws[12] = {{1, 2, 0, 1., kS},  {0, 3, 2, 1., kS},  {1, 4, 4, -1., kS}, {0, 5, 5, -1., kS},
                         {8, 5, 8, 1., kD},  {9, 4, 11, 1., kD}, {10, 3, 14, 1., kD}, {11, 2, 17, 1., kD},
                         {6, 5, 6, -1., kD}, {7, 4, 9, -1., kD}, {8, 3, 12, -1., kD}, {9, 2, 15, -1., kD}};
+    // Every coupling edge has exactly one P endpoint (S-P and P-D edges; each P level has three),
+    // so each term sits on its P state's lane: Im(w_a conj(w_P)) = -Im(w_P conj(w_a)).  The kick
+    // is then the sum over the four P lanes — the same broadcast pattern as dp, not a 16-lane tree.
     for (const KW& w : kws)
         for (int j = 0; j < 3; ++j)
-            if (kFastCol[w.row][j] == w.col) f.kw[j][w.row] = w.sgn * (w.scale * gs[w.g]);
+            if (kFastCol[w.col][j] == w.row) f.kw[j][w.col] = -(w.sgn * (w.scale * gs[w.g]));
     f.cphi = 2. * (1. + q.kRat) * q.gamToE;
     if (p->qt_model != 0) build_pump_tables(p, q, f);
     f.dt2 = (0.5 * q.dtQ) * (0.5 * q.dtQ);
@@ -1034,7 +1038,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
     if (!s) return fail("NULL context");
     if (s->nloc == 0) return 0;
     HIPCHK(hipSetDevice(s->dev));
-    const bool tm = s->timing && (s->tcount[0]++ % s->tperiod == 0);
+    const bool tm = s->timing && (s->tcount[0]++ % s->tperiod == s->tperiod / 2);
     // timing: the Newton-3 tile kernel (one launch) records its own timestamps; the other
     // schemes (several kernels, collectives) are bracketed by events on the stream
     const bool tm_marks = tm && !s->use_n3;
@@ -1129,7 +1133,7 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             HIPCHK(launch_d48_resolve(r, s->stream));
             a.U = s->dU;
         }
-        const bool tm = s->timing && (s->tcount[1]++ % s->tperiod == 0);
+        const bool tm = s->timing && (s->tcount[1]++ % s->tperiod == s->tperiod / 2);
         hipEvent_t e0 = nullptr, e1 = nullptr;       // timing: the kernel's own timestamps
         if (tm && (take_events(s, 1, &e0, &e1))) return -1;
         if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->substep_mode, s->stream, e0, e1));

@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
             for (int k = 0; k < NS; ++k)
                 kv[k] = kick_term(w[k], w[COL[k][0]], w[COL[k][1]], w[COL[k][2]], T.kw[0][k],
                                   T.kw[1][k], T.kw[2][k]);
-            kick = tree_lanes<MODEL>(kv);
+            kick = sum_p<MODEL>(kv + 2);                 // the kick terms sit on the P lanes
             const double phi = (u * T.cphi) * tPart;
             double sn, cs;
             sincos_q<true>(phi, sn, cs);
@@ -463,7 +463,10 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
                 sincos_fast(phin, snn, csn);
             };
             if (nojump) {
-                kick = lane_tree16(kick_term(w, w0, w1, w2, kw0, kw1, kw2));
+                {                                 // kick terms on the P lanes (host table)
+                    const double kt = kick_term(w, w0, w1, w2, kw0, kw1, kw2);
+                    kick = DPPX ? lane_sum_p8(kt) : lane_sum_p(kt);
+                }
                 next_phase();
                 const cxd md = {mre, fma(mi1, u, mi0)};
                 const cxd c2 = {fma(dms, sn, c2re), fma(dmc, cs, c2im)};

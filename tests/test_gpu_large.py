@@ -139,3 +139,59 @@ def test_spatial_order_tile_skipping_is_exact(orc):
     print(f"C3 sorted vs unsorted: max|dF|/max|F| = {err:.3e}")
     assert err <= 1e-13
     s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_newton3_blocks_above_64k_local_group(world, orc):
+    """N > 65,536 (Newton-3 blocks in Hilbert order, the scheme every sharded BASELINE config uses)
+    as an in-process rank group on one MI355X: each rank evaluates its blocks' pairs for all ions,
+    the dense partials are summed in rank order (RCCL's reduce-scatter in a real group).  Stated
+    cross-world tolerance: forces within 1e-13 of world 1 (max-norm relative), positions and
+    velocities within 1e-12 after two MD steps with QT on (the rank-order sum changes rounding only)"""
+    import mdqtplasmasims_amd as M
+    from mdqtplasmasims_amd.engine import comm_init_local
+    kw = dict(N0=70000, seed=19, rng_mode=1)
+    ref = M.Simulation(**kw).init()
+    assert ref.const("force_scheme") == 3 and ref.N > 65536
+    st = ref.get_state()
+    sims = [M.Simulation(world_size=world, rank=r, **kw) for r in range(world)]
+    for s in sims:
+        s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+        assert s.const("force_scheme") == 3
+    comm_init_local(sims)
+    for s in sims:
+        s.allgather_positions()
+    for s in sims:
+        s.forces()
+    ref.forces()
+    G = ref.get_state()["F"]
+    worst = 0.0
+    for s in sims:
+        lo, hi = s.slab_bounds()
+        F = s.get_state()["F"][:, lo:hi]
+        worst = max(worst, np.abs(F - G[:, lo:hi]).max() / np.abs(G).max())
+    print(f"world {world}: forces vs world 1 max|dF|/max|F| = {worst:.3e}")
+    assert worst < 1e-13
+    ratio = int(ref.const("plasmaToQuantumTimestepRatio"))
+    for _ in range(2):
+        for s in sims:
+            s.substeps(ratio)
+        for s in sims:
+            s.allgather_positions()
+        for s in sims:
+            s.forces()
+    for s in sims:
+        s.substeps(ratio)
+    ref.substeps(ratio)
+    ref.md_steps(2)
+    b = ref.get_state()
+    for s in sims:
+        lo, hi = s.slab_bounds()
+        a = s.get_state()
+        dR = np.abs(a["R"][:, lo:hi] - b["R"][:, lo:hi]).max()
+        dV = np.abs(a["V"][:, lo:hi] - b["V"][:, lo:hi]).max()
+        assert dR < 1e-12 and dV < 1e-12, (dR, dV)
+    for s in sims:
+        s.close()
+    ref.close()

@@ -9,7 +9,13 @@
  * (MCMD:54, :87), consumed in the reference's order: the Metropolis draws inside the device
  * MC kernel (mt19937 + libstdc++ generate_canonical<double, 53> on the GPU, the state handed
  * over from and back to the host engine), the Maxwell-Boltzmann velocities, collision rolls and
- * tag rolls on the host.  With the same seed the trajectory is the reference program's.
+ * tag rolls on the host.  With the same seed the trajectory follows the reference program's
+ * stream: the Metropolis energy change is summed in a fixed tree order (and, with force_kernel 1,
+ * from reciprocal-form pair energies with a polynomial exp) where the reference sums
+ * sequentially with libm exp (MCMD:341-357), so an accept decision whose dice lies within a few
+ * ulp of exp(-dE Gamma / 2) can go the other way — the stream then shifts and the runs part
+ * statistically.  The parity tests pin 3,000 MC steps bit for bit against the reference build;
+ * longer horizons are statistical parity, not a bitwise guarantee.
  *
  * Conventions as include/mdqt.h: opaque context, int status (0 ok, <0 error; message in
  * mdqt_last_error()), caller-owned host buffers, R/V/A as [3][N] row-major like the reference's

@@ -51,7 +51,11 @@ typedef struct mdqt_params {
     /* ---- extensions ---- */
     int qt_enabled;       /* 1 = MDQT (reference); 0 = MD-only (qstep body skipped, t advances) */
     int rng_mode;         /* 1 = Philox4x32-10 keyed (seed, job) x (global ion, qstep): fast,
-                           *     reproducible, partition-invariant (default);
+                           *     reproducible, the same draws for an ion at any world size
+                           *     (default; trajectories are bit-identical across world sizes
+                           *     with the owner-computes rows scheme, N <= 65,536, and agree to
+                           *     rounding with the Newton-3 block scheme above that — its rank
+                           *     partials are summed in the reduce-scatter's order);
                            * 0 = the reference's own drand48 stream in its consumption order
                            *     (SpeedUp:486, :575-687; one stream, world_size 1): trajectory
                            *     parity with the 1-thread reference, one launch per substep   */
@@ -149,7 +153,11 @@ int         mdqt_tag_spin_up(mdqt_ctx* c, int* tags, int* n_up);
  *   "substep_kernel": 0 = auto, 1 = thread per ion, 2 = 16-lane group per ion
  *   "force_kernel":   1 = fast reciprocal form (default), 0 = the reference's exact operations
  *                     (the two differ by a few ulp per pair; both meet the 1e-13 force gate)
- *   "force_scheme":   0 = auto, 1 = owner-computes rows, 2 = Newton-3 tile pairs (one GPU)
+ *   "force_scheme":   0 = auto, 1 = owner-computes rows, 2 = Newton-3 tile pairs (one GPU),
+ *                     3 = Newton-3 block pairs (auto above 65,536 ions; sharded: reduce-scatter)
+ *   "force_sort":     block pairs only: 1 = Hilbert-curve order with exact skipping of tile
+ *                     pairs >= L/2 apart (default), 2 = the same order, nothing skipped (bit-
+ *                     identical to 1), 0 = storage order
  *   "qt_enabled":     1 = qstep() runs in the substeps, 0 = skipped (t still advances): the
  *                     pumping programs' pump window (randomFrozenStartTag408Linear.cpp main)
  *   "qt_math":        0 = the reference's exact operations, 1 = FMA-contracted with a refined

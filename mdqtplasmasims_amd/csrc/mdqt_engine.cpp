@@ -1044,7 +1044,8 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
     const bool tm_marks = tm && !s->use_n3;
     if (tm_marks && mark(s, 0)) return -1;
     if (s->use_n3) {
-        N3Args a;
+        N3Args a{};                  // variant 2 (MCMD's exact pair set, rc2) is not used here
+        if (s->force_variant > 1) return fail("mdqt_forces: force_kernel must be 0 or 1");
         a.R = s->dR; a.P = s->dFpart; a.pairs = s->dPairs;
         a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs;
         ForceArgs c = force_args(s, nullptr);

@@ -4,15 +4,22 @@
         -m mdqtplasmasims_amd.sharded <job> --N0=1000000 --qt=0 [--tmax=...] [--md-steps=K]
 
 Each rank owns the slab of ions [rank*S, min((rank+1)*S, N)) (libmdqt `mdqt_slab`, a pure function
-of N and the world size).  The only data-path collective is the RCCL all-gather of the position
-slabs before every force evaluation, issued inside libmdqt on the context's stream over xGMI.
-Output steps all-reduce scalars, the 3 x 2001 KDE bins and the per-ion file columns; rank 0
+of N and the world size).  Data-path collectives per MD step, issued inside libmdqt on the
+context's stream over xGMI: the RCCL all-gather of the position slabs before every force
+evaluation, and — with Newton-3 block pairs (N > 65,536: every sharded BASELINE config) — one
+reduce-scatter of the ranks' dense partial forces (each rank evaluates its blocks' pairs for all
+ions).  Output steps all-reduce scalars, the 3 x 2001 KDE bins and the per-ion file columns; rank 0
 writes the reference's files.  torch.distributed (gloo) is used only for the rendezvous: rank 0
 creates the RCCL unique id and broadcasts it.
 
-Partition invariance: force rows do not depend on the slab (the j-segmentation is a function of
-N only) and the quantum-jump stream is keyed by the GLOBAL ion id, so 1/2/4/8-GPU runs produce
-bit-identical trajectories (tests/test_gpu_parity.py::test_sharded_local_group_bit_identical).
+World-size invariance: the quantum-jump stream is keyed by the GLOBAL ion id.  With the
+owner-computes rows scheme (N <= 65,536, or force_scheme 1) force rows do not depend on the slab
+(the j-segmentation is a function of N only), so 1/2/4/8-GPU runs are bit-identical
+(tests/test_gpu_parity.py::test_sharded_local_group_bit_identical).  With Newton-3 block pairs
+the rank partials are summed in the reduce-scatter's order, so results for different world sizes
+agree to rounding, not bit for bit: forces within 1e-13 of world 1, two MD steps within 1e-12
+(tests/test_gpu_large.py::test_sharded_newton3_blocks_above_64k_local_group,
+tests/test_n3b_protocol.py for the block ownership and the partial reduction over gloo).
 """
 from __future__ import annotations
 

@@ -73,12 +73,18 @@ typedef struct mdqt_params {
                            * 3 = 422 nm linear, 5 levels (randomFrozenStartTag422Linear.cpp:390).
                            * Pumping models use states 0..6 / 0..4 of the 12-state psi layout. */
     char saveDirectory[256]; /* SpeedUp:56 */
+    /* ---- the optical-pumping programs' main() (mdqt_run_pump; qt_model 1-3) ---- */
+    double tpumpreal;     /* randomFrozenStartTag408Linear.cpp:58  pump duration (s)           */
+    double tstartV0;      /* :78  pump window start (omega_E^-1); window = (tstartV0, tendV0)   */
 } mdqt_params;
 
 typedef struct mdqt_ctx mdqt_ctx;
 
 /* ---- lifecycle ---- */
 void        mdqt_default_params(mdqt_params* p);            /* SpeedUp:56-85 defaults          */
+/* the pumping programs' defaults: model 1 = randomFrozenStartTag408Linear.cpp:52-80,
+ * 2 = randomFrozenStartTag408Quad.cpp:55-81, 3 = randomFrozenStartTag422Linear.cpp:52-78 */
+void        mdqt_default_params_pump(mdqt_params* p, int qt_model);
 int         mdqt_create(const mdqt_params* p, mdqt_ctx** out); /* + constant operators :1163-1215 */
 void        mdqt_destroy(mdqt_ctx* c);
 const char* mdqt_last_error(void);                           /* thread-local message            */
@@ -148,6 +154,20 @@ int         mdqt_flush_files(mdqt_ctx* c);
  * = tagParticles (MonteCarloFollowedByQTTagging408Linear.cpp:1022).  tags: [N] (may be NULL;
  * a sharded context fills its slab), *n_up: number tagged (this context's ions). */
 int         mdqt_tag_spin_up(mdqt_ctx* c, int* tags, int* n_up);
+/* The optical-pumping programs' main() (randomFrozenStartTag408Linear.cpp:981-1076, 408Quad :990-1086,
+ * 422Linear :946-1031; qt_model 1-3): directory PumpTime..PumpStart..Det..Om..Density..Ge..NumIons..
+ * (:990), init() or readConditions(c0); the time loop — leapfrog MD step (step() :377-394,
+ * forces at the half-drifted positions) every plasmaToQuantumTimestepRatio quantum steps, qstep()
+ * only inside the pump window (tstartV0, tstartV0 + tpumpreal 813490 sqrt(density)), t += dtQ
+ * otherwise; at the first t >= tendV0 measureSpinUps() (:600, spinUpIons_timestep%06d.dat), output()
+ * and the VAF; then output() every sampleFreq MD steps: energies.dat, taggedMoments.dat,
+ * vel_distX_timestep%06d.dat of the spin-up ions (4001 bins, :799-935), VAF.dat (:938-975);
+ * writeConditions(c0) at the end: ions_, spinUpIonsList_, conditions_ (:667-707).  Quantum jumps
+ * and the tags draw from the Philox stream (the reference's shared drand48 is racy).
+ * world_size 1. */
+int         mdqt_run_pump(mdqt_ctx* c);
+/* the spin-up list of the pumping run (N ints; 0 before measureSpinUps) */
+int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
 
 /* ---- tuning knobs ----
  *   "substep_kernel": 0 = auto, 1 = thread per ion, 2 = 16-lane group per ion

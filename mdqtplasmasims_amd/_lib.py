@@ -29,6 +29,7 @@ class MdqtParams(C.Structure):
         ("seed", C.c_uint32), ("job", C.c_uint32), ("device", C.c_int), ("world_size", C.c_int),
         ("rank", C.c_int), ("force_segments", C.c_int), ("qt_model", C.c_int),
         ("saveDirectory", C.c_char * 256),
+        ("tpumpreal", C.c_double), ("tstartV0", C.c_double),
     ]
 
 
@@ -119,6 +120,9 @@ SIGNATURES = [
     ("mdqt_write_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_read_conditions", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_run", C.c_int, [C.c_void_p]),
+    ("mdqt_run_pump", C.c_int, [C.c_void_p]),
+    ("mdqt_get_spin_up_list", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("mdqt_default_params_pump", None, [C.POINTER(MdqtParams), C.c_int]),
     ("mdqt_flush_files", C.c_int, [C.c_void_p]),
     ("mdqt_tag_spin_up", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("mdqt_set_option", C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),

@@ -651,7 +651,7 @@ __global__ __launch_bounds__(256) void k_anisotropize(double* __restrict__ V, in
 constexpr int TKDE_CHUNK = 256;
 
 __global__ __launch_bounds__(256) void k_tagged_kde(const double* __restrict__ V, const int* __restrict__ tags, int N,
-                                                    int S, double* __restrict__ part) {
+                                                    int S, int bin0, double* __restrict__ part) {
     __shared__ double sv[3][TKDE_CHUNK];
     __shared__ int st[TKDE_CHUNK];
     const int j = blockIdx.x * 256 + threadIdx.x;
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(256) void k_tagged_kde(const double* __restrict__ V
         st[threadIdx.x] = 0;
     }
     __syncthreads();
-    const double vel = (double)(j - 2000) * 0.0025;                 // QTT:250
+    const double vel = (double)(j + bin0) * 0.0025;                 // QTT:250 (bin0 = -2000)
     const double V2 = 1. / (2. * 0.002 * 0.002);                   // QTT:1072
     double p[3] = {0., 0., 0.};
     const int m = min(TKDE_CHUNK, N - i0);
@@ -779,10 +779,11 @@ hipError_t launch_anisotropize(double* V, int N, int S, double tpd, hipStream_t 
 }
 
 // part must hold ceil(N / 256) x 3 x TKDE_BINS doubles, out 3 x TKDE_BINS
-hipError_t launch_tagged_kde(const double* V, const int* tags, int N, int S, double* part, double* out, hipStream_t s) {
+hipError_t launch_tagged_kde(const double* V, const int* tags, int N, int S, double* part, double* out, hipStream_t s,
+                             int bin0) {
     if (N <= 0) return hipSuccess;
     const int nch = (N + TKDE_CHUNK - 1) / TKDE_CHUNK;
-    hipLaunchKernelGGL(k_tagged_kde, dim3((TKDE_BINS + 255) / 256, nch), dim3(256), 0, s, V, tags, N, S, part);
+    hipLaunchKernelGGL(k_tagged_kde, dim3((TKDE_BINS + 255) / 256, nch), dim3(256), 0, s, V, tags, N, S, bin0, part);
     hipLaunchKernelGGL(k_tagged_kde_reduce, dim3((3 * TKDE_BINS + 255) / 256), dim3(256), 0, s, part, nch, out);
     return hipGetLastError();
 }

@@ -112,6 +112,13 @@ struct mdqt_ctx {
     double* dRs = nullptr;         // [3][Npad] positions in sorted order
     double* dBoxes = nullptr;      // [6][T] tile boxes
     int capSortN = 0;
+    // the optical-pumping programs' main() (mdqt_run_pump)
+    std::vector<int> spinUp;       // SpinUpList (randomFrozenStartTag408Linear.cpp:105)
+    int nSpinUp = 0;
+    int* dSpinUp = nullptr;        // device copy for the tagged distribution
+    double* dTkde = nullptr;       // tagged KDE partials + result
+    int pumpBin0 = -2000;          // velocity bins (j + pumpBin0) 0.0025: init() :306 / readConditions :723
+    std::vector<double> vaHold;    // Vholder of Zfunc (:938-961)
     bool rs_pending = false;       // in-process group: F = sum of the ranks' dFr chunks, not formed yet
     const double** dPeerParts = nullptr;   // device array of the group's dFr pointers
     int nslots = 0, npairs = 0, capPairs = 0;
@@ -177,6 +184,24 @@ extern "C" void mdqt_default_params(mdqt_params* p) {
     p->qt_enabled = 1; p->rng_mode = 1; p->seed = 12345; p->job = 1;
     p->device = -1; p->world_size = 1; p->rank = 0; p->force_segments = 0; p->qt_model = 0;
     strcpy(p->saveDirectory, "dataLaserCool/");                                              // :56
+    p->tpumpreal = 0.0000002; p->tstartV0 = 15;           // randomFrozenStartTag408Linear.cpp:58, :78
+}
+
+// The optical-pumping programs' compile-time globals (randomFrozenStartTag408Linear.cpp:52-80,
+// randomFrozenStartTag408Quad.cpp:55-81, randomFrozenStartTag422Linear.cpp:52-78): N0 3500,
+// Ge 0.1, density 2, sampleFreq 40, tmax 25, tstartV0 15 in all three; per program the pump
+// detuning, Rabi frequency, pump time and directory.
+extern "C" void mdqt_default_params_pump(mdqt_params* p, int qt_model) {
+    mdqt_default_params(p);
+    p->qt_model = qt_model;
+    p->tmax = 25; p->Ge = 0.1; p->density = 2; p->N0 = 3500; p->sampleFreq = 40; p->tstartV0 = 15;
+    if (qt_model == 2) {
+        p->detuning = 0; p->Om = 2; p->tpumpreal = 0.0000001; strcpy(p->saveDirectory, "data/");
+    } else if (qt_model == 3) {
+        p->detuning = -1; p->Om = 1.3; p->tpumpreal = 0.0000001; strcpy(p->saveDirectory, "data422/");
+    } else {
+        p->detuning = -2.5; p->Om = 0.7; p->tpumpreal = 0.0000002; strcpy(p->saveDirectory, "data408/");
+    }
 }
 
 extern "C" const char* mdqt_last_error(void) { return g_err.c_str(); }
@@ -725,6 +750,8 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     if (s->dTab) (void)hipFree(s->dTab);
     if (s->dFTab) (void)hipFree(s->dFTab);
     if (s->dComm) (void)hipFree(s->dComm);
+    if (s->dSpinUp) (void)hipFree(s->dSpinUp);
+    if (s->dTkde) (void)hipFree(s->dTkde);
     if (s->dX48) (void)hipFree(s->dX48);
     if (s->dFlags) (void)hipFree(s->dFlags);
     if (s->comm) (void)ncclCommDestroy(s->comm);
@@ -1610,6 +1637,293 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
         tsc += n;
     }
     return mdqt_write_conditions(s, s->c0);             // :1381; also joins the writers
+}
+
+// ---------------------------------------------------------------------------------------------
+// The optical-pumping programs' main() — randomFrozenStartTag408Linear.cpp (":" lines below),
+// randomFrozenStartTag408Quad.cpp, randomFrozenStartTag422Linear.cpp (same flow).
+// ---------------------------------------------------------------------------------------------
+
+static int setup_directories_pump(mdqt_ctx* s) {                // :985-999
+    const mdqt_params* p = &s->p;
+    char base[512];
+    strncpy(base, p->saveDirectory, sizeof(base) - 1);
+    base[sizeof(base) - 1] = 0;
+    mkdir(base, 0777);
+    char name[256];
+    snprintf(name, sizeof name, "PumpTime%dPumpStart%dDet%dOm%dDensity%dGe%dNumIons%d",
+             (int)(unsigned)(1000000000. * p->tpumpreal), (int)(unsigned)(p->tstartV0),
+             (int)(unsigned)(100. * fabs(p->detuning)), (int)(unsigned)(100. * p->Om),
+             (int)(unsigned)(10. * p->density), (int)(unsigned)(1000 * p->Ge), (int)(unsigned)p->N0);
+    snprintf(s->saveDirectory, sizeof(s->saveDirectory), "%s%s", base, name);
+    mkdir(s->saveDirectory, 0777);
+    char jb[64];
+    snprintf(jb, sizeof jb, "/job%d/", (int)p->job);
+    strncat(s->saveDirectory, jb, sizeof(s->saveDirectory) - strlen(s->saveDirectory) - 1);
+    mkdir(s->saveDirectory, 0777);
+    struct stat st;
+    if (stat(s->saveDirectory, &st) != 0 || !S_ISDIR(st.st_mode))
+        return fail("cannot create output directory %s", s->saveDirectory);
+    return 0;
+}
+
+// step() :377-394: step_R(dt/2) (at t == 0 with forces() first and the DT^2 F term), step_V(dt)
+// with forces() at the half-drifted positions, step_R(dt/2)
+static int md_step_pump(mdqt_ctx* s) {
+    const double dt = s->dtQ * s->ratio;                         // :389 dt=quantumTimestep*ratio
+    const double DT = 0.5 * dt, DT2 = DT * DT;
+    const int moving = s->t > 0 ? 1 : 0;
+    HIPCHK(hipSetDevice(s->dev));
+    double* R = s->dR;
+    if (!moving) {                                               // :331 forces() before the first drift
+        if (mdqt_forces(s)) return -1;
+        if (settle_forces(s)) return -1;
+    }
+    HIPCHK(launch_leapfrog_half(R, s->dV, s->dF, s->nloc, s->S, s->L, DT, DT2, moving, 0., s->stream));
+    if (mdqt_forces(s)) return -1;                               // step_V: forces() :361
+    if (settle_forces(s)) return -1;
+    HIPCHK(launch_leapfrog_half(R, s->dV, s->dF, s->nloc, s->S, s->L, DT, DT2, moving, dt, s->stream));
+    return 0;
+}
+
+// measureSpinUps() :600-665 (tags from the Philox stream, mdqt_tag_spin_up)
+static int measure_spin_ups(mdqt_ctx* s) {
+    const int N = s->N;
+    s->spinUp.assign((size_t)(N > 0 ? N : 1), 0);
+    int n_up = 0;
+    if (mdqt_tag_spin_up(s, s->spinUp.data(), &n_up)) return -1;
+    s->nSpinUp = n_up;
+    if (!s->dSpinUp) HIPCHK(hipMalloc(&s->dSpinUp, (size_t)s->capS * sizeof(int)));
+    HIPCHK(hipMemcpyAsync(s->dSpinUp, s->spinUp.data(), (size_t)N * sizeof(int), hipMemcpyHostToDevice, s->stream));
+    char b[96];
+    snprintf(b, sizeof b, "spinUpIons_timestep%06d.dat", s->c0);
+    FILE* fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    fprintf(fa, "%i", s->nSpinUp);                               // :651-662
+    fclose(fa);
+    return 0;
+}
+
+// output() :799-935: energies (EkinX without subtracting <vx>), the spin-up ions' moments and x
+// velocity distribution over 4001 bins, counter++; host sums in the reference's order
+static int output_pump(mdqt_ctx* s) {
+    const int N = s->N;
+    std::vector<double> V((size_t)3 * (N > 0 ? N : 1), 0.);
+    if (mdqt_get_state(s, nullptr, V.data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
+    double EkinX = 0., EkinY = 0., EkinZ = 0.;
+    for (int i = 0; i < N; i++) {                                // :812-817
+        EkinX += 0.5 * (V[i] * V[i]);
+        EkinY += 0.5 * (V[(size_t)N + i] * V[(size_t)N + i]);
+        EkinZ += 0.5 * (V[(size_t)2 * N + i] * V[(size_t)2 * N + i]);
+    }
+    EkinX /= (double)N; EkinY /= (double)N; EkinZ /= (double)N;
+    double e;
+    if (mdqt_epotential(s, &e)) return -1;                       // :821
+    FILE* fa = open_in(s, "energies.dat", "a");                  // :825-829
+    if (!fa) return -1;
+    fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\n", s->t, EkinX, EkinY, EkinZ, s->Epot,
+            EkinX + EkinY + EkinZ + s->Epot - s->Epot0);
+    fclose(fa);
+    // tagged x distribution on the device (:831-864 exp(-V2 (vel_j - v)^2) summed over spin-up ions)
+    const int nch = (N + 255) / 256;
+    if (!s->dTkde) HIPCHK(hipMalloc(&s->dTkde, ((size_t)(nch > 0 ? nch : 1) + 1) * 3 * TKDE_BINS * sizeof(double)));
+    if (!s->dSpinUp) {
+        HIPCHK(hipMalloc(&s->dSpinUp, (size_t)s->capS * sizeof(int)));
+        HIPCHK(hipMemsetAsync(s->dSpinUp, 0, (size_t)s->capS * sizeof(int), s->stream));
+    }
+    std::vector<double> P((size_t)3 * TKDE_BINS, 0.);
+    if (N > 0) {
+        HIPCHK(launch_tagged_kde(s->dV, s->dSpinUp, N, s->S, s->dTkde + (size_t)3 * TKDE_BINS, s->dTkde, s->stream,
+                                 s->pumpBin0));
+        HIPCHK(hipMemcpyAsync(P.data(), s->dTkde, P.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    // moments of the tagged x velocities (:836-851, :866-876)
+    double m1 = 0, m2 = 0, m3 = 0, m4 = 0;
+    unsigned nt = 0;
+    const bool have = !s->spinUp.empty() && (int)s->spinUp.size() >= N;
+    for (int i = 0; i < N; i++) {
+        const double v = V[i];
+        if (have && s->spinUp[i]) {
+            m1 += v; m2 += v * v; m3 += v * v * v; m4 += v * v * v * v;
+            nt += 1;
+        }
+    }
+    m1 /= nt; m2 /= nt; m3 /= nt; m4 /= nt;
+    fa = open_in(s, "taggedMoments.dat", "a");
+    if (!fa) return -1;
+    fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\n", s->t, m1, m2, m3, m4);
+    fclose(fa);
+    char b[96];
+    snprintf(b, sizeof b, "vel_distX_timestep%06d.dat", s->c0);   // :887-901 (X only)
+    fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    for (int j = 0; j < TKDE_BINS; j++) fprintf(fa, "%lg\t%lg\n", (double)(j + s->pumpBin0) * 0.0025, P[j]);
+    fclose(fa);
+    s->counter++;                                                // :929
+    return 0;
+}
+
+// Zfunc(c1V) + printVAF(t) :938-975 (host, the reference's order)
+static int vaf_pump(mdqt_ctx* s, int c1V) {
+    const int N = s->N;
+    std::vector<double> V((size_t)3 * (N > 0 ? N : 1), 0.);
+    if (mdqt_get_state(s, nullptr, V.data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
+    if (c1V == 0) s->vaHold.assign(V.begin(), V.begin() + N);
+    if ((int)s->vaHold.size() < N) s->vaHold.resize((size_t)N, 0.);
+    double VAF = 0.0;
+    for (int j = 0; j < N; j++) VAF += 1 / ((double)(N)) * (s->vaHold[j] * V[j]);
+    FILE* fa = open_in(s, "VAF.dat", "a");
+    if (!fa) return -1;
+    fprintf(fa, "%lg\t%lg\n", s->t, VAF);
+    fclose(fa);
+    return 0;
+}
+
+static int write_conditions_pump(mdqt_ctx* s, int c0) {        // :667-707
+    const int N = s->N;
+    std::vector<double> R((size_t)3 * (N > 0 ? N : 1), 0.), V(R.size(), 0.);
+    if (mdqt_get_state(s, R.data(), V.data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
+    char b[96];
+    snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
+    FILE* fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    fprintf(fa, "%i\t%i", N, s->counter);
+    fclose(fa);
+    snprintf(b, sizeof b, "spinUpIonsList_timestep%06d.dat", c0);
+    fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    for (int i = 0; i < N; i++) fprintf(fa, "%i\n", (int)s->spinUp.size() > i ? s->spinUp[i] : 0);
+    fclose(fa);
+    snprintf(b, sizeof b, "conditions_timestep%06d.dat", c0);
+    fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    for (int i = 0; i < N; i++)
+        fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\t\n", R[i], R[(size_t)N + i], R[(size_t)2 * N + i], V[i],
+                V[(size_t)N + i], V[(size_t)2 * N + i]);
+    fclose(fa);
+    return 0;
+}
+
+static int read_conditions_pump(mdqt_ctx* s, int c0) {         // :709-797
+    s->t = ((double)c0 - 9.) * TIMESTEP + 0.02;                 // :713
+    s->pumpBin0 = 0;                                             // :721-724 vel[i] = i 0.0025
+    char b[96];
+    snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
+    FILE* fa = open_in(s, b, "r");
+    if (!fa) return -1;
+    int j, m, N = -1;
+    while (fscanf(fa, "%i\t%i", &j, &m) == 2) { N = j; s->counter = (unsigned)m; }
+    fclose(fa);
+    if (N < 0) return fail("%s: no ion count", b);
+    std::vector<int> up((size_t)(N > 0 ? N : 1), 0);
+    snprintf(b, sizeof b, "spinUpIonsList_timestep%06d.dat", c0);
+    fa = open_in(s, b, "r");
+    if (!fa) return -1;
+    int i = 0, sUp;
+    while (i < N && fscanf(fa, "%i\n", &sUp) == 1) up[i++] = sUp;
+    fclose(fa);
+    std::vector<double> R((size_t)3 * (N > 0 ? N : 1), 0.), V(R.size(), 0.);
+    snprintf(b, sizeof b, "conditions_timestep%06d.dat", c0);
+    fa = open_in(s, b, "r");
+    if (!fa) return -1;
+    double a, bb, z, d, e, f;
+    i = 0;
+    while (i < N && fscanf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\n", &a, &bb, &z, &d, &e, &f) == 6) {
+        R[i] = a; R[(size_t)N + i] = bb; R[(size_t)2 * N + i] = z;
+        V[i] = d; V[(size_t)N + i] = e; V[(size_t)2 * N + i] = f;
+        i++;
+    }
+    fclose(fa);
+    if (i != N) return fail("%s: %d of %d rows", b, i, N);
+    const double t = s->t;
+    if (resize(s, N)) return -1;
+    // wvFns are not read (the reference's read loop is commented out, :772-795): they stay zero
+    std::vector<double> psi((size_t)24 * (N > 0 ? N : 1), 0.), tp((size_t)(N > 0 ? N : 1), 0.);
+    if (upload(s, R.data(), V.data(), N, psi.data(), tp.data())) return -1;
+    s->spinUp = up;
+    s->nSpinUp = 0;
+    for (int k = 0; k < N; ++k) s->nSpinUp += up[k] ? 1 : 0;
+    if (s->dSpinUp) { (void)hipFree(s->dSpinUp); s->dSpinUp = nullptr; }
+    HIPCHK(hipMalloc(&s->dSpinUp, (size_t)s->capS * sizeof(int)));
+    HIPCHK(hipMemcpyAsync(s->dSpinUp, up.data(), (size_t)N * sizeof(int), hipMemcpyHostToDevice, s->stream));
+    s->t = t;
+    s->c0 = c0;
+    return 0;
+}
+
+extern "C" int mdqt_get_spin_up_list(mdqt_ctx* s, int* tags, int* n_up) {
+    if (!s) return fail("NULL context");
+    for (int i = 0; i < s->N && tags; ++i) tags[i] = (int)s->spinUp.size() > i ? s->spinUp[i] : 0;
+    if (n_up) *n_up = s->nSpinUp;
+    return 0;
+}
+
+extern "C" int mdqt_run_pump(mdqt_ctx* s) {                     // main() :981-1076
+    if (!s) return fail("NULL context");
+    if (s->p.qt_model < 1 || s->p.qt_model > 3) return fail("mdqt_run_pump: qt_model must be 1, 2 or 3");
+    if (s->p.world_size != 1) return fail("mdqt_run_pump: world_size 1 only");
+    if (setup_directories_pump(s)) return -1;
+    int recorded = 0;                                            // recordedSpinUps :81
+    s->spinUp.clear();
+    s->nSpinUp = 0;
+    s->pumpBin0 = -2000;
+    if (s->p.newRun == 1) {                                      // :1036-1046
+        if (mdqt_init(s)) return -1;
+    } else {
+        if (read_conditions_pump(s, s->p.c0)) return -1;
+        recorded = 1;
+    }
+    const double tpump = s->p.tpumpreal * 813490 * sqrt(s->p.density);      // :79
+    const double tendV0 = s->p.tstartV0 + tpump;                             // :80
+    const double tstartV0 = s->p.tstartV0;
+    const double tend = s->p.tmax + 0.0009;
+    const int sf = s->p.sampleFreq, ratio = s->ratio;
+    int tsc = ratio;                                             // :1033
+    // quantum steps are queued while nothing else happens and run as one fused launch
+    int pending = 0;
+    double tv = s->t;                                            // the loop's t (s->t lags by `pending` qsteps)
+    auto flush = [&]() -> int {
+        if (pending > 0) {
+            if (run_substeps(s, pending, 0, 1, 1)) return -1;    // qstep() x pending :396-598
+            pending = 0;
+            if (s->t != tv) return fail("mdqt_run_pump: time bookkeeping mismatch");
+        }
+        return 0;
+    };
+    while (tv <= tend) {                                         // :1050
+        if (recorded == 0 && tv >= tendV0) {                     // :1052-1058
+            if (flush()) return -1;
+            if (measure_spin_ups(s)) return -1;
+            recorded = 1;
+            if (output_pump(s)) return -1;
+            if (vaf_pump(s, 0)) return -1;
+        }
+        if ((s->c0 + 1) % sf == 0 && tsc == 1 && recorded == 1) {   // :1062-1069
+            if (flush()) return -1;
+            if (output_pump(s)) return -1;
+            if (vaf_pump(s, 1)) return -1;
+        }
+        if (tsc == ratio) {                                      // :1070-1074
+            if (flush()) return -1;
+            if (md_step_pump(s)) return -1;
+            s->c0++;
+            tsc = 0;
+        }
+        if (tv < tendV0 && tv > tstartV0) {                      // :1075-1077 qstep()
+            pending++;
+            tv += s->dtQ;                                        // qstep's t += dtQuant :597
+            if (pending == MAXSUB && flush()) return -1;
+        } else {                                                 // :1078-1080
+            if (flush()) return -1;
+            s->t += s->dtQ;
+            tv = s->t;
+        }
+        tsc++;
+    }
+    if (flush()) return -1;
+    if (flush_files(s)) return -1;
+    return write_conditions_pump(s, s->c0);                      // :1084
 }
 
 // ---------------------------------------------------------------------------------------------

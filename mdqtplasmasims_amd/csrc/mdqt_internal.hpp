@@ -337,7 +337,15 @@ void build_pump_program(int model, double detuning, double Om, double dtQ, doubl
 // recordTaggedParticleMoments' velocity distribution of the tagged ions (QT tagging programs):
 // out[c][j] = sum over tagged i (ascending) of exp(-V2 (vel_j - V[c][i])^2), vel_j = (j - 2000) 0.0025
 constexpr int TKDE_BINS = 4001;
-hipError_t launch_tagged_kde(const double* V, const int* tags, int N, int S, double* part, double* out, hipStream_t s);
+// bins vel_j = (j + bin0) 0.0025: bin0 = -2000 (the programs' init(), e.g. randomFrozenStartTag408Linear.cpp:306),
+// 0 after their readConditions (:723 sets vel[i] = i 0.0025)
+hipError_t launch_tagged_kde(const double* V, const int* tags, int N, int S, double* part, double* out, hipStream_t s,
+                             int bin0 = -2000);
+// one half of the pumping programs' leapfrog MD step (randomFrozenStartTag408Linear.cpp step(), :317-394):
+// if kick != 0, V += kick F first (step_V); then step_R: R += DT V (moving) or R += DT V + DT2 F
+// (t == 0), and the reinsertion into [0, L]
+hipError_t launch_leapfrog_half(double* R, double* V, const double* F, int n, int S, double L, double DT, double DT2,
+                                int moving, double kick, hipStream_t s);
 
 // drand48 in the reference's order (SpeedUp:486, :575-687: ions in index order, 1 draw per
 // ion, 4-5 for a quantum jump): one workgroup assigns every ion its uniforms from the single

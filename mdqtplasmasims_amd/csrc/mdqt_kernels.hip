@@ -698,4 +698,35 @@ hipError_t launch_kde(const double* V, int n, int S, const double* vxAvg, double
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// the optical-pumping programs' MD step (randomFrozenStartTag408Linear.cpp step() :377-394 =
+// step_R(dt/2) :317-356, step_V(dt) :358-375 with forces() at the half-drifted positions,
+// step_R(dt/2)), in two launches around forces(): the reference's operations, exact
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_leapfrog_half(double* __restrict__ R, double* __restrict__ V,
+                                                       const double* __restrict__ F, int n, int S, double L,
+                                                       double DT, double DT2, int moving, double kick) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const size_t k = (size_t)c * S + i;
+        double v = V[k];
+        const double f = F[k];
+        if (kick != 0.) { v += kick * f; V[k] = v; }                 // V[c][i] += DT*F[c][i]   :366-370
+        double r = R[k];
+        r = moving ? r + DT * v : r + (DT * v + DT2 * f);            // :320-338
+        if (r < 0) r += L;                                           // :346-354
+        if (r > L) r -= L;
+        R[k] = r;
+    }
+}
+
+hipError_t launch_leapfrog_half(double* R, double* V, const double* F, int n, int S, double L, double DT, double DT2,
+                                int moving, double kick, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_leapfrog_half, dim3((n + 255) / 256), dim3(256), 0, s, R, V, F, n, S, L, DT, DT2, moving, kick);
+    return hipGetLastError();
+}
+
 }  // namespace mdqt

@@ -50,6 +50,21 @@ def default_params(**kw) -> MdqtParams:
     return p
 
 
+def default_params_pump(qt_model: int, **kw) -> MdqtParams:
+    """the optical-pumping program's defaults (qt_model 1 / 2 / 3 = randomFrozenStartTag408Linear /
+    408Quad / 422Linear.cpp globals), then the overrides in kw"""
+    p = MdqtParams()
+    lib().mdqt_default_params_pump(C.byref(p), int(qt_model))
+    for k, v in kw.items():
+        if k not in PARAM_NAMES:
+            raise KeyError(f"unknown parameter {k!r}")
+        if k == "saveDirectory":
+            p.saveDirectory = v.encode() if isinstance(v, str) else v
+        else:
+            setattr(p, k, v)
+    return p
+
+
 def device_count() -> int:
     return lib().mdqt_device_count()
 
@@ -99,8 +114,10 @@ def comm_init_local(sims) -> None:
 class Simulation:
     """One MDQT system (or one rank's slab of it) resident on one MI355X."""
 
-    def __init__(self, **params):
-        self.params = default_params(**params)
+    def __init__(self, pump_program: int = 0, **params):
+        """pump_program 1 / 2 / 3: start from that optical-pumping program's defaults
+        (mdqt_default_params_pump) instead of SpeedUp's"""
+        self.params = default_params_pump(pump_program, **params) if pump_program else default_params(**params)
         h = C.c_void_p()
         check(lib().mdqt_create(C.byref(self.params), C.byref(h)), "mdqt_create")
         self.h = h
@@ -249,6 +266,19 @@ class Simulation:
 
     def run(self):
         check(lib().mdqt_run(self.h), "run")
+
+    def run_pump(self):
+        """the optical-pumping programs' main() (randomFrozenStartTag408Linear.cpp:981-1076;
+        qt_model 1-3): mdqt_run_pump"""
+        check(lib().mdqt_run_pump(self.h), "run_pump")
+
+    def spin_up_list(self):
+        """(tags[N], n_up) of the pumping run's measureSpinUps()"""
+        tags = np.zeros(self.N, dtype=np.int32)
+        n = C.c_int()
+        check(lib().mdqt_get_spin_up_list(self.h, tags.ctypes.data_as(C.POINTER(C.c_int)), C.byref(n)),
+              "spin_up_list")
+        return tags, n.value
 
     def flush_files(self):
         """wait for the background file writers (mdqt_flush_files)"""

@@ -65,6 +65,9 @@ struct orc_sim {
     char saveDirectory[1024];
     uint64_t* ion_ids;                /* Philox ion key of local ion i (NULL: i); sampled-ion checks */
     int n_ion_ids;
+    int* spinUp;                      /* SpinUpList (randomFrozenStartTag408Linear.cpp:105), orc_run_pump */
+    int nSpinUp;
+    double* vaHold;                   /* Vholder of Zfunc (:938-961) */
 };
 
 /* ------------------------------------------------------------------------------------------ */
@@ -139,6 +142,7 @@ void orc_default_params(orc_params* p) {
     p->N0 = 3500; p->newRun = 1; p->c0 = 0; p->sampleFreq = 40; p->reNormalizewvFns = 0;
     p->qt_enabled = 1; p->rng_mode = 0; p->seed = 12345; p->job = 1; p->nthreads = 1;
     strcpy(p->saveDirectory, "dataLaserCool/");
+    p->tpumpreal = 0.0000002; p->tstartV0 = 15;          /* randomFrozenStartTag408Linear.cpp:58, :78 */
 }
 
 static int reserve(orc_sim* s, int cap) {
@@ -255,6 +259,8 @@ void orc_destroy(orc_sim* s) {
     if (!s) return;
     free(s->R); free(s->V); free(s->F); free(s->psi); free(s->tPart); free(s->Vholder);
     free(s->ion_ids);
+    free(s->spinUp);
+    free(s->vaHold);
     free(s);
 }
 
@@ -1184,4 +1190,198 @@ int orc_run(orc_sim* s) {                                                      /
         timeStepCounter++;
     }
     return orc_write_conditions(s, s->c0);                                    /* :1381 */
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* The optical-pumping programs' main(): randomFrozenStartTag408Linear.cpp (":" lines),         */
+/* randomFrozenStartTag408Quad.cpp and randomFrozenStartTag422Linear.cpp follow the same flow.   */
+/* ------------------------------------------------------------------------------------------ */
+
+static void step_R_pump(orc_sim* s, double DT) {                                 /* :317-356 */
+    const int c = s->cap;
+    if (s->t > 0) {
+        for (int i = 0; i < s->N; i++)
+            for (int k = 0; k < 3; ++k) s->R[(size_t)k * c + i] += DT * s->V[(size_t)k * c + i];
+    } else {
+        orc_forces(s);
+        for (int i = 0; i < s->N; i++)
+            for (int k = 0; k < 3; ++k)
+                s->R[(size_t)k * c + i] += DT * s->V[(size_t)k * c + i] + DT * DT * s->F[(size_t)k * c + i];
+    }
+    for (int i = 0; i < s->N; i++)
+        for (int k = 0; k < 3; ++k) {
+            double* r = &s->R[(size_t)k * c + i];
+            if (*r < 0) *r += s->L;
+            if (*r > s->L) *r -= s->L;
+        }
+}
+
+static void md_step_pump(orc_sim* s) {                                           /* :377-394 */
+    const int c = s->cap;
+    const double dt = s->dtQ * s->ratio;
+    step_R_pump(s, 0.5 * dt);
+    orc_forces(s);                                                               /* step_V :358-375 */
+    for (int i = 0; i < s->N; i++)
+        for (int k = 0; k < 3; ++k) s->V[(size_t)k * c + i] += dt * s->F[(size_t)k * c + i];
+    step_R_pump(s, 0.5 * dt);
+}
+
+static int setup_dirs_pump(orc_sim* s) {                                         /* :985-999 */
+    const orc_params* p = &s->p;
+    char base[512];
+    strncpy(base, p->saveDirectory, sizeof(base) - 1);
+    base[sizeof(base) - 1] = 0;
+    mkdir(base, 0777);
+    char name[256];
+    snprintf(name, sizeof name, "PumpTime%dPumpStart%dDet%dOm%dDensity%dGe%dNumIons%d",
+             (int)(unsigned)(1000000000. * p->tpumpreal), (int)(unsigned)(p->tstartV0),
+             (int)(unsigned)(100. * fabs(p->detuning)), (int)(unsigned)(100. * p->Om),
+             (int)(unsigned)(10. * p->density), (int)(unsigned)(1000 * p->Ge), (int)(unsigned)p->N0);
+    snprintf(s->saveDirectory, sizeof(s->saveDirectory), "%s%s", base, name);
+    mkdir(s->saveDirectory, 0777);
+    char jb[64];
+    snprintf(jb, sizeof jb, "/job%d/", (int)p->job);
+    strncat(s->saveDirectory, jb, sizeof(s->saveDirectory) - strlen(s->saveDirectory) - 1);
+    mkdir(s->saveDirectory, 0777);
+    return 0;
+}
+
+static int measure_spin_ups_pump(orc_sim* s) {                                    /* :600-665 */
+    free(s->spinUp);
+    s->spinUp = calloc((size_t)(s->N > 0 ? s->N : 1), sizeof(int));
+    s->nSpinUp = orc_tag_spin_up(s, s->spinUp);
+    char b[96];
+    snprintf(b, sizeof b, "spinUpIons_timestep%06d.dat", s->c0);
+    FILE* fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    fprintf(fa, "%i", s->nSpinUp);
+    fclose(fa);
+    return 0;
+}
+
+static int output_pump(orc_sim* s, int bin0) {                                    /* :799-935 */
+    const int N = s->N, c = s->cap;
+    const double *Vx = s->V, *Vy = s->V + c, *Vz = s->V + 2 * c;
+    double EkinX = 0.0, EkinY = 0.0, EkinZ = 0.0;
+    for (int i = 0; i < N; i++) {
+        EkinX += 0.5 * (Vx[i] * Vx[i]);
+        EkinY += 0.5 * (Vy[i] * Vy[i]);
+        EkinZ += 0.5 * (Vz[i] * Vz[i]);
+    }
+    EkinX /= (double)N; EkinY /= (double)N; EkinZ /= (double)N;
+    orc_epotential(s);
+    FILE* fa = open_in(s, "energies.dat", "a");
+    if (!fa) return -1;
+    fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\n", s->t, EkinX, EkinY, EkinZ, s->Epot, EkinX + EkinY + EkinZ + s->Epot - s->Epot0);
+    fclose(fa);
+    const double V2 = 1. / (2. * 0.002 * 0.002);
+    double* PvelX = calloc(4001, sizeof(double));
+    double firstMom = 0, secondMom = 0, thirdMom = 0, fourthMom = 0;
+    unsigned numTagged = 0;
+    for (int i = 0; i < N; i++) {
+        const double currVx = Vx[i];
+        const int up = s->spinUp ? s->spinUp[i] : 0;
+        if (up) {
+            firstMom += currVx; secondMom += currVx * currVx; thirdMom += currVx * currVx * currVx;
+            fourthMom += currVx * currVx * currVx * currVx;
+            numTagged += 1;
+        }
+        if (up == 1)
+            for (int j = 0; j < 4001; j++) {
+                const double vel = (double)(j + bin0) * 0.0025;
+                PvelX[j] += exp(-V2 * (vel - Vx[i]) * (vel - Vx[i]));
+            }
+    }
+    firstMom /= numTagged; secondMom /= numTagged; thirdMom /= numTagged; fourthMom /= numTagged;
+    fa = open_in(s, "taggedMoments.dat", "a");
+    if (!fa) { free(PvelX); return -1; }
+    fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\n", s->t, firstMom, secondMom, thirdMom, fourthMom);
+    fclose(fa);
+    for (int j = 0; j < 4001; j++) PvelX[j] /= (6.0 * sqrt(2 * M_PI * 0.002 * 0.002));
+    char b[96];
+    snprintf(b, sizeof b, "vel_distX_timestep%06d.dat", s->c0);
+    fa = open_in(s, b, "w");
+    if (!fa) { free(PvelX); return -1; }
+    for (int j = 0; j < 4001; j++) fprintf(fa, "%lg\t%lg\n", (double)(j + bin0) * 0.0025, PvelX[j]);
+    fclose(fa);
+    free(PvelX);
+    s->counter++;
+    return 0;
+}
+
+static int vaf_pump(orc_sim* s, int c1V) {                                        /* :938-975 */
+    const int N = s->N;
+    if (c1V == 0) {
+        free(s->vaHold);
+        s->vaHold = malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
+        for (int j = 0; j < N; j++) s->vaHold[j] = s->V[j];
+    }
+    double VAF = 0.0;
+    for (int j = 0; j < N; j++) VAF += 1 / ((double)(N)) * (s->vaHold[j] * s->V[j]);
+    FILE* fa = open_in(s, "VAF.dat", "a");
+    if (!fa) return -1;
+    fprintf(fa, "%lg\t%lg\n", s->t, VAF);
+    fclose(fa);
+    return 0;
+}
+
+static int write_conditions_pump(orc_sim* s, int c0) {                           /* :667-707 */
+    const int N = s->N, c = s->cap;
+    char b[96];
+    snprintf(b, sizeof b, "ions_timestep%06d.dat", c0);
+    FILE* fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    fprintf(fa, "%i\t%i", N, s->counter);
+    fclose(fa);
+    snprintf(b, sizeof b, "spinUpIonsList_timestep%06d.dat", c0);
+    fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    for (int i = 0; i < N; i++) fprintf(fa, "%i\n", s->spinUp ? s->spinUp[i] : 0);
+    fclose(fa);
+    snprintf(b, sizeof b, "conditions_timestep%06d.dat", c0);
+    fa = open_in(s, b, "w");
+    if (!fa) return -1;
+    for (int i = 0; i < N; i++)
+        fprintf(fa, "%lg\t%lg\t%lg\t%lg\t%lg\t%lg\t\n", s->R[i], s->R[c + i], s->R[2 * (size_t)c + i], s->V[i],
+                s->V[c + i], s->V[2 * (size_t)c + i]);
+    fclose(fa);
+    return 0;
+}
+
+int orc_get_spin_up_list(const orc_sim* s, int* tags) {
+    for (int i = 0; i < s->N && tags; ++i) tags[i] = s->spinUp ? s->spinUp[i] : 0;
+    return s->nSpinUp;
+}
+
+int orc_run_pump(orc_sim* s) {                                                   /* :981-1076 */
+    if (s->p.qt_model < 1 || s->p.qt_model > 3) return -1;
+    if (setup_dirs_pump(s)) return -1;
+    s->x48 = orc_srand48_state(s->p.seed);
+    if (orc_init(s)) return -1;                                                  /* newRun == 1 */
+    int recorded = 0;
+    const int bin0 = -2000;                                                      /* init() :306 */
+    const double tpump = s->p.tpumpreal * 813490 * sqrt(s->p.density);          /* :79 */
+    const double tendV0 = s->p.tstartV0 + tpump;                                /* :80 */
+    int tsc = s->ratio;                                                          /* :1033 */
+    while (s->t <= s->p.tmax + 0.0009) {                                         /* :1050 */
+        if (recorded == 0 && s->t >= tendV0) {                                   /* :1052-1058 */
+            if (measure_spin_ups_pump(s)) return -1;
+            recorded = 1;
+            if (output_pump(s, bin0)) return -1;
+            if (vaf_pump(s, 0)) return -1;
+        }
+        if ((s->c0 + 1) % s->p.sampleFreq == 0 && tsc == 1 && recorded == 1) {   /* :1062-1069 */
+            if (output_pump(s, bin0)) return -1;
+            if (vaf_pump(s, 1)) return -1;
+        }
+        if (tsc == s->ratio) {                                                   /* :1070-1074 */
+            md_step_pump(s);
+            s->c0++;
+            tsc = 0;
+        }
+        if (s->t < tendV0 && s->t > s->p.tstartV0) orc_qstep(s);                /* :1075-1080 */
+        else s->t += s->dtQ;
+        tsc++;
+    }
+    return write_conditions_pump(s, s->c0);
 }

@@ -57,6 +57,8 @@ typedef struct orc_params {
     int qt_model;         /* 0 = SpeedUp 12-level cooling; 1/2/3 = 408 linear / 408 quad / 422 linear
                            * optical pumping (randomFrozenStartTag*.cpp qstep; Philox only) */
     char saveDirectory[256]; /* SpeedUp:56 */
+    double tpumpreal;     /* randomFrozenStartTag408Linear.cpp:58 (orc_run_pump) */
+    double tstartV0;      /* randomFrozenStartTag408Linear.cpp:78 */
 } orc_params;
 
 typedef struct orc_sim orc_sim;
@@ -125,6 +127,12 @@ int    orc_output(orc_sim* s);                 /* SpeedUp:917-1032 */
 int    orc_write_conditions(orc_sim* s, int c0); /* SpeedUp:725-784 */
 int    orc_read_conditions(orc_sim* s, int c0);  /* SpeedUp:785-916 */
 int    orc_setup_directories(orc_sim* s);        /* SpeedUp:1145-1160 */
+/* the optical-pumping programs' main() (randomFrozenStartTag408Linear.cpp:981-1076 and the 408Quad /
+ * 422Linear copies; qt_model 1-3): leapfrog MD step every ratio quantum steps, qstep() only in
+ * the pump window, measureSpinUps(), output() of the tagged ions, VAF, writeConditions() */
+int    orc_run_pump(orc_sim* s);
+/* its spin-up list (N ints) and count */
+int    orc_get_spin_up_list(const orc_sim* s, int* tags);
 const char* orc_save_directory(const orc_sim* s);
 
 /* RNG primitives (exported for the known-answer tests) */

@@ -29,6 +29,7 @@ class OrcParams(C.Structure):
         ("reNormalizewvFns", C.c_int), ("qt_enabled", C.c_int), ("rng_mode", C.c_int),
         ("seed", C.c_uint32), ("job", C.c_uint32), ("nthreads", C.c_int), ("qt_model", C.c_int),
         ("saveDirectory", C.c_char * 256),
+        ("tpumpreal", C.c_double), ("tstartV0", C.c_double),
     ]
 
 
@@ -106,6 +107,8 @@ def lib():
         L.orc_tag_spin_up.restype = C.c_int
         L.orc_set_qt_constants.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_double, C.c_double]
         L.orc_tag_spin_up.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        L.orc_run_pump.argtypes = [C.c_void_p]
+        L.orc_get_spin_up_list.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -229,6 +232,15 @@ class OracleSim:
 
     def run(self):
         return lib().orc_run(self.h)
+
+    def run_pump(self):
+        """the optical-pumping programs' main() (randomFrozenStartTag408Linear.cpp:981-1076)"""
+        return lib().orc_run_pump(self.h)
+
+    def spin_up_list(self):
+        tags = np.zeros(self.N, dtype=np.int32)
+        n = lib().orc_get_spin_up_list(self.h, tags.ctypes.data_as(C.POINTER(C.c_int)))
+        return tags, n
 
     def output(self):
         return lib().orc_output(self.h)

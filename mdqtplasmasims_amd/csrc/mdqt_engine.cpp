@@ -112,6 +112,18 @@ struct mdqt_ctx {
     double* dRs = nullptr;         // [3][Npad] positions in sorted order
     double* dBoxes = nullptr;      // [6][T] tile boxes
     int capSortN = 0;
+    // overlapped MD step (option "overlap", default on where it applies: one GPU, Newton-3 tiles,
+    // lane QT kernel): the QT launch of step k runs on its own stream beside step k's force
+    // launch and waits on the device for the force workgroups' arrivals (see mdqt_md_steps)
+    int overlap_opt = 1;
+    hipStream_t qs = nullptr;              // the QT stream
+    hipEvent_t evQ = nullptr, evS = nullptr;
+    unsigned long long* dArrive = nullptr; // force workgroups finished, monotonic
+    unsigned long long arriveEpoch = 0;
+    int* dSpinErr = nullptr;
+    unsigned long long* force_arrive = nullptr;   // set around a force launch of an overlapped step
+    hipStream_t sub_stream = nullptr;             // set around the QT launch of an overlapped step
+    unsigned long long sub_target = 0;
     // the optical-pumping programs' main() (mdqt_run_pump)
     std::vector<int> spinUp;       // SpinUpList (randomFrozenStartTag408Linear.cpp:105)
     int nSpinUp = 0;
@@ -159,6 +171,13 @@ static int settle_forces(mdqt_ctx* s);
 // L/8 in half a substep: not a physical run).  Checked at every host synchronisation point;
 // from then on every pair is range-checked, and the call reports the event as an error.
 static int check_range_flag(mdqt_ctx* s) {
+    if (s->dSpinErr) {                  // an overlapped QT launch gave up waiting for its forces
+        int e = 0;
+        if (hipMemcpyAsync(&e, s->dSpinErr, sizeof e, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+            hipStreamSynchronize(s->stream) != hipSuccess)
+            return fail("reading the overlap flag failed");
+        if (e) return fail("overlapped MD step: a QT launch timed out waiting for its force launch");
+    }
     int f = 0;
     if (hipMemcpyAsync(&f, s->dFlags, sizeof f, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
         hipStreamSynchronize(s->stream) != hipSuccess)
@@ -751,6 +770,11 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     if (s->dFTab) (void)hipFree(s->dFTab);
     if (s->dComm) (void)hipFree(s->dComm);
     if (s->dSpinUp) (void)hipFree(s->dSpinUp);
+    if (s->dArrive) (void)hipFree(s->dArrive);
+    if (s->dSpinErr) (void)hipFree(s->dSpinErr);
+    if (s->evQ) (void)hipEventDestroy(s->evQ);
+    if (s->evS) (void)hipEventDestroy(s->evS);
+    if (s->qs) (void)hipStreamDestroy(s->qs);
     if (s->dTkde) (void)hipFree(s->dTkde);
     if (s->dX48) (void)hipFree(s->dX48);
     if (s->dFlags) (void)hipFree(s->dFlags);
@@ -1081,6 +1105,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         a.guard = c.guard;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (tm && take_events(s, 0, &e0, &e1)) return -1;
+        a.arrive = s->force_arrive;                // overlapped MD step: count finished workgroups
         HIPCHK(launch_forces_n3(a, s->force_variant, s->stream, e0, e1));
         s->f_pending = true;       // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots;
@@ -1137,6 +1162,11 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         a.V = s->dV; a.F = s->dF; a.psi = s->dPsi; a.tPart = s->dTp;
         a.Fpart = s->dFpart; a.nseg = s->f_pending ? s->pend_nseg : 1;
         a.oor = s->dFlags;
+        if (s->sub_stream) {                            // overlapped MD step (mdqt_md_steps)
+            a.arrive = s->dArrive;
+            a.arrive_target = s->sub_target;
+            a.spin_err = s->dSpinErr;
+        }
         s->f_pending = false;
         a.n = s->nloc; a.S = s->S; a.gid0 = (uint64_t)s->lo;
         a.q0 = s->qidx;
@@ -1164,7 +1194,8 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         const bool tm = s->timing && (s->tcount[1]++ % s->tperiod == s->tperiod / 2);
         hipEvent_t e0 = nullptr, e1 = nullptr;       // timing: the kernel's own timestamps
         if (tm && (take_events(s, 1, &e0, &e1))) return -1;
-        if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->substep_mode, s->stream, e0, e1));
+        hipStream_t st = s->sub_stream ? s->sub_stream : s->stream;
+        if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->sub_stream ? 2 : s->substep_mode, st, e0, e1));
         else HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream, e0, e1));
         if (advance_t) {
             s->t = t;
@@ -1208,8 +1239,60 @@ extern "C" int mdqt_substeps(mdqt_ctx* s, int n) {
     return run_substeps(s, n, 1, 1, 1);
 }
 
+// The overlapped MD step applies to one unsharded system on the Newton-3 tile scheme with the
+// lane-per-state QT kernel (qt_math 2, Philox stream), one fused launch per MD interval.
+static bool overlap_applies(const mdqt_ctx* s) {
+    return s->overlap_opt && s->p.world_size == 1 && s->local.empty() && s->use_n3 && s->qt_math == 2 &&
+           s->p.qt_enabled && s->p.rng_mode == 1 && s->ratio <= MAXSUB && s->nloc > 0 &&
+           (s->substep_mode == 2 || (s->substep_mode == 0 && s->nloc < kLaneKernelMaxIons));
+}
+
+static int overlap_setup(mdqt_ctx* s) {
+    if (s->qs) return 0;
+    HIPCHK(hipStreamCreateWithFlags(&s->qs, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s->evQ, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&s->evS, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(hipMalloc(&s->dArrive, sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&s->dSpinErr, sizeof(int)));
+    HIPCHK(hipMemset(s->dArrive, 0, sizeof(unsigned long long)));
+    HIPCHK(hipMemset(s->dSpinErr, 0, sizeof(int)));
+    HIPCHK(hipDeviceSynchronize());
+    s->arriveEpoch = 0;
+    return 0;
+}
+
+// MD steps with the force and QT launches overlapped: step k's force launch (context stream)
+// waits for step k-1's QT launch by an event; step k's QT launch (its own stream, in order after
+// step k-1's) starts at once, issues its prologue loads and Philox draws while the forces are
+// computed, and waits on the device until all force workgroups of step k have arrived.  Same
+// kernels, same operations: bit-identical to the sequential order (tests/test_gpu_parity.py).
+static int md_steps_overlapped(mdqt_ctx* s, int n) {
+    if (overlap_setup(s)) return -1;
+    HIPCHK(hipEventRecord(s->evS, s->stream));
+    HIPCHK(hipStreamWaitEvent(s->qs, s->evS, 0));
+    for (int k = 0; k < n; ++k) {
+        if (k > 0) HIPCHK(hipStreamWaitEvent(s->stream, s->evQ, 0));
+        if (k > 0 && k % 64 == 0 && check_range_flag(s)) return -1;
+        s->force_arrive = s->dArrive;
+        const int rc = mdqt_forces(s);
+        s->force_arrive = nullptr;
+        if (rc) return -1;
+        s->arriveEpoch += (unsigned long long)s->npairs;
+        s->c0++;
+        s->sub_stream = s->qs;
+        s->sub_target = s->arriveEpoch;
+        const int rq = run_substeps(s, s->ratio, 1, 1, 1);
+        s->sub_stream = nullptr;
+        if (rq) return -1;
+        HIPCHK(hipEventRecord(s->evQ, s->qs));
+    }
+    HIPCHK(hipStreamWaitEvent(s->stream, s->evQ, 0));      // later work on the context stream
+    return 0;
+}
+
 extern "C" int mdqt_md_steps(mdqt_ctx* s, int n) {
     if (!s) return fail("NULL context");
+    if (n > 0 && overlap_applies(s)) return md_steps_overlapped(s, n);
     for (int k = 0; k < n; ++k) {
         if (k > 0 && k % 64 == 0 && check_range_flag(s)) return -1;
         if (mdqt_allgather_positions(s)) return -1;     // sharded: other slabs' R
@@ -1940,6 +2023,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         s->scheme_opt = value;
         choose_segments(s);
         return ensure_aux(s);
+    }
+    if (!strcmp(name, "overlap")) {                    // force || QT launches of an MD step (mdqt_md_steps)
+        if (value < 0 || value > 1) return fail("overlap must be 0 or 1");
+        s->overlap_opt = value;
+        return 0;
     }
     if (!strcmp(name, "force_sort")) {                 // Newton-3 blocks: Hilbert order + tile-pair skipping
         if (value < 0 || value > 2) return fail("force_sort must be 0 (off), 1 (on) or 2 (sorted, no skipping)");

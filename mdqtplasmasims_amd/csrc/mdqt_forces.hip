@@ -224,7 +224,15 @@ __device__ __forceinline__ double n3_jsum(const double (*accj)[3][128], int k, i
     return w;
 }
 
-template <int VARIANT, bool GUARD, bool RAGGED>
+// slot stores: plain, or write-through (sc1) when the QT launch of an overlapped MD step reads
+// them after an arrival count instead of a kernel boundary (MI355X_MICROARCH.md, hand-off forms)
+template <bool SIG>
+__device__ __forceinline__ void slot_store(double* p, double v) {
+    if constexpr (SIG) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+template <int VARIANT, bool GUARD, bool RAGGED, bool SIG>
 __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
                                         double (*ia)[3][64]) {
@@ -278,7 +286,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
 #pragma unroll
             for (int w = 1; w < N3W; ++w) v += ia[w][k][l];
             if (diag) v = v - n3_jsum(accj, k, l);
-            if (i < S) Pi[(size_t)k * S + i] = v;
+            if (i < S) slot_store<SIG>(&Pi[(size_t)k * S + i], v);
         }
     } else if (q == 1 && !diag) {                   // rows of J -> slot I
         double* Pj = a.P + (size_t)I * slab3;
@@ -286,8 +294,13 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const double w = n3_jsum(accj, k, l);
-            if (j < S) Pj[(size_t)k * S + j] = -w;
+            if (j < S) slot_store<SIG>(&Pj[(size_t)k * S + j], -w);
         }
+    }
+    if constexpr (SIG) {                            // every storing wave drained, then one arrival
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(a.arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -307,8 +320,14 @@ __global__ __launch_bounds__(64 * N3W) void k_pairs_n3(N3Args a) {
 #endif
     const int2 IJ = a.pairs[blockIdx.x];
     const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
-    if ((a.N & 63) && IJ.y == a.ntiles - 1) n3_tile<VARIANT, GUARD, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
-    else n3_tile<VARIANT, GUARD, false>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+    const bool rag = (a.N & 63) && IJ.y == a.ntiles - 1;
+    if (a.arrive) {
+        if (rag) n3_tile<VARIANT, GUARD, true, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+        else n3_tile<VARIANT, GUARD, false, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+    } else {
+        if (rag) n3_tile<VARIANT, GUARD, true, false>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+        else n3_tile<VARIANT, GUARD, false, false>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+    }
 #if defined(MDQT_EXPT_STAMPS)
     __syncthreads();
     if (threadIdx.x == 0 && blockIdx.x < 8192) {

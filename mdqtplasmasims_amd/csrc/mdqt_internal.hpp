@@ -146,6 +146,13 @@ struct SubstepArgs {
     double expDet[MAXSUB];  // expDetuning(t) (:447)
     uint32_t movmask;       // bit s: t[s] > 0 (step_R's moving branch, :360); set by the host
     int expdet_zero;        // every expDet[s] == 0 (fracOfSig = 0, the default)
+    // overlapped MD step (lane kernel, world 1): the force kernel runs concurrently on another
+    // stream and counts its finished workgroups in *arrive; this launch does its prologue, then
+    // waits until *arrive >= arrive_target before it reads the force partials (write-through
+    // stores there, L1-bypassing loads here: mdqt_forces.hip k_pairs_n3)
+    const unsigned long long* arrive;
+    unsigned long long arrive_target;
+    int* spin_err;          // set if the wait gave up (bounded spin)
     QTConst qc;
 };
 
@@ -251,6 +258,8 @@ struct N3Args {
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;          // as ForceArgs::guard (exact variant only; the fast one needs no guard)
     double rc2;         // variant 2: smallest double x with sqrt(x) >= Rcut (pair kept iff r2 < rc2)
+    unsigned long long* arrive;   // overlapped MD step: +1 per finished workgroup (after its
+                                  // write-through partial stores), nullptr = off
 };
 
 // Newton-3 over block pairs (mdqt_forces.hip k_pairs_n3b): blocks of 16 tiles, cyclic half

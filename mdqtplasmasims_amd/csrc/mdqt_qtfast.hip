@@ -347,7 +347,9 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     // partial q_k of all three components (its loads issued together, 4 slots per round), the
     // DPP tree combines them in slot_sum16's order
     double qf[3] = {0., 0., 0.};
-    if (nseg > 1) {
+    // overlapped MD step (a.arrive): the partials are read after the arrival wait below, with
+    // L1-bypassing loads; otherwise right here, with the other prologue loads
+    auto slot_partials = [&](bool sc1) {
         const double* base_p = a.Fpart + i;
         const size_t plane = (size_t)3 * S;
         for (int s0 = k; s0 < nseg; s0 += 64) {
@@ -356,13 +358,20 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
             for (int u = 0; u < 4; ++u) {
                 const int sl = s0 + 16 * u;
 #pragma unroll
-                for (int cc = 0; cc < 3; ++cc) t[u][cc] = sl < nseg ? base_p[(size_t)sl * plane + (size_t)cc * S] : 0.;
+                for (int cc = 0; cc < 3; ++cc) {
+                    const double* q = base_p + (size_t)sl * plane + (size_t)cc * S;
+                    t[u][cc] = sl < nseg ? (sc1 ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q)
+                                         : 0.;
+                }
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
                 for (int cc = 0; cc < 3; ++cc) qf[cc] = qf[cc] + t[u][cc];
         }
+    };
+    if (nseg > 1) {
+        if (!a.arrive) slot_partials(false);
     } else {
         f = a.F[(size_t)c * S + i];
     }
@@ -398,6 +407,17 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
                 su[grp][s][1] = x1;
             }
         }
+    }
+    if (a.arrive) {                                   // wait for the concurrent force launch
+        if (threadIdx.x == 0) {
+            int it = 0;
+            while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++it > (1 << 21)) { *a.spin_err = 1; break; }   // bounded: never hang the GPU
+            }
+        }
+        __syncthreads();
+        if (nseg > 1) slot_partials(true);
     }
     if (nseg > 1) {
         const double fx = lane_tree16(qf[0]), fy = lane_tree16(qf[1]), fz = lane_tree16(qf[2]);

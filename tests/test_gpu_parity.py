@@ -586,3 +586,22 @@ def test_norm_decay_and_partition_of_qt(eng):
     assert np.abs(nrm - 1).max() < 1e-3
     o7, P, pops = s.observables()
     assert np.all(pops >= -1e-15) and np.all(pops.sum(1) < 1.001)
+
+
+@pytest.mark.parametrize("N0", [500, 3500])
+def test_overlapped_md_step_bit_identical(eng, N0):
+    """mdqt_md_steps with the force and QT launches overlapped (QT prologue on its own stream, a
+    device-side arrival count instead of the kernel boundary, write-through partials) is the same
+    arithmetic as the sequential order: bit for bit, over MD steps with quantum jumps"""
+    out = []
+    for ov in (0, 1):
+        s = eng.Simulation(N0=N0, seed=71).init()
+        s.set_option("overlap", ov)
+        s.md_steps(30)
+        s.synchronize()
+        out.append(s.get_state())
+        s.close()
+    a, b = out
+    for k in ("R", "V", "F", "psi", "tPart"):
+        assert np.array_equal(a[k], b[k]), k
+    assert (a["tPart"] < 30 * 0.002 - 1e-9).sum() > 0          # jumps happened

@@ -74,9 +74,9 @@ def parse():
     ap.add_argument("--qt-math", type=int, default=2, choices=[0, 1, 2],
                     help="0: the reference's exact QT operations, 1: FMA-contracted, 2: reassociated "
                          "(option qt_math, the library default)")
-    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
-                    help="1: each MD step's QT launch overlaps its force launch (option overlap, the "
-                         "library default); 0: the sequential order (bit-identical results)")
+    ap.add_argument("--overlap", type=int, default=0, choices=[0, 1],
+                    help="1: each MD step's QT launch overlaps its force launch (option overlap; "
+                         "measured slower, DESIGN.md §8); 0: the sequential order (library default)")
     ap.add_argument("--no-pump-lines", action="store_true",
                     help="skip the optical-pumping model lines (SURVEY §8(f)3)")
     ap.add_argument("--no-mcmd-lines", action="store_true",

@@ -112,10 +112,10 @@ struct mdqt_ctx {
     double* dRs = nullptr;         // [3][Npad] positions in sorted order
     double* dBoxes = nullptr;      // [6][T] tile boxes
     int capSortN = 0;
-    // overlapped MD step (option "overlap", default on where it applies: one GPU, Newton-3 tiles,
-    // lane QT kernel): the QT launch of step k runs on its own stream beside step k's force
-    // launch and waits on the device for the force workgroups' arrivals (see mdqt_md_steps)
-    int overlap_opt = 1;
+    // overlapped MD step (option "overlap", OFF by default — measured slower): the
+    // QT launch of step k runs on its own stream beside step k's force launch and waits on the
+    // device for the force workgroups' arrivals (see md_steps_overlapped)
+    int overlap_opt = 0;
     hipStream_t qs = nullptr;              // the QT stream
     hipEvent_t evQ = nullptr, evS = nullptr;
     unsigned long long* dArrive = nullptr; // force workgroups finished, monotonic
@@ -1166,6 +1166,7 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             a.arrive = s->dArrive;
             a.arrive_target = s->sub_target;
             a.spin_err = s->dSpinErr;
+            a.arrive_sleep = 2;
         }
         s->f_pending = false;
         a.n = s->nloc; a.S = s->S; a.gid0 = (uint64_t)s->lo;
@@ -1266,6 +1267,10 @@ static int overlap_setup(mdqt_ctx* s) {
 // step k-1's) starts at once, issues its prologue loads and Philox draws while the forces are
 // computed, and waits on the device until all force workgroups of step k have arrived.  Same
 // kernels, same operations: bit-identical to the sequential order (tests/test_gpu_parity.py).
+// Measured at C2 (one MI355X): 104-107 us per MD step against 45.6 sequential — the two
+// cross-stream event waits cost ~17 us per step by themselves, and the resident QT waves (176
+// VGPRs) leave room for 1,344 of the force launch's 1,596 workgroups, so it runs in two rounds
+// (17.6 -> 52-70 us).  Kept as an option (default off) with its bit-identity test.
 static int md_steps_overlapped(mdqt_ctx* s, int n) {
     if (overlap_setup(s)) return -1;
     HIPCHK(hipEventRecord(s->evS, s->stream));

@@ -153,6 +153,7 @@ struct SubstepArgs {
     const unsigned long long* arrive;
     unsigned long long arrive_target;
     int* spin_err;          // set if the wait gave up (bounded spin)
+    int arrive_sleep;       // s_sleep 1 (64 cycles) units between polls (2)
     QTConst qc;
 };
 

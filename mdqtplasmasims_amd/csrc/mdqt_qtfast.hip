@@ -412,7 +412,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         if (threadIdx.x == 0) {
             int it = 0;
             while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
-                __builtin_amdgcn_s_sleep(2);
+                for (int z = 0; z < a.arrive_sleep; ++z) __builtin_amdgcn_s_sleep(1);
                 if (++it > (1 << 21)) { *a.spin_err = 1; break; }   // bounded: never hang the GPU
             }
         }

@@ -105,7 +105,7 @@ struct mdqt_ctx {
     double* dFr = nullptr;         // sharded n3b: this rank's dense partial forces [world][3][S]
     // spatial order of the n3b scheme (mdqt_sort.hip; option "force_sort", default on)
     int sort_mode = 1;             // 0 off, 1 sorted + tile-pair skipping, 2 sorted, nothing skipped (tests)
-    uint32_t* dKeys = nullptr;     // [2][N] Morton keys, sorted keys
+    uint32_t* dKeys = nullptr;     // [2][N] Hilbert keys, sorted keys
     int* dIon = nullptr;           // [2][N] identity, sorted index -> ion
     void* dSortTmp = nullptr;
     size_t sortTmpBytes = 0;

@@ -306,7 +306,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
 
 #if defined(MDQT_EXPT_STAMPS)
 // diagnostic build only: per-workgroup start/end (s_memrealtime, 100 MHz) and placement
-__device__ unsigned long long g_n3_stamps[4 * 8192];
+__device__ unsigned long long g_n3_stamps[6 * 8192];
 #endif
 
 template <int VARIANT, bool GUARD>
@@ -317,6 +317,7 @@ __global__ __launch_bounds__(64 * N3W) void k_pairs_n3(N3Args a) {
     __shared__ double mj[128];
 #if defined(MDQT_EXPT_STAMPS)
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
     const int2 IJ = a.pairs[blockIdx.x];
     const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
@@ -332,17 +333,20 @@ __global__ __launch_bounds__(64 * N3W) void k_pairs_n3(N3Args a) {
     __syncthreads();
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        g_n3_stamps[4 * blockIdx.x] = t_start;
-        g_n3_stamps[4 * blockIdx.x + 1] = t_end;
-        g_n3_stamps[4 * blockIdx.x + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-        g_n3_stamps[4 * blockIdx.x + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+        const unsigned long long c_end = __builtin_amdgcn_s_memtime();
+        g_n3_stamps[6 * blockIdx.x] = t_start;
+        g_n3_stamps[6 * blockIdx.x + 1] = t_end;
+        g_n3_stamps[6 * blockIdx.x + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        g_n3_stamps[6 * blockIdx.x + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+        g_n3_stamps[6 * blockIdx.x + 4] = c_start;                                       // core clock
+        g_n3_stamps[6 * blockIdx.x + 5] = c_end;
     }
 #endif
 }
 
 #if defined(MDQT_EXPT_STAMPS)
 extern "C" int mdqt_expt_n3_stamps(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_n3_stamps), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_n3_stamps), sizeof(unsigned long long) * 6 * n) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -556,6 +560,14 @@ hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int 
 hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (a.npairs <= 0) return hipSuccess;
     dim3 grid(a.npairs);
+#if defined(MDQT_EXPT_N3LDS)
+    // diagnostic build only: extra dynamic LDS per workgroup (bytes) to cap workgroups per CU
+    if (variant == 1 && !a.guard) {
+        if (ev0) hipExtLaunchKernelGGL(k_pairs_n3<1, false>, grid, dim3(64 * N3W), MDQT_EXPT_N3LDS, s, ev0, ev1, 0, a);
+        else hipLaunchKernelGGL((k_pairs_n3<1, false>), grid, dim3(64 * N3W), MDQT_EXPT_N3LDS, s, a);
+        return hipGetLastError();
+    }
+#endif
     if (variant == 2) {
         if (a.guard) launch_timed(k_pairs_n3<2, true>, grid, dim3(64 * N3W), s, ev0, ev1, a);
         else launch_timed(k_pairs_n3<2, false>, grid, dim3(64 * N3W), s, ev0, ev1, a);

@@ -285,7 +285,7 @@ struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]
     int N, S, Npad;
     double L;
-    uint32_t *keys, *keys2;  // [N] Morton keys, sorted keys
+    uint32_t *keys, *keys2;  // [N] Hilbert keys, sorted keys
     int *ion, *perm;         // [N] identity, sorted index -> ion
     void* tmp;               // hipCUB radix-sort scratch
     size_t tmp_bytes;

@@ -19,9 +19,9 @@ s.synchronize()
 n = s.counters and 1596
 ntiles = (s.N + 63) // 64
 n = ntiles * (ntiles + 1) // 2
-buf = (C.c_ulonglong * (4 * n))()
+buf = (C.c_ulonglong * (6 * n))()
 assert lib().mdqt_expt_n3_stamps(buf, n) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.int64)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 6).astype(np.int64)
 t0 = a[:, 0].min()
 st = (a[:, 0] - t0) * 10e-3      # us (100 MHz)
 en = (a[:, 1] - t0) * 10e-3
@@ -41,4 +41,6 @@ print("distinct CUs used:", len(u), " WGs per CU min/mean/max:", cnt.min(), roun
 print("per-XCC WGs:", np.bincount(xcc, minlength=8))
 diag = np.array([0])
 hist = np.histogram(st, bins=10)[0]
+clk = (a[:, 5] - a[:, 4]) / np.maximum(a[:, 1] - a[:, 0], 1) * 100e6 / 1e9
+print("core clock GHz (s_memtime / s_memrealtime) pct 0/50/100:", np.percentile(clk, [0, 50, 100]).round(3))
 print("start histogram (10 bins over span):", hist)

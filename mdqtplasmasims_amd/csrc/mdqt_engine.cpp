@@ -110,7 +110,7 @@ struct mdqt_ctx {
     void* dSortTmp = nullptr;
     size_t sortTmpBytes = 0;
     double* dRs = nullptr;         // [3][Npad] positions in sorted order
-    double* dBoxes = nullptr;      // [6][T] tile boxes
+    double* dBoxes = nullptr;      // [12][T] tile boxes, raw coordinate bounds
     int capSortN = 0;
     // overlapped MD step (option "overlap", OFF by default — measured slower): the
     // QT launch of step k runs on its own stream beside step k's force launch and waits on the
@@ -611,7 +611,7 @@ static int ensure_aux(mdqt_ctx* s) {
             if (!s->sortTmpBytes) return fail("radix sort scratch size query failed");
             HIPCHK(hipMalloc(&s->dSortTmp, s->sortTmpBytes));
             HIPCHK(hipMalloc(&s->dRs, (size_t)3 * Tc * 64 * sizeof(double)));
-            HIPCHK(hipMalloc(&s->dBoxes, (size_t)6 * Tc * sizeof(double)));
+            HIPCHK(hipMalloc(&s->dBoxes, (size_t)12 * Tc * sizeof(double)));
             s->capSortN = Nc;
         }
     }

@@ -190,12 +190,21 @@ __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restric
 // ------------------------------------------------------------------------------------------
 // one rotation step of a Newton-3 tile pair: lane's ion i against the J-tile ion at LDS index
 // idx; +f to the i accumulator (registers) and to the j accumulator (ds_add_f64, no return)
-template <int VARIANT, bool GUARD, bool RAGGED>
+// SHIFT (fast variant, spatial order): the tile pair's minimum-image multiples n (one per axis,
+// wave-uniform) are known to be those of every pair, so mic_r's rint(dx / L) is not recomputed
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
-                                        double* az, double& fx, double& fy, double& fz, const PairC& c) {
+                                        double* az, double& fx, double& fy, double& fz, const PairC& c,
+                                        const double* nsh = nullptr) {
     double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
-    mic_v<VARIANT, GUARD>(dx, dy, dz, c);
+    if constexpr (SHIFT) {
+        dx = fma(-nsh[0], c.L, dx);                 // = mic_r's fma(-rint(dx / L), L, dx)
+        dy = fma(-nsh[1], c.L, dy);
+        dz = fma(-nsh[2], c.L, dz);
+    } else {
+        mic_v<VARIANT, GUARD>(dx, dy, dz, c);
+    }
     double ft = pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];
     ft *= m;
@@ -363,6 +372,23 @@ extern "C" int mdqt_expt_n3_stamps(unsigned long long* out, int n) {
 // run order, skipping slots this rank does not write.
 // ------------------------------------------------------------------------------------------
 constexpr int BW = 16;                              // tiles per block = waves per workgroup
+#if defined(MDQT_EXPT_CLS)
+// diagnostic build only: tile-pair classes of k_pairs_n3b (skip, per pair, uniform image)
+__device__ unsigned long long g_cls_count[3];
+extern "C" int mdqt_expt_cls_count(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cls_count), sizeof(unsigned long long) * 3) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[3] = {0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_cls_count), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
+__device__ __forceinline__ double uniform_f64(double v) {   // a wave-uniform value into SGPRs
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
 
 __device__ __forceinline__ const double* tile_base(const double* Rall, int tile, int S) {
     const int g = tile * 64;                        // S is a multiple of 64: tiles never straddle slabs
@@ -370,22 +396,25 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
     return Rall + (size_t)w * 3 * S + (g - w * S);
 }
 
-template <int VARIANT, bool GUARD, bool RAGGED>
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false>
 __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi, double zi, double mi,
                                          const double (*pj)[128], const double* mj, double* ax, double* ay,
-                                         double* az, double& fx, double& fy, double& fz, const PairC& c) {
+                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
+                                         const double* nsh = nullptr) {
     if (!diag) {
         for (int t0 = 0; t0 < 64; t0 += 16) {
 #pragma unroll
             for (int t = 0; t < 16; ++t)
-                n3_step<VARIANT, GUARD, RAGGED>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
+                                                       c, nsh);
         }
     } else {
         for (int t0 = 1; t0 < 33; t0 += 16) {
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 const double m = (t0 + t == 32 && l >= 32) ? 0. : 1.;   // lane distance 32: once
-                n3_step<VARIANT, GUARD, RAGGED>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
+                                                       c, nsh);
             }
         }
     }
@@ -418,23 +447,36 @@ void k_pairs_n3b(N3BArgs a) {
         const double* p = tile_ptr(I) + l;
         xi = p[0]; yi = p[PS]; zi = p[2 * PS]; mi = 1.;
     }
-    // tile I's box (spatial order): a tile pair whose boxes are >= L/2 apart in the minimum image
-    // has no pair inside the cutoff (SpeedUp:222) and adds exact zeros: skipped whole
-    double bc[3] = {0., 0., 0.}, bh[3] = {0., 0., 0.};
-    if (srt && vI)
-#pragma unroll
-        for (int c3 = 0; c3 < 3; ++c3) { bc[c3] = a.boxes[(size_t)c3 * T + I]; bh[c3] = a.boxes[(size_t)(3 + c3) * T + I]; }
+    // Tile-pair classes in spatial order (SpeedUp:222 keeps a pair only below r = L/2), decided
+    // for all BW waves' tile pairs (I, J) by the staging wave's lanes 0..BW-1 into tp[q]:
+    //  * skip (force_sort 1): boxes >= L/2 apart in the minimum image — no pair inside the
+    //    cutoff, the tile pair adds exact zeros;
+    //  * uniform image: every pair's raw separation fl(xi - xj) lies in [fl(lo_I - hi_J),
+    //    fl(hi_I - lo_J)] (rounding is monotone), and so does rint(fl(dx / L)) between the rints
+    //    of the two ends; equal ends = one minimum-image multiple per axis for every pair, bit for
+    //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
+    //  * otherwise the per-pair minimum image.
+    __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class (-1 skip, 1 uniform, 0 per pair)
     const double rc2 = a.Rcut * a.Rcut;
-    auto far_apart = [&](int J) {
+    auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
+        const double* B = a.boxes;
         double g2 = 0.;
+        bool uni = true;
+        double n[3];
 #pragma unroll
         for (int c3 = 0; c3 < 3; ++c3) {
-            double d = bc[c3] - a.boxes[(size_t)c3 * T + J];
+            double d = B[(size_t)c3 * T + Iw] - B[(size_t)c3 * T + J];
             d = fma(-__builtin_rint(d * c.invL), a.L, d);
-            const double gap = fabs(d) - (bh[c3] + a.boxes[(size_t)(3 + c3) * T + J]);
+            const double gap = fabs(d) - (B[(size_t)(3 + c3) * T + Iw] + B[(size_t)(3 + c3) * T + J]);
             g2 = gap > 0. ? fma(gap, gap, g2) : g2;
+            const double lo = B[(size_t)(6 + c3) * T + Iw] - B[(size_t)(9 + c3) * T + J];
+            const double hi = B[(size_t)(9 + c3) * T + Iw] - B[(size_t)(6 + c3) * T + J];
+            const double nlo = __builtin_rint(lo * c.invL), nhi = __builtin_rint(hi * c.invL);
+            uni = uni && (nlo == nhi);
+            n[c3] = nlo;
         }
-        return g2 > rc2;
+        const double cls = (a.use_sort == 1 && g2 > rc2) ? -1. : (VARIANT == 1 && uni) ? 1. : 0.;
+        return make_double4(n[0], n[1], n[2], cls);
     };
     // the run's i accumulator lives in LDS (read and written once per block distance) so that
     // the three-level blocking fits the 64-VGPR budget of two 16-wave workgroups per CU
@@ -460,11 +502,19 @@ void k_pairs_n3b(N3BArgs a) {
                 pj[1][l] = yj; pj[1][l + 64] = yj;
                 pj[2][l] = zj; pj[2][l + 64] = zj;
                 mj[l] = vj ? 1. : 0.; mj[l + 64] = mj[l];
+                if (srt && l < BW && P * BW + l < T) {
+                    const double4 t4 = classify(P * BW + l, J);
+                    tp[l][0] = t4.x; tp[l][1] = t4.y; tp[l][2] = t4.z; tp[l][3] = t4.w;
+#if defined(MDQT_EXPT_CLS)
+                    atomicAdd(&g_cls_count[(int)t4.w + 1], 1ull);
+#endif
+                }
             }
 #pragma unroll
             for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
             __syncthreads();
-            if (vI && (db > 0 || J >= I) && !(a.use_sort == 1 && far_apart(J))) {
+            const double cls = srt ? uniform_f64(tp[q][3]) : 0.;
+            if (vI && (db > 0 || J >= I) && cls >= 0.) {
                 const bool diag = (db == 0 && J == I);
                 // blocked i accumulation: the tile pair's 64 steps into a fresh sum, those into the
                 // block distance's sum, those into the run's (a run is ~1e5 pair terms at N = 1e6;
@@ -473,7 +523,11 @@ void k_pairs_n3b(N3BArgs a) {
                 double tx = 0., ty = 0., tz = 0.;
                 if (ragN && (I == T - 1 || J == T - 1))
                     n3b_pair<VARIANT, GUARD, true>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
-                else
+                else if (VARIANT == 1 && cls > 0.) {
+                    const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
+                    n3b_pair<VARIANT, GUARD, false, VARIANT == 1>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
+                                                                  tz, c, nsh);
+                } else
                     n3b_pair<VARIANT, GUARD, false>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
                 bx += tx; by += ty; bz += tz;
             }

@@ -279,7 +279,7 @@ struct N3BArgs {
                         // 2: the same order, nothing skipped (tests: bit-identical to 1)
     const double* Rs;   // [3][Npad] positions in sorted order
     const int* perm;    // sorted index -> ion
-    const double* boxes;// [6][T]: tile center (x, y, z), half extents (x, y, z)
+    const double* boxes;// [12][T]: tile center (x, y, z), half extents, raw coordinate min, max
 };
 struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]
@@ -290,7 +290,7 @@ struct SortArgs {
     void* tmp;               // hipCUB radix-sort scratch
     size_t tmp_bytes;
     double* Rs;              // out [3][Npad]
-    double* boxes;           // out [6][T]
+    double* boxes;           // out [12][T]
 };
 hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s);
 size_t spatial_order_tmp_bytes(int N);

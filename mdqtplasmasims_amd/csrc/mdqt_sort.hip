@@ -83,7 +83,9 @@ __global__ __launch_bounds__(256) void k_gather_sorted(const double* __restrict_
     }
 }
 
-// one wave per tile; boxes[c][T] = center, boxes[3 + c][T] = half extent (+ a rounding margin)
+// one wave per tile; boxes[c][T] = center, boxes[3 + c][T] = half extent (+ a rounding margin),
+// boxes[6 + c][T] / boxes[9 + c][T] = min / max of the raw coordinates (exact; for the tile pair's
+// uniform minimum image in k_pairs_n3b)
 __global__ __launch_bounds__(256) void k_tile_boxes(const double* __restrict__ Rs, int N, int Npad, int T, double L,
                                                     double* __restrict__ boxes) {
     const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -99,14 +101,19 @@ __global__ __launch_bounds__(256) void k_tile_boxes(const double* __restrict__ R
         double d = v ? X[j] - ref : 0.;
         d = fma(-__builtin_rint(d * invL), L, d);          // minimum-image offset from the reference ion
         double lo = d, hi = d;
+        double rl = v ? X[j] : ref, rh = rl;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) {
             lo = fmin(lo, __shfl_xor(lo, m));
             hi = fmax(hi, __shfl_xor(hi, m));
+            rl = fmin(rl, __shfl_xor(rl, m));
+            rh = fmax(rh, __shfl_xor(rh, m));
         }
         if (l == c) {
             boxes[(size_t)c * T + tile] = ref + 0.5 * (lo + hi);
             boxes[(size_t)(3 + c) * T + tile] = 0.5 * (hi - lo) * (1. + 1e-12) + 1e-12 * L;
+            boxes[(size_t)(6 + c) * T + tile] = rl;
+            boxes[(size_t)(9 + c) * T + tile] = rh;
         }
     }
 }

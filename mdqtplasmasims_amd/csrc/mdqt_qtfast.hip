@@ -310,7 +310,9 @@ __device__ unsigned long long g_qt_stamps[6 * 4096];
 #else
 #define LANE_WPE_ATTR
 #endif
-template <bool DPPX>
+// ALLMOVE: the launch drifts (do_step) and every substep has t > 0 (all but the simulation's first
+// launch): step_R's non-moving branch (:360) and the last substep's no-drift select compiled out
+template <bool DPPX, bool ALLMOVE>
 __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
 #if defined(MDQT_EXPT_QTSTAMPS)
     unsigned long long st_[6];
@@ -377,22 +379,14 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     }
     const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
     const uint64_t gid = a.gid0 + (uint64_t)i;
-    // per-substep constants in registers, not kernel-argument loads inside the substep loop (a
-    // scalar load indexed by the substep waits ~100+ cycles in every iteration): the moving flags
-    // as a bit mask, expDetuning(t) of substep s in lane s & 15 of the row (s < 16: ed0, else ed1)
+    // per-substep constants out of kernel-argument loads inside the substep loop (a scalar load
+    // indexed by the substep waits ~100+ cycles in every iteration): the moving flags as a bit
+    // mask, expDetuning(t) of every substep in an LDS row (one broadcast read per substep, issued
+    // with the uniforms; it replaces a readlane and its scalar branches in every iteration)
     const uint32_t movmask = a.movmask;
-    const bool edz = a.expdet_zero != 0;
-    const double ed0 = edz ? 0. : a.expDet[k], ed1 = edz ? 0. : a.expDet[k + 16];
-    // (read ed0 / ed1 themselves, written with every lane active: a value selected per lane
-    // inside a divergent branch would be stale in the inactive lane the read picks)
-    auto rl = [](double e, int l) {
-        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(e), l),
-                                __builtin_amdgcn_readlane(__double2loint(e), l));
-    };
-    auto expdet = [&](int s) -> double {
-        if (edz) return 0.;
-        return s < 16 ? rl(ed0, s & 15) : rl(ed1, s & 15);
-    };
+    __shared__ double edt[MAXSUB];
+    if (threadIdx.x < MAXSUB)
+        edt[threadIdx.x] = (a.expdet_zero != 0 || (int)threadIdx.x >= a.nsub) ? 0. : a.expDet[threadIdx.x];
     // u1, u2 of every substep of the launch staged in LDS: Philox draws computed lane-parallel
     // (lane k: substeps k, k + 16), or the rng_mode 0 uniforms of the single substep
     __shared__ double su[kLaneWG / 16][MAXSUB][2];
@@ -440,7 +434,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         y0 = {t0.x, t0.y}; y1 = {t1.x, t1.y}; y2 = {t2.x, t2.y};
     };
     auto drift = [&](double& pp, double& vv, int sub) {   // step(): step_R, step_V, step_R (:418-430)
-        const bool moving = (movmask >> sub) & 1u;
+        const bool moving = ALLMOVE || ((movmask >> sub) & 1u);
         pp = half_drift(pp, vv, f, moving, DT, DT2, L);
         vv = vv + dt * f;                             // step_V(dt) :398-409
         pp = half_drift(pp, vv, f, moving, DT, DT2, L);
@@ -455,10 +449,11 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         // they are evaluated before s's Runge-Kutta stages and overlap them.  Same operations on
         // the same values as the plain order: bit-identical.
         if (a.do_step) drift(p, v, 0);
+        double pre_p = p, pre_v = v;                  // ALLMOVE: the state after the last substep
         double sn, cs;
-        sincos_q<true>(((v * qc.pv2q + expdet(0)) * cphi) * (tPart + qc.dtQ), sn, cs);
+        double u = v * qc.pv2q + edt[0];              // vx on every state lane (carried: the next
+        sincos_q<true>((u * cphi) * (tPart + qc.dtQ), sn, cs);   // substep's is formed with its phase)
         for (int s = 0; s < a.nsub; ++s) {
-            const double u = v * qc.pv2q + expdet(s);      // vx on every state lane
             tPart += qc.dtQ;
             const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp) : lane_sum_p(nrm2(w) * hdp);
             const double u1 = su[grp][s][0], u2 = su[grp][s][1];
@@ -469,17 +464,25 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
             // substep s + 1's drift and phase, placed in the same basic block as the work they
             // overlap (straight-line: the last substep computes a harmless extra value, the
             // |phi| >= 2^20 library fallback is applied afterwards)
-            double vn, pn, phin, snn, csn;
+            double vn, pn, un, phin, snn, csn;
             auto next_phase = [&]() {
                 vn = fma(kmask, kick, v);             // :705 (x lanes)
                 pn = p;
                 const int s1 = s + 1 < a.nsub ? s + 1 : s;
                 double pd = pn, vd = vn;
                 drift(pd, vd, s1);
-                const bool adv = a.do_step && s + 1 < a.nsub;   // no drift after the last substep
-                pn = adv ? pd : pn;
-                vn = adv ? vd : vn;
-                phin = ((vn * qc.pv2q + expdet(s1)) * cphi) * (tPart + qc.dtQ);
+                if constexpr (ALLMOVE) {              // always advance; the launch keeps the state
+                    pre_p = pn;                       // before the last substep's extra drift
+                    pre_v = vn;
+                    pn = pd;
+                    vn = vd;
+                } else {
+                    const bool adv = a.do_step && s + 1 < a.nsub;   // no drift after the last substep
+                    pn = adv ? pd : pn;
+                    vn = adv ? vd : vn;
+                }
+                un = vn * qc.pv2q + edt[s1];
+                phin = (un * cphi) * (tPart + qc.dtQ);
                 sincos_fast(phin, snn, csn);
             };
             if (nojump) {
@@ -534,8 +537,13 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
             }();
             v = vn;
             p = pn;
+            u = un;
             sn = snn;
             cs = csn;
+        }
+        if constexpr (ALLMOVE) {
+            p = pre_p;
+            v = pre_v;
         }
     }
     QT_STAMP(2, __builtin_amdgcn_s_memtime());
@@ -582,8 +590,15 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
     if (a.qc.model < 0 || a.qc.model >= NMODELS) return hipErrorInvalidValue;
     const dim3 gl((a.n + kLaneWG / 16 - 1) / (kLaneWG / 16)), bl(kLaneWG), gt((a.n + 255) / 256), b(256);
     if (mode == 2) {
-        if (a.qc.model == 0) launch_timed(k_substeps_lanes_r<true>, gl, bl, s, ev0, ev1, a, tab + 1);
-        else launch_timed(k_substeps_lanes_r<false>, gl, bl, s, ev0, ev1, a, tab + 1);
+        const uint64_t all = (1ull << a.nsub) - 1;
+        const bool allmove = a.do_step && (a.movmask & all) == all;
+        if (a.qc.model == 0) {
+            if (allmove) launch_timed(k_substeps_lanes_r<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+            else launch_timed(k_substeps_lanes_r<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+        } else {
+            if (allmove) launch_timed(k_substeps_lanes_r<false, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+            else launch_timed(k_substeps_lanes_r<false, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+        }
     }
     else if (a.qc.model == 0) launch_timed(k_substeps_r<0>, gt, b, s, ev0, ev1, a, tab);
     else if (a.qc.model == 1) launch_timed(k_substeps_r<1>, gt, b, s, ev0, ev1, a, tab);

@@ -119,6 +119,18 @@ __device__ __forceinline__ cxd renorm_div(cxd w, double sumsq) {
 #ifndef MDQT_FAST_SINCOS
 #define MDQT_FAST_SINCOS 1
 #endif
+// Horner step z * p + c as one three-address v_fma_f64.  (With the coefficient c held in a VGPR —
+// the lane kernel's SGPRs are all taken — the compiler otherwise emits a copy of c and the
+// two-address v_fmac_f64: one extra VALU per step.)  Same operation, same value as fma(z, p, c).
+__device__ __forceinline__ double hfma(double z, double p, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(p), "v"(c));
+    return r;
+#else
+    return fma(z, p, c);
+#endif
+}
 // the reduction + kernels without the range check (valid for |x| < 2^20), branch-free
 __device__ __forceinline__ void sincos_fast(double x, double& sn, double& cs) {
     const double n = rint(x * 0.63661977236758134308);           // 2/pi
@@ -126,13 +138,13 @@ __device__ __forceinline__ void sincos_fast(double x, double& sn, double& cs) {
     r = fma(-n, 6.12323399573676603587e-17, r);
     r = fma(-n, -1.49738490485916983014e-33, r);
     const double z = r * r;
-    const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
-                                         2.75573137070700676789e-06), -1.98412698298579493134e-04),
-                          8.33333333332248946124e-03);
-    const double sr = fma(r * z, fma(z, ps, -1.66666666666666324348e-01), r);
-    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
-                                                 -2.75573143513906633035e-07), 2.48015872894767294178e-05),
-                                  -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+    const double ps = hfma(z, hfma(z, hfma(z, hfma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                           2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                           8.33333333332248946124e-03);
+    const double sr = fma(r * z, hfma(z, ps, -1.66666666666666324348e-01), r);
+    const double pc = z * hfma(z, hfma(z, hfma(z, hfma(z, hfma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                    -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                                   -1.38888888888741095749e-03), 4.16666666666666019037e-02);
     const double hz = 0.5 * z;
     const double wc = 1.0 - hz;
     const double cr = wc + (((1.0 - wc) - hz) + z * pc);

@@ -310,9 +310,11 @@ __device__ unsigned long long g_qt_stamps[6 * 4096];
 #else
 #define LANE_WPE_ATTR
 #endif
-// ALLMOVE: the launch drifts (do_step) and every substep has t > 0 (all but the simulation's first
-// launch): step_R's non-moving branch (:360) and the last substep's no-drift select compiled out
-template <bool DPPX, bool ALLMOVE>
+// FAST: the production launch — step + qstep (do_step, do_qt), every substep with t > 0 (all but
+// the simulation's first launch), F from the force slots (nseg > 1), no arrival wait: step_R's
+// non-moving branch (:360), the last substep's no-drift select and the other paths' loads and
+// branches are compiled out (straight-line prologue: one memory round trip)
+template <bool DPPX, bool FAST>
 __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
 #if defined(MDQT_EXPT_QTSTAMPS)
     unsigned long long st_[6];
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     double p = a.R[(size_t)c * S + i], v = a.V[(size_t)c * S + i], f;
     double tPart = a.tPart[i];
     cxd w = {0., 0.};
-    if (a.do_qt && st < NS) w = {a.psi[(size_t)(2 * st) * S + i], a.psi[(size_t)(2 * st + 1) * S + i]};
+    if ((FAST || a.do_qt) && st < NS) w = {a.psi[(size_t)(2 * st) * S + i], a.psi[(size_t)(2 * st + 1) * S + i]};
     const int nseg = a.nseg;
     // F: the canonical slot_sum16 distributed over the ion's 16 lanes — lane k forms the strided
     // partial q_k of all three components (its loads issued together, 4 slots per round), the
@@ -351,28 +353,45 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     double qf[3] = {0., 0., 0.};
     // overlapped MD step (a.arrive): the partials are read after the arrival wait below, with
     // L1-bypassing loads; otherwise right here, with the other prologue loads
-    auto slot_partials = [&](bool sc1) {
+    auto slot_round = [&](int s0, double (*t)[3], bool sc1) {   // slots s0, s0 + 16, + 32, + 48
         const double* base_p = a.Fpart + i;
         const size_t plane = (size_t)3 * S;
-        for (int s0 = k; s0 < nseg; s0 += 64) {
-            double t[4][3];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int sl = s0 + 16 * u;
+        for (int u = 0; u < 4; ++u) {
+            const int sl = s0 + 16 * u;
 #pragma unroll
-                for (int cc = 0; cc < 3; ++cc) {
+            for (int cc = 0; cc < 3; ++cc) {
+                if (FAST) {   // unconditional loads (clamped slot, in range), the select at the sum:
+                              // no branch around the load, so nothing forces an early wait on it
+                    const double* q = base_p + (size_t)min(sl, nseg - 1) * plane + (size_t)cc * S;
+                    const double x = *q;
+                    t[u][cc] = sl < nseg ? x : 0.;
+                } else {
                     const double* q = base_p + (size_t)sl * plane + (size_t)cc * S;
                     t[u][cc] = sl < nseg ? (sc1 ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q)
                                          : 0.;
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int cc = 0; cc < 3; ++cc) qf[cc] = qf[cc] + t[u][cc];
         }
     };
-    if (nseg > 1) {
+    auto slot_add = [&](double (*t)[3]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) qf[cc] = qf[cc] + t[u][cc];
+    };
+    auto slot_partials = [&](bool sc1) {
+        for (int s0 = k; s0 < nseg; s0 += 64) {
+            double t[4][3];
+            slot_round(s0, t, sc1);
+            slot_add(t);
+        }
+    };
+    // FAST: the first round's loads stay in flight across the Philox draws below; summed after
+    double t0[4][3];
+    if (FAST) {
+        slot_round(k, t0, false);
+    } else if (nseg > 1) {
         if (!a.arrive) slot_partials(false);
     } else {
         f = a.F[(size_t)c * S + i];
@@ -385,12 +404,14 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     // with the uniforms; it replaces a readlane and its scalar branches in every iteration)
     const uint32_t movmask = a.movmask;
     __shared__ double edt[MAXSUB];
-    if (threadIdx.x < MAXSUB)
-        edt[threadIdx.x] = (a.expdet_zero != 0 || (int)threadIdx.x >= a.nsub) ? 0. : a.expDet[threadIdx.x];
+    // (loaded here, written to LDS after the force sum below: an LDS write of a loaded value waits
+    // for every load issued before it, which would stall the Philox draws behind the slot loads)
+    const double edv = (threadIdx.x < MAXSUB && a.expdet_zero == 0 && (int)threadIdx.x < a.nsub)
+                           ? a.expDet[threadIdx.x] : 0.;
     // u1, u2 of every substep of the launch staged in LDS: Philox draws computed lane-parallel
     // (lane k: substeps k, k + 16), or the rng_mode 0 uniforms of the single substep
     __shared__ double su[kLaneWG / 16][MAXSUB][2];
-    if (a.do_qt) {
+    if (FAST || a.do_qt) {
         if (a.U) {
             if (k == 0) { su[grp][0][0] = a.U[i]; su[grp][0][1] = a.U[(size_t)S + i]; }
         } else {
@@ -402,7 +423,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
             }
         }
     }
-    if (a.arrive) {                                   // wait for the concurrent force launch
+    if (!FAST && a.arrive) {                          // wait for the concurrent force launch
         if (threadIdx.x == 0) {
             int it = 0;
             while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
@@ -413,11 +434,20 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         __syncthreads();
         if (nseg > 1) slot_partials(true);
     }
-    if (nseg > 1) {
+    if (FAST) {
+        slot_add(t0);
+        for (int s0 = k + 64; s0 < nseg; s0 += 64) {
+            double t[4][3];
+            slot_round(s0, t, false);
+            slot_add(t);
+        }
+    }
+    if (FAST || nseg > 1) {
         const double fx = lane_tree16(qf[0]), fy = lane_tree16(qf[1]), fz = lane_tree16(qf[2]);
         f = c == 0 ? fx : c == 1 ? fy : fz;
         if (store && owner) a.F[(size_t)c * S + i] = f;
     }
+    if (threadIdx.x < MAXSUB) edt[threadIdx.x] = edv;
     __syncthreads();
     __shared__ double2 xg[DPPX ? 1 : kLaneWG];
     auto exchange = [&](cxd y, cxd& y0, cxd& y1, cxd& y2) {
@@ -434,13 +464,13 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         y0 = {t0.x, t0.y}; y1 = {t1.x, t1.y}; y2 = {t2.x, t2.y};
     };
     auto drift = [&](double& pp, double& vv, int sub) {   // step(): step_R, step_V, step_R (:418-430)
-        const bool moving = ALLMOVE || ((movmask >> sub) & 1u);
+        const bool moving = FAST || ((movmask >> sub) & 1u);
         pp = half_drift(pp, vv, f, moving, DT, DT2, L);
         vv = vv + dt * f;                             // step_V(dt) :398-409
         pp = half_drift(pp, vv, f, moving, DT, DT2, L);
     };
     QT_STAMP(1, __builtin_amdgcn_s_memtime());
-    if (!a.do_qt) {
+    if (!FAST && !a.do_qt) {
         if (a.do_step)
             for (int s = 0; s < a.nsub; ++s) drift(p, v, s);
     } else {
@@ -448,8 +478,8 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         // and the sin / cos of its coupling phase (:508) depend on nothing else of substep s, so
         // they are evaluated before s's Runge-Kutta stages and overlap them.  Same operations on
         // the same values as the plain order: bit-identical.
-        if (a.do_step) drift(p, v, 0);
-        double pre_p = p, pre_v = v;                  // ALLMOVE: the state after the last substep
+        if (FAST || a.do_step) drift(p, v, 0);
+        double pre_p = p, pre_v = v;                  // FAST: the state after the last substep
         double sn, cs;
         double u = v * qc.pv2q + edt[0];              // vx on every state lane (carried: the next
         sincos_q<true>((u * cphi) * (tPart + qc.dtQ), sn, cs);   // substep's is formed with its phase)
@@ -471,7 +501,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
                 const int s1 = s + 1 < a.nsub ? s + 1 : s;
                 double pd = pn, vd = vn;
                 drift(pd, vd, s1);
-                if constexpr (ALLMOVE) {              // always advance; the launch keeps the state
+                if constexpr (FAST) {                 // always advance; the launch keeps the state
                     pre_p = pn;                       // before the last substep's extra drift
                     pre_v = vn;
                     pn = pd;
@@ -541,7 +571,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
             sn = snn;
             cs = csn;
         }
-        if constexpr (ALLMOVE) {
+        if constexpr (FAST) {
             p = pre_p;
             v = pre_v;
         }
@@ -553,7 +583,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
             a.V[(size_t)c * S + i] = v;
             if (!(p >= -0.125 * L && p <= 1.125 * L)) *a.oor = 1;
         }
-        if (a.do_qt) {
+        if (FAST || a.do_qt) {
             if (k == 0) a.tPart[i] = tPart;
             if (st < NS) {
                 a.psi[(size_t)(2 * st) * S + i] = w.re;
@@ -591,7 +621,7 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
     const dim3 gl((a.n + kLaneWG / 16 - 1) / (kLaneWG / 16)), bl(kLaneWG), gt((a.n + 255) / 256), b(256);
     if (mode == 2) {
         const uint64_t all = (1ull << a.nsub) - 1;
-        const bool allmove = a.do_step && (a.movmask & all) == all;
+        const bool allmove = a.do_step && a.do_qt && a.nseg > 1 && !a.arrive && (a.movmask & all) == all;
         if (a.qc.model == 0) {
             if (allmove) launch_timed(k_substeps_lanes_r<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
             else launch_timed(k_substeps_lanes_r<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);

@@ -552,9 +552,17 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
                     n3 = dpp<BCAST(2)>(nk); n4 = dpp<BCAST(3)>(nk); n5 = dpp<BCAST(4)>(nk); n6 = dpp<BCAST(5)>(nk);
                 }
                 double randDOrS, randDir, rand3, dummy;
-                draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
-                draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
-                (void)dummy;
+                if (a.U) {
+                    draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 1, randDOrS, randDir);
+                    draw_pair(qc, a.U, S, i, gid, a.q0 + (uint64_t)s, 2, rand3, dummy);
+                    (void)dummy;
+                } else {                              // both pairs in one Philox evaluation: lanes 0-7
+                    double x0, x1;                    // draw pair 1, lanes 8-15 pair 2 (the whole
+                    philox_pair(qc, gid, a.q0 + (uint64_t)s, k < 8 ? 1 : 2, x0, x1);   // group is active)
+                    randDOrS = dpp<BCAST(0)>(x0);
+                    randDir = dpp<BCAST(0)>(x1);
+                    rand3 = dpp<BCAST(8)>(x0);
+                }
                 const int target = qc.model == 0 ? jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick)
                                                  : jump_target_pump(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
                 w = {st == target ? 1. : 0., 0.};

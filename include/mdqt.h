@@ -218,6 +218,10 @@ int         mdqt_partial_observables(mdqt_ctx* c, double vxAvg, double out5[5], 
  * syncs, returns the summed device time (ms) and bracketed-launch counts since the last
  * call, and resets. */
 int         mdqt_enable_timing(mdqt_ctx* c, int period);
+/* the same for one kind only: kinds bit 0 = force launches, bit 1 = fused-substep launches (an
+ * event-timed launch costs its MD step a few us, so a timed region may sample only its dominant
+ * kernel) */
+int         mdqt_enable_timing_kinds(mdqt_ctx* c, int period, int kinds);
 int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
                                     int* nsub);
 

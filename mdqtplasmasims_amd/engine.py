@@ -315,9 +315,10 @@ class Simulation:
     def comm_init(self, uid: bytes):
         check(lib().mdqt_comm_init(self.h, uid, len(uid)), "comm_init")
 
-    def enable_timing(self, period: int = 1):
-        """bracket every `period`-th hot-kernel launch with HIP events (0/False: off)"""
-        check(lib().mdqt_enable_timing(self.h, int(period)))
+    def enable_timing(self, period: int = 1, kinds: int = 3):
+        """bracket every `period`-th hot-kernel launch with HIP events (0/False: off); kinds:
+        bit 0 force launches, bit 1 fused-substep launches"""
+        check(lib().mdqt_enable_timing_kinds(self.h, int(period), int(kinds)))
 
     def kernel_time_totals(self):
         """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""

@@ -87,20 +87,23 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r01_v11_c2_pmc.json")):
+def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r02_c2_pmc.json")):
     """HBM bytes per launch of the kernel from the committed rocprofv3 --pmc summary of the same
     C2 workload (FETCH_SIZE and WRITE_SIZE in separate passes, kB -> B; no gfx950 x2 read
-    correction: the kernel's loads are 8 B/lane, outside the guide's calibrated 16 B/lane case)."""
+    correction: the kernel's loads are 8 B/lane, outside the guide's calibrated 16 B/lane case).
+    The production instance (the most dispatched one of the kernel family) is taken."""
     try:
         with open(path) as f:
             d = json.load(f)
     except OSError:
         return None
+    best = None
     for k, v in d.items():
         short = k.split("(")[0].replace("void ", "").replace("mdqt::", "")
         if short.startswith(kernel_prefix) and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            return (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
-    return None
+            if best is None or v.get("dispatches", 0) > best.get("dispatches", 0):
+                best = v
+    return None if best is None else (best["FETCH_SIZE"] + best["WRITE_SIZE"]) * 1024.0
 
 
 def cpu_threads():

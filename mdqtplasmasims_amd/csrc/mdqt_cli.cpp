@@ -6,6 +6,10 @@
 // Writes the same directory tree (SpeedUp:1143-1160) and the same files
 // (energies.dat, vel_dist{X,Y,Z}_time%06d.dat, statePopulationsVsVTime%06d.dat,
 // ions_/conditions_/VZERO_/wvFns_timestep%06d.dat) through the C ABI of include/mdqt.h.
+//
+//   --pump_program=1|2|3 runs instead the main() of randomFrozenStartTag408Linear.cpp /
+//   408Quad.cpp / 422Linear.cpp (their defaults, :52-80; mdqt_run_pump): the PumpTime...
+//   directory, spinUpIons_*, taggedMoments.dat, tagged vel_distX_*, VAF.dat, the conditions.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -20,13 +24,19 @@ static void usage(void) {
             "                  [--N0=3500] [--newRun=1] [--c0=0] [--sampleFreq=40]\n"
             "                  [--reNormalizewvFns=0] [--saveDirectory=dataLaserCool/]\n"
             "                  [--seed=<srand48 seed; default time(NULL)+job as SpeedUp:1219>]\n"
-            "                  [--qt=1] [--device=-1]\n");
+            "                  [--qt=1] [--device=-1]\n"
+            "       mdqt <job> --pump_program=1|2|3 [--tpumpreal=2e-7] [--tstartV0=15] [... as above]\n");
 }
 
 int main(int argc, char** argv) {
     if (argc < 2) { usage(); return 2; }
     mdqt_params p;
     mdqt_default_params(&p);
+    int pump = 0;                                           // the pumping programs' defaults first
+    for (int i = 2; i < argc; ++i)
+        if (!strncmp(argv[i], "--pump_program=", 15)) pump = atoi(argv[i] + 15);
+    if (pump < 0 || pump > 3) { usage(); return 2; }
+    if (pump) mdqt_default_params_pump(&p, pump);
     const double job = atof(argv[1]);                       // SpeedUp:1145
     p.job = (uint32_t)job;
     int seed_given = 0;
@@ -43,11 +53,12 @@ int main(int argc, char** argv) {
 #define DPAR(name) if (!strcmp(key, #name)) { p.name = atof(v); continue; }
 #define IPAR(name) if (!strcmp(key, #name)) { p.name = atoi(v); continue; }
         DPAR(Ge) DPAR(tmax) DPAR(density) DPAR(sig0) DPAR(Te) DPAR(fracOfSig) DPAR(detuning)
-        DPAR(detuningDP) DPAR(Om) DPAR(OmDP)
+        DPAR(detuningDP) DPAR(Om) DPAR(OmDP) DPAR(tpumpreal) DPAR(tstartV0)
         IPAR(N0) IPAR(newRun) IPAR(c0) IPAR(sampleFreq) IPAR(reNormalizewvFns) IPAR(device) IPAR(qt_model)
 #undef DPAR
 #undef IPAR
         if (!strcmp(key, "qt")) { p.qt_enabled = atoi(v); continue; }
+        if (!strcmp(key, "pump_program")) continue;         // applied above
         if (!strcmp(key, "seed")) { p.seed = (uint32_t)strtoul(v, NULL, 10); seed_given = 1; continue; }
         if (!strcmp(key, "saveDirectory")) {
             strncpy(p.saveDirectory, v, sizeof(p.saveDirectory) - 1);
@@ -62,7 +73,7 @@ int main(int argc, char** argv) {
         fprintf(stderr, "mdqt: %s\n", mdqt_last_error());
         return 1;
     }
-    int rc = mdqt_run(c);
+    int rc = pump ? mdqt_run_pump(c) : mdqt_run(c);
     if (rc) fprintf(stderr, "mdqt: %s\n", mdqt_last_error());
     else printf("%i\n", mdqt_get_N(c));
     mdqt_destroy(c);

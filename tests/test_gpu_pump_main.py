@@ -81,3 +81,21 @@ def test_pump_program_directory_names(tmp_path):
         s.run_pump()                                     # tmax < 0: directories, init(), writeConditions only
         assert os.path.basename(os.path.dirname(s.save_directory.rstrip("/"))) == name, s.save_directory
         s.close()
+
+
+def test_cli_pump_program(tmp_path):
+    """`mdqt <job> --pump_program=3` runs the 422 nm program's main(): its defaults
+    (randomFrozenStartTag422Linear.cpp:52-78) overridden by the flags, the PumpTime... tree"""
+    import subprocess
+    from mdqtplasmasims_amd import CLI_PATH
+    r = subprocess.run([CLI_PATH, "2", "--pump_program=3", "--N0=300", "--tmax=0.3", "--sampleFreq=10",
+                        "--tpumpreal=5.2e-8", "--tstartV0=0.1", "--seed=5", f"--saveDirectory={tmp_path}/"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    dirs = [d for d in os.listdir(tmp_path) if d.startswith("PumpTime")]
+    assert len(dirs) == 1 and dirs[0].endswith("Det100Om130Density20Ge100NumIons300"), dirs
+    job = tmp_path / dirs[0] / "job2"
+    names = os.listdir(job)
+    assert "taggedMoments.dat" in names and "VAF.dat" in names and "energies.dat" in names
+    assert any(n.startswith("spinUpIons_timestep") for n in names)
+    assert any(n.startswith("vel_distX_timestep") for n in names)

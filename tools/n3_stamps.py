@@ -44,3 +44,12 @@ hist = np.histogram(st, bins=10)[0]
 clk = (a[:, 5] - a[:, 4]) / np.maximum(a[:, 1] - a[:, 0], 1) * 100e6 / 1e9
 print("core clock GHz (s_memtime / s_memrealtime) pct 0/50/100:", np.percentile(clk, [0, 50, 100]).round(3))
 print("start histogram (10 bins over span):", hist)
+# per-CU end times grouped by the number of workgroups the CU ran
+last = {}
+for kk, e, c in zip(key, en, np.ones_like(en)):
+    last.setdefault(kk, []).append(e)
+by = {}
+for kk, es in last.items():
+    by.setdefault(len(es), []).append(max(es))
+for nwg, ends in sorted(by.items()):
+    print(f"CUs with {nwg} WGs: {len(ends)}, last end pct 0/50/100:", np.percentile(ends, [0, 50, 100]).round(2))

@@ -118,8 +118,13 @@ struct mdqt_ctx {
     int overlap_opt = 0;
     hipStream_t qs = nullptr;              // the QT stream
     hipEvent_t evQ = nullptr, evS = nullptr;
-    unsigned long long* dArrive = nullptr; // force workgroups finished, monotonic
-    unsigned long long arriveEpoch = 0;
+    unsigned long long* dArrive = nullptr; // [ntiles] finished tile pairs per tile, monotonic
+    int arriveCap = 0;                     // tiles dArrive holds
+    unsigned long long arriveEpoch = 0;    // each counter's value after the last launch (T per launch)
+    // one MD step in one launch (option "fused_step", OFF by default — measured slower, DESIGN.md
+    // §8): k_md_step, see md_step_fused
+    int fused_opt = 0;
+    int last_fused = 0;                    // the last MD step ran as one k_md_step launch
     int* dSpinErr = nullptr;
     unsigned long long* force_arrive = nullptr;   // set around a force launch of an overlapped step
     hipStream_t sub_stream = nullptr;             // set around the QT launch of an overlapped step
@@ -800,6 +805,8 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_segments")) return s->nseg;
     if (!strcmp(n, "force_scheme")) return s->use_n3b ? 3 : s->use_n3 ? 2 : 1;
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
+    if (!strcmp(n, "fused_step")) return s->fused_opt;
+    if (!strcmp(n, "md_step_fused")) return s->last_fused;     // 1: the last MD step was one k_md_step launch
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
     return NAN;
@@ -1249,24 +1256,40 @@ static bool overlap_applies(const mdqt_ctx* s) {
            (s->substep_mode == 2 || (s->substep_mode == 0 && s->nloc < kLaneKernelMaxIons));
 }
 
+// per-tile arrival counters of the overlapped / fused MD step (monotonic: a launch adds T to
+// every tile's counter, the waiters compare with the running epoch)
+static int arrive_setup(mdqt_ctx* s) {
+    const int T = (s->N + 63) / 64;
+    if (s->dArrive && s->arriveCap >= T) return 0;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    if (s->qs) HIPCHK(hipStreamSynchronize(s->qs));
+    if (s->dArrive) HIPCHK(hipFree(s->dArrive));
+    s->dArrive = nullptr;
+    HIPCHK(hipMalloc(&s->dArrive, (size_t)T * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(s->dArrive, 0, (size_t)T * sizeof(unsigned long long)));
+    if (!s->dSpinErr) {
+        HIPCHK(hipMalloc(&s->dSpinErr, sizeof(int)));
+        HIPCHK(hipMemset(s->dSpinErr, 0, sizeof(int)));
+    }
+    HIPCHK(hipDeviceSynchronize());
+    s->arriveCap = T;
+    s->arriveEpoch = 0;
+    return 0;
+}
+
 static int overlap_setup(mdqt_ctx* s) {
+    if (arrive_setup(s)) return -1;
     if (s->qs) return 0;
     HIPCHK(hipStreamCreateWithFlags(&s->qs, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&s->evQ, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(hipEventCreateWithFlags(&s->evS, hipEventDisableTiming | hipEventDisableSystemFence));
-    HIPCHK(hipMalloc(&s->dArrive, sizeof(unsigned long long)));
-    HIPCHK(hipMalloc(&s->dSpinErr, sizeof(int)));
-    HIPCHK(hipMemset(s->dArrive, 0, sizeof(unsigned long long)));
-    HIPCHK(hipMemset(s->dSpinErr, 0, sizeof(int)));
-    HIPCHK(hipDeviceSynchronize());
-    s->arriveEpoch = 0;
     return 0;
 }
 
 // MD steps with the force and QT launches overlapped: step k's force launch (context stream)
 // waits for step k-1's QT launch by an event; step k's QT launch (its own stream, in order after
 // step k-1's) starts at once, issues its prologue loads and Philox draws while the forces are
-// computed, and waits on the device until all force workgroups of step k have arrived.  Same
+// computed, and waits on the device until the tile pairs of its ions' tile have arrived.  Same
 // kernels, same operations: bit-identical to the sequential order (tests/test_gpu_parity.py).
 // Measured at C2 (one MI355X): 104-107 us per MD step against 45.6 sequential — the two
 // cross-stream event waits cost ~17 us per step by themselves, and the resident QT waves (176
@@ -1283,7 +1306,7 @@ static int md_steps_overlapped(mdqt_ctx* s, int n) {
         const int rc = mdqt_forces(s);
         s->force_arrive = nullptr;
         if (rc) return -1;
-        s->arriveEpoch += (unsigned long long)s->npairs;
+        s->arriveEpoch += (unsigned long long)((s->N + 63) / 64);   // T tile pairs touch every tile
         s->c0++;
         s->sub_stream = s->qs;
         s->sub_target = s->arriveEpoch;
@@ -1296,11 +1319,86 @@ static int md_steps_overlapped(mdqt_ctx* s, int n) {
     return 0;
 }
 
+// One MD step as ONE launch (mdqt_qtfast.hip k_md_step): the Newton-3 tile pairs of forces() and
+// the interval's fused substeps, the QT workgroups waiting on the device for the arrival counts
+// of their ions' tiles instead of a kernel boundary.  Applies to one unsharded system on the tile
+// scheme with the lane QT kernel's FAST instance (qt_math 2, Philox, t > 0, the whole interval in
+// one launch, no range guard).  Same operations as forces() + substeps(ratio): bit-identical.
+// Measured at C2 (one MI355X, per-workgroup stamps `tools/md_stamps.py`): 56-63 us per MD step
+// against 43.5 for the two launches — one kernel has one VGPR count, so the tile pairs run with
+// the QT part's 162 (3 waves per SIMD instead of 7), the QT workgroups dispatched while the last
+// tile pairs still run take their CU slots, and the substep loops of early-complete tiles compete
+// with the remaining tile pairs; the force work ends at 32-37 us instead of 18.  Kept as an option
+// (default off) with its bit-identity tests.
+static bool fused_applies(mdqt_ctx* s) {
+    if (!(s->fused_opt && !s->overlap_opt && s->p.world_size == 1 && s->local.empty() && s->use_n3 &&
+          s->qt_math == 2 && s->p.qt_enabled && s->p.rng_mode == 1 && s->ratio <= MAXSUB && s->nloc > 0 &&
+          s->t > 0 && s->force_variant <= 1 &&
+          (s->substep_mode == 2 || (s->substep_mode == 0 && s->nloc < kLaneKernelMaxIons))))
+        return false;
+    return !force_args(s, nullptr).guard;
+}
+
+static int md_step_fused(mdqt_ctx* s) {
+    if (arrive_setup(s)) return -1;
+    HIPCHK(hipSetDevice(s->dev));
+    const unsigned long long T = (unsigned long long)((s->N + 63) / 64);
+    N3Args f{};
+    const ForceArgs c = force_args(s, nullptr);
+    f.R = s->dR; f.P = s->dFpart; f.pairs = s->dPairs;
+    f.N = s->N; f.S = s->S; f.ntiles = (int)T; f.npairs = s->npairs;
+    f.L = c.L; f.lDeb = c.lDeb; f.Rcut = c.Rcut; f.invlDeb = c.invlDeb; f.micT = c.micT;
+    f.micGuard = c.micGuard; f.guard = 0;
+    f.arrive = s->dArrive;
+    SubstepArgs a;                                     // as run_substeps(s, ratio, 1, 1, 1)
+    memset(&a, 0, sizeof a);
+    const int m = s->ratio;
+    a.R = s->dR; a.V = s->dV; a.F = s->dF; a.psi = s->dPsi; a.tPart = s->dTp;
+    a.Fpart = s->dFpart; a.nseg = s->nslots;
+    a.oor = s->dFlags;
+    a.arrive = s->dArrive;
+    a.arrive_target = s->arriveEpoch + T;
+    a.spin_err = s->dSpinErr;
+    a.arrive_sleep = 2;
+    a.n = s->nloc; a.S = s->S; a.gid0 = (uint64_t)s->lo;
+    a.q0 = s->qidx;
+    a.nsub = m; a.do_step = 1; a.do_qt = 1;
+    a.L = s->L;
+    a.qc = s->qc;
+    double t = s->t;
+    a.movmask = 0;
+    a.expdet_zero = 1;
+    for (int k = 0; k < m; ++k) {
+        a.t[k] = t;
+        a.expDet[k] = expDetuning_of(&s->p, t);
+        if (t > 0) a.movmask |= 1u << k;
+        if (a.expDet[k] != 0.) a.expdet_zero = 0;
+        t += s->dtQ;                                   // qstep: t += dtQuant (:716)
+    }
+    if (a.movmask != (m >= 32 ? 0xFFFFFFFFu : (1u << m) - 1u)) return fail("md_step_fused: t <= 0 in the interval");
+    const bool tm = s->timing && (s->tkinds & 2u) && (s->tcount[1]++ % s->tperiod == s->tperiod / 2);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (tm && take_events(s, 1, &e0, &e1)) return -1;
+    HIPCHK(launch_md_step(f, a, s->dFTab, s->force_variant, s->stream, e0, e1));
+    s->arriveEpoch += T;
+    s->f_pending = false;                              // F written by the QT workgroups
+    s->t = t;
+    s->qidx += (uint64_t)m;
+    return 0;
+}
+
 extern "C" int mdqt_md_steps(mdqt_ctx* s, int n) {
     if (!s) return fail("NULL context");
     if (n > 0 && overlap_applies(s)) return md_steps_overlapped(s, n);
     for (int k = 0; k < n; ++k) {
         if (k > 0 && k % 64 == 0 && check_range_flag(s)) return -1;
+        if (fused_applies(s)) {
+            if (local_reduce(s) || md_step_fused(s)) return -1;
+            s->last_fused = 1;
+            s->c0++;
+            continue;
+        }
+        s->last_fused = 0;
         if (mdqt_allgather_positions(s)) return -1;     // sharded: other slabs' R
         if (mdqt_forces(s)) return -1;
         s->c0++;
@@ -1711,6 +1809,22 @@ extern "C" int mdqt_run(mdqt_ctx* s) {                        // main(), SpeedUp
         if ((s->c0 + 1) % sf == 0 && tsc == 1)                                          // :1365
             if (output_async(s)) return -1;             // files formatted while the loop goes on
         if (tsc == ratio) {                                                             // :1369
+            // a whole interval without an output or the end inside it: one k_md_step launch
+            if (fused_applies(s)) {
+                const long c1 = s->c0 + 1;
+                int n = 0, ts = 0;
+                double tt = s->t;
+                do {
+                    n++; ts++; tt += s->dtQ;
+                } while (n < MAXSUB && tt <= tend && !((c1 + 1) % sf == 0 && ts == 1) && ts != ratio);
+                if (n == ratio) {
+                    if (local_reduce(s) || md_step_fused(s)) return -1;
+                    s->last_fused = 1;
+                    s->c0++;
+                    continue;                            // tsc stays = ratio
+                }
+            }
+            s->last_fused = 0;
             if (mdqt_allgather_positions(s)) return -1;                                 // §8e
             if (mdqt_forces(s)) return -1;
             s->c0++;
@@ -2029,6 +2143,17 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         s->scheme_opt = value;
         choose_segments(s);
         return ensure_aux(s);
+    }
+    if (!strcmp(name, "expt_force_sig")) {             // diagnostic: unfused force launches with the fused
+        if (value < 0 || value > 1) return fail("expt_force_sig must be 0 or 1");   // step's signalling
+        if (value && arrive_setup(s)) return -1;
+        s->force_arrive = value ? s->dArrive : nullptr;
+        return 0;
+    }
+    if (!strcmp(name, "fused_step")) {                 // one k_md_step launch per MD step (mdqt_md_steps)
+        if (value < 0 || value > 1) return fail("fused_step must be 0 or 1");
+        s->fused_opt = value;
+        return 0;
     }
     if (!strcmp(name, "overlap")) {                    // force || QT launches of an MD step (mdqt_md_steps)
         if (value < 0 || value > 1) return fail("overlap must be 0 or 1");

@@ -146,10 +146,11 @@ struct SubstepArgs {
     double expDet[MAXSUB];  // expDetuning(t) (:447)
     uint32_t movmask;       // bit s: t[s] > 0 (step_R's moving branch, :360); set by the host
     int expdet_zero;        // every expDet[s] == 0 (fracOfSig = 0, the default)
-    // overlapped MD step (lane kernel, world 1): the force kernel runs concurrently on another
-    // stream and counts its finished workgroups in *arrive; this launch does its prologue, then
-    // waits until *arrive >= arrive_target before it reads the force partials (write-through
-    // stores there, L1-bypassing loads here: mdqt_forces.hip k_pairs_n3)
+    // overlapped / fused MD step (lane kernel, world 1): the force work runs concurrently (another
+    // stream, or the first workgroups of k_md_step) and counts its finished tile pairs per tile in
+    // arrive[ntiles]; this launch does its prologue, then waits until arrive[tile of its ions] >=
+    // arrive_target before it reads the force partials (write-through stores there, L1-bypassing
+    // loads here: mdqt_pairs.hpp n3_tile)
     const unsigned long long* arrive;
     unsigned long long arrive_target;
     int* spin_err;          // set if the wait gave up (bounded spin)
@@ -259,8 +260,9 @@ struct N3Args {
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;          // as ForceArgs::guard (exact variant only; the fast one needs no guard)
     double rc2;         // variant 2: smallest double x with sqrt(x) >= Rcut (pair kept iff r2 < rc2)
-    unsigned long long* arrive;   // overlapped MD step: +1 per finished workgroup (after its
-                                  // write-through partial stores), nullptr = off
+    unsigned long long* arrive;   // [ntiles] arrival counts (overlapped / fused MD step): a finished
+                                  // tile pair (I, J) adds 1 to arrive[I] and arrive[J] after its
+                                  // write-through slot stores — T per tile per launch; nullptr = off
 };
 
 // Newton-3 over block pairs (mdqt_forces.hip k_pairs_n3b): blocks of 16 tiles, cyclic half
@@ -401,6 +403,11 @@ hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, i
 // qt_math 2: the reassociated kernels of mdqt_qtfast.hip (same modes as launch_substeps)
 hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s,
                              hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);   // tab[0] by state, tab[1] by lane
+// one MD step in one launch: Newton-3 tile pairs + the FAST lane QT kernel (mdqt_qtfast.hip
+// k_md_step); f.arrive / a.arrive = the per-tile arrival counters, a.arrive_target their value
+// after this launch's tile pairs
+hipError_t launch_md_step(const N3Args& f, const SubstepArgs& a, const FastTab* tab, int variant, hipStream_t s,
+                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // measureSpinUps (randomFrozenStartTag408Linear.cpp:600, :422Linear) / tagParticles
 // (MonteCarloFollowedByQTTagging408Linear.cpp:1022): tag[i] = 1 with probability of spin up
 hipError_t launch_tag_spin_up(const double* psi, int n, int S, uint64_t gid0, uint64_t q, const QTConst& qc,

@@ -1,0 +1,239 @@
+// Pair terms of forces() (SpeedUp:192-236) and the Newton-3 tile-pair body, shared by the force
+// kernels (mdqt_forces.hip) and the fused MD-step kernel (mdqt_qtfast.hip).
+#pragma once
+#include "mdqt_internal.hpp"
+
+#include <math.h>
+
+namespace mdqt {
+
+struct PairC {
+    double L, T, G, Rcut, lDeb, invlDeb, invL;
+    double rc2;         // VARIANT 2: pair kept iff r2 < rc2 (= sqrt(r2) < Rcut exactly)
+};
+
+__device__ __forceinline__ const double* pos_base(const double* Rall, int g, int S) {
+    const int w = g / S;
+    return Rall + (size_t)w * 3 * S + (g - w * S);
+}
+
+// Minimum image dx -= L*round(dx/L) (SpeedUp:218-220), exactly, without the division: for
+// |dx/L| < 1.5, round(dx/L) is +1 iff dx >= T and -1 iff dx <= -T, T the smallest double with
+// fl(T/L) >= 0.5 (host nextafter search), and dx - copysign(L, dx) is bit-identical to dx - L
+// resp. dx + L.  GUARD: positions may have left [-L/8, 9L/8] (set_state input), so take the
+// division form for separations beyond G = 1.25 L.
+template <bool GUARD>
+__device__ __forceinline__ void mic(double& dx, double& dy, double& dz, const PairC& c) {
+    if (GUARD && !(fabs(dx) < c.G && fabs(dy) < c.G && fabs(dz) < c.G)) {
+        dx -= c.L * round(dx / c.L);
+        dy -= c.L * round(dy / c.L);
+        dz -= c.L * round(dz / c.L);
+        return;
+    }
+    dx = (fabs(dx) >= c.T) ? dx - copysign(c.L, dx) : dx;
+    dy = (fabs(dy) >= c.T) ? dy - copysign(c.L, dy) : dy;
+    dz = (fabs(dz) >= c.T) ? dz - copysign(c.L, dz) : dz;
+}
+
+// Minimum image of the fast variant: dx -= L rint(dx / L) with the reciprocal (3 operations per
+// axis, any |dx|).  It differs from the reference's round(dx/L) only when dx/L lies within an ulp
+// of +-1/2, i.e. for pairs on the cutoff shell r ~ L/2 (with the other two separations below
+// ~1e-7 L for the pair to fall inside the cutoff either way): a measure-zero event.
+__device__ __forceinline__ void mic_r(double& dx, double& dy, double& dz, const PairC& c) {
+    dx = fma(-__builtin_rint(dx * c.invL), c.L, dx);
+    dy = fma(-__builtin_rint(dy * c.invL), c.L, dy);
+    dz = fma(-__builtin_rint(dz * c.invL), c.L, dz);
+}
+
+template <int VARIANT, bool GUARD>
+__device__ __forceinline__ void mic_v(double& dx, double& dy, double& dz, const PairC& c) {
+    if (VARIANT == 1) mic_r(dx, dy, dz, c);
+    else mic<GUARD>(dx, dy, dz, c);
+}
+
+// Force factor ft of one minimum-image separation (F_i += d * ft), 0 unless 0 < r < L/2
+// (:221-224).  Branch-free: out-of-range values are discarded by the final select.
+template <int VARIANT>
+__device__ __forceinline__ double pair_ft(double dx, double dy, double dz, const PairC& c) {
+    if (VARIANT == 0) {
+        const double r2 = dx * dx + dy * dy + dz * dz;
+        const double dr = sqrt(r2);
+        const double ft = (1. / dr + c.invlDeb) * exp(-dr / c.lDeb) / (dr * dr);   // :224
+        return (dr > 0 && dr < c.Rcut) ? ft : 0.;
+    } else {
+        const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+        const double ri = rsq3(r2);
+        const double dr = r2 * ri;
+        const double ft = ((ri + c.invlDeb) * exp_neg(-dr * c.invlDeb)) * (ri * ri);
+        if (VARIANT == 2)                        // the reference's pair set: r2 as :216, exact cutoff
+            return (dx * dx + dy * dy + dz * dz < c.rc2 && r2 > 0) ? ft : 0.;
+        return (dr < c.Rcut) ? ft : 0.;          // r2 = 0 (coincident ions) gives dr = NaN: 0
+    }
+}
+
+// Pair potential exp(-r/lDeb)/r (:265), 0 unless 0 < r < L/2
+template <int VARIANT>
+__device__ __forceinline__ double pair_u(double dx, double dy, double dz, const PairC& c) {
+    if (VARIANT == 0) {
+        const double dr = sqrt(dx * dx + dy * dy + dz * dz);
+        const double u = exp(-dr / c.lDeb) / (dr);
+        return (dr > 0 && dr < c.Rcut) ? u : 0.;
+    } else {
+        const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+        const double ri = rsq3(r2);
+        const double dr = r2 * ri;
+        const double u = exp_neg(-dr * c.invlDeb) * ri;
+        return (dr < c.Rcut) ? u : 0.;           // r2 = 0 gives dr = NaN: 0
+    }
+}
+
+template <int VARIANT>
+__device__ __forceinline__ void accum(double& f, double d, double ft) {
+    if (VARIANT == 0) f += d * ft;        // the reference's F[i] += dx*ftotal (:225-230)
+    else f = fma(d, ft, f);
+}
+
+// ------------------------------------------------------------------------------------------
+// Newton-3 tile pairs: one workgroup (4 waves) per tile pair (I, J), I <= J.  Lane l holds ion
+// I*64 + l; the J tile sits in LDS twice over (positions j and j + 64), so at rotation step s
+// lane l meets ion J*64 + ((l + s) & 63) at LDS index l + s (an immediate offset in the unrolled
+// loop).  Each distinct pair is evaluated once: +f goes to the i accumulator (registers), +f to
+// the j accumulator (ds_add_f64 at index l + s; the wave's LDS operations run in order, so the
+// accumulation order is fixed), and the j side is negated at the end (exact).  Wave q takes
+// rotation steps [16q, 16q + 16) (diagonal tile: lane distances 1 + 8q .. 8 + 8q, the 32nd only
+// for lanes < 32).  The four waves' partials are combined in a fixed order and written to slot
+// J (rows of I) and slot I (rows of J); the diagonal tile's two sides are summed into slot I.
+// F = canonical sum of the ntiles slots (seg_sum).  Deterministic, no global atomics.
+// ------------------------------------------------------------------------------------------
+// one rotation step of a Newton-3 tile pair: lane's ion i against the J-tile ion at LDS index
+// idx; +f to the i accumulator (registers) and to the j accumulator (ds_add_f64, no return)
+// SHIFT (fast variant, spatial order): the tile pair's minimum-image multiples n (one per axis,
+// wave-uniform) are known to be those of every pair, so mic_r's rint(dx / L) is not recomputed
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false>
+__device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
+                                        const double (*pj)[128], const double* mj, double* ax, double* ay,
+                                        double* az, double& fx, double& fy, double& fz, const PairC& c,
+                                        const double* nsh = nullptr) {
+    double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
+    if constexpr (SHIFT) {
+        dx = fma(-nsh[0], c.L, dx);                 // = mic_r's fma(-rint(dx / L), L, dx)
+        dy = fma(-nsh[1], c.L, dy);
+        dz = fma(-nsh[2], c.L, dz);
+    } else {
+        mic_v<VARIANT, GUARD>(dx, dy, dz, c);
+    }
+    double ft = pair_ft<VARIANT>(dx, dy, dz, c);
+    if (RAGGED) ft *= mi * mj[idx];
+    ft *= m;
+    const double px = dx * ft, py = dy * ft, pz = dz * ft;
+    fx += px; fy += py; fz += pz;
+#if defined(MDQT_EXPT_NOJACC)
+    (void)ax; (void)ay; (void)az;
+#else
+    __hip_atomic_fetch_add(&ax[idx], px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
+}
+
+#ifndef MDQT_N3_WAVES
+#define MDQT_N3_WAVES 4
+#endif
+constexpr int N3W = MDQT_N3_WAVES;                  // waves per tile pair (2, 4 or 8)
+static_assert(N3W == 2 || N3W == 4 || N3W == 8, "waves per tile pair");
+
+// the j accumulators of the N3W waves, both halves of each, combined in wave order
+__device__ __forceinline__ double n3_jsum(const double (*accj)[3][128], int k, int l) {
+    double w = accj[0][k][l] + accj[0][k][l + 64];
+#pragma unroll
+    for (int q = 1; q < N3W; ++q) w += accj[q][k][l] + accj[q][k][l + 64];
+    return w;
+}
+
+// slot stores: plain, or write-through (sc1) when the QT launch of an overlapped MD step reads
+// them after an arrival count instead of a kernel boundary (MI355X_MICROARCH.md, hand-off forms)
+#ifndef MDQT_EXPT_SIGMODE
+#define MDQT_EXPT_SIGMODE 0     // diagnostic builds: 1 = no arrival atomics, 2 = plain slot stores
+#endif
+template <bool SIG>
+__device__ __forceinline__ void slot_store(double* p, double v) {
+    if constexpr (SIG && MDQT_EXPT_SIGMODE != 2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+template <int VARIANT, bool GUARD, bool RAGGED, bool SIG>
+__device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
+                                        double (*pj)[128], double (*accj)[3][128], double* mj,
+                                        double (*ia)[3][64]) {
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int S = a.S, N = a.N;
+    const double* X = a.R;
+    const double* Y = a.R + S;
+    const double* Z = a.R + 2 * S;
+    if (q == 0) {                                   // stage the J tile (twice over)
+        const int j = J * 64 + l;
+        const bool vj = !RAGGED || j < N;
+        const double xj = vj ? X[j] : 0., yj = vj ? Y[j] : 0., zj = vj ? Z[j] : 0.;
+        pj[0][l] = xj; pj[0][l + 64] = xj;
+        pj[1][l] = yj; pj[1][l + 64] = yj;
+        pj[2][l] = zj; pj[2][l + 64] = zj;
+        if (RAGGED) { mj[l] = vj ? 1. : 0.; mj[l + 64] = mj[l]; }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
+    const int i = I * 64 + l;
+    const bool vi = !RAGGED || i < N;
+    const double xi = vi ? X[i] : 0., yi = vi ? Y[i] : 0., zi = vi ? Z[i] : 0.;
+    const double mi = vi ? 1. : 0.;
+    __syncthreads();
+    double fx = 0., fy = 0., fz = 0.;
+    double* ax = accj[q][0];
+    double* ay = accj[q][1];
+    double* az = accj[q][2];
+    auto step = [&](int idx, double m) {
+        n3_step<VARIANT, GUARD, RAGGED>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+    };
+    const bool diag = I == J;
+    if (!diag) {
+        const int b = l + (64 / N3W) * q;
+#pragma unroll
+        for (int t = 0; t < 64 / N3W; ++t) step(b + t, 1.);
+    } else {
+        const int b = l + 1 + (32 / N3W) * q;
+#pragma unroll
+        for (int t = 0; t < 32 / N3W - 1; ++t) step(b + t, 1.);
+        step(b + 32 / N3W - 1, (q == N3W - 1 && l >= 32) ? 0. : 1.);  // lane distance 32: once per pair
+    }
+    ia[q][0][l] = fx; ia[q][1][l] = fy; ia[q][2][l] = fz;
+    __syncthreads();
+    const size_t slab3 = (size_t)3 * S;
+    if (q == 0) {                                   // rows of I -> slot J (diagonal: I)
+        double* Pi = a.P + (size_t)J * slab3;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            double v = ia[0][k][l];
+#pragma unroll
+            for (int w = 1; w < N3W; ++w) v += ia[w][k][l];
+            if (diag) v = v - n3_jsum(accj, k, l);
+            if (i < S) slot_store<SIG>(&Pi[(size_t)k * S + i], v);
+        }
+    } else if (q == 1 && !diag) {                   // rows of J -> slot I
+        double* Pj = a.P + (size_t)I * slab3;
+        const int j = J * 64 + l;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double w = n3_jsum(accj, k, l);
+            if (j < S) slot_store<SIG>(&Pj[(size_t)k * S + j], -w);
+        }
+    }
+    if constexpr (SIG) {                            // every storing wave drained, then one arrival
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (MDQT_EXPT_SIGMODE != 1 && threadIdx.x == 0) {   // one arrival per tile whose rows were written
+            __hip_atomic_fetch_add(a.arrive + I, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (J != I) __hip_atomic_fetch_add(a.arrive + J, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+}  // namespace mdqt

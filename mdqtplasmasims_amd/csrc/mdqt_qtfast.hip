@@ -16,6 +16,7 @@
 // substep; tests/test_gpu_parity.py bounds it against the oracle).  The thread-per-ion and
 // lane-per-state kernels below perform the same operations in the same order: bit-identical.
 #include "mdqt_device.hpp"
+#include "mdqt_pairs.hpp"
 
 #include <math.h>
 
@@ -302,6 +303,12 @@ __device__ unsigned long long g_qt_stamps[6 * 4096];
 #define QT_STAMP(slot, v) ((void)0)
 #endif
 
+#if defined(MDQT_EXPT_MDSTAMPS)
+// diagnostic build only (k_md_step): per-workgroup s_memrealtime at entry and exit (+ after the
+// wait, QT workgroups)
+__device__ unsigned long long g_md_stamps[4 * 4096];
+#endif
+
 #ifndef MDQT_LANE_WPE
 #define MDQT_LANE_WPE 0
 #endif
@@ -314,8 +321,11 @@ __device__ unsigned long long g_qt_stamps[6 * 4096];
 // the simulation's first launch), F from the force slots (nseg > 1), no arrival wait: step_R's
 // non-moving branch (:360), the last substep's no-drift select and the other paths' loads and
 // branches are compiled out (straight-line prologue: one memory round trip)
-template <bool DPPX, bool FAST>
-__global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
+// FUSED (with FAST; the QT workgroups of k_md_step): the force partials of this launch's own
+// tile pairs are read after the arrival count of the ions' tile is complete, with L1-bypassing
+// loads (the tile pairs' slot stores are write-through: MI355X_MICROARCH.md, hand-off forms)
+template <bool DPPX, bool FAST, bool FUSED>
+__device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTab* __restrict__ tab, int blk) {
 #if defined(MDQT_EXPT_QTSTAMPS)
     unsigned long long st_[6];
 #endif
@@ -323,7 +333,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     QT_STAMP(4, __builtin_amdgcn_s_memrealtime());
     const int k = threadIdx.x & 15;
     const int grp = threadIdx.x >> 4;
-    const int iraw = blockIdx.x * (kLaneWG / 16) + grp;
+    const int iraw = blk * (kLaneWG / 16) + grp;
     const bool store = iraw < a.n;
     const int i = store ? iraw : a.n - 1;             // idle groups shadow the last ion
     const QTConst& qc = a.qc;
@@ -364,7 +374,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
                 if (FAST) {   // unconditional loads (clamped slot, in range), the select at the sum:
                               // no branch around the load, so nothing forces an early wait on it
                     const double* q = base_p + (size_t)min(sl, nseg - 1) * plane + (size_t)cc * S;
-                    const double x = *q;
+                    const double x = sc1 ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
                     t[u][cc] = sl < nseg ? x : 0.;
                 } else {
                     const double* q = base_p + (size_t)sl * plane + (size_t)cc * S;
@@ -390,7 +400,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     // FAST: the first round's loads stay in flight across the Philox draws below; summed after
     double t0[4][3];
     if (FAST) {
-        slot_round(k, t0, false);
+        if (!FUSED) slot_round(k, t0, false);
     } else if (nseg > 1) {
         if (!a.arrive) slot_partials(false);
     } else {
@@ -426,7 +436,8 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     if (!FAST && a.arrive) {                          // wait for the concurrent force launch
         if (threadIdx.x == 0) {
             int it = 0;
-            while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
+            const unsigned long long* cnt = a.arrive + (blk * (kLaneWG / 16)) / 64;   // the ions' tile
+            while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
                 for (int z = 0; z < a.arrive_sleep; ++z) __builtin_amdgcn_s_sleep(1);
                 if (++it > (1 << 21)) { *a.spin_err = 1; break; }   // bounded: never hang the GPU
             }
@@ -434,11 +445,26 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         __syncthreads();
         if (nseg > 1) slot_partials(true);
     }
+    if (FUSED) {                                      // this launch's tile pairs of the ions' tile
+        if (threadIdx.x == 0) {
+            const unsigned long long* cnt = a.arrive + (blk * (kLaneWG / 16)) / 64;
+            int it = 0;
+            while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++it > (1 << 22)) { *a.spin_err = 1; break; }   // bounded: never hang the GPU
+            }
+        }
+        __syncthreads();
+#if defined(MDQT_EXPT_MDSTAMPS)
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_md_stamps[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
+        slot_round(k, t0, true);
+    }
     if (FAST) {
         slot_add(t0);
         for (int s0 = k + 64; s0 < nseg; s0 += 64) {
             double t[4][3];
-            slot_round(s0, t, false);
+            slot_round(s0, t, FUSED);
             slot_add(t);
         }
     }
@@ -603,7 +629,7 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     __builtin_amdgcn_s_waitcnt(0);
     st_[3] = __builtin_amdgcn_s_memtime();
     st_[5] = __builtin_amdgcn_s_memrealtime();
-    const int wv = (int)(blockIdx.x * (kLaneWG / 64) + (threadIdx.x >> 6));
+    const int wv = (int)(blk * (kLaneWG / 64) + (threadIdx.x >> 6));
     if ((threadIdx.x & 63) < 6 && wv < 4096) {              // vector stores, one slot per lane
         const int q = threadIdx.x & 63;
         unsigned long long v = st_[0];
@@ -612,6 +638,70 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
         g_qt_stamps[6 * wv + q] = v;
     }
 #endif
+}
+
+template <bool DPPX, bool FAST>
+__global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
+    lane_substeps<DPPX, FAST, false>(a, tab, blockIdx.x);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_md_step: one MD step of one system (world 1, Newton-3 tiles, the lane QT kernel's FAST
+// instance) in ONE launch — forces() (SpeedUp:192-236) then the interval's fused step(); qstep();
+// substeps (:1376-1377).  Workgroups [0, npairs) are the tile pairs of k_pairs_n3 (same body,
+// write-through slot stores, one arrival per tile whose rows they wrote); workgroups npairs.. are
+// the lane kernel's 16-ion groups, which do their prologue (loads, Philox draws) while the force
+// workgroups run and wait for the arrival count of their ions' tile before reading the slots.
+// Workgroups are dispatched in index order, so every force workgroup is placed before any QT
+// workgroup: the waits cannot starve a force workgroup of a slot.  Same operations on the same
+// values as the two launches: bit-identical (tests/test_gpu_parity.py).  Saves the QT launch's
+// dispatch and hides its prologue behind the force kernel's tail.
+// ------------------------------------------------------------------------------------------
+static_assert(kLaneWG == 64 * N3W, "k_md_step: one workgroup size for both parts");
+#if defined(MDQT_EXPT_MDSTAMPS)
+extern "C" int mdqt_expt_md_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_md_stamps), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+}
+#define MD_STAMP(slot) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_md_stamps[4 * blockIdx.x + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define MD_STAMP(slot) ((void)0)
+#endif
+template <bool DPPX, int VARIANT>
+__global__ __launch_bounds__(256) void k_md_step(N3Args f, SubstepArgs a, const FastTab* __restrict__ tab) {
+    MD_STAMP(0);
+    if ((int)blockIdx.x < f.npairs) {
+        __shared__ double pj[3][128];
+        __shared__ double accj[N3W][3][128];
+        __shared__ double ia[N3W][3][64];
+        __shared__ double mj[128];
+        const int2 IJ = f.pairs[blockIdx.x];
+        const PairC c = {f.L, f.micT, f.micGuard, f.Rcut, f.lDeb, f.invlDeb, 1. / f.L, f.rc2};
+        const bool rag = (f.N & 63) && IJ.y == f.ntiles - 1;
+        if (rag) n3_tile<VARIANT, false, true, true>(f, c, IJ.x, IJ.y, pj, accj, mj, ia);
+        else n3_tile<VARIANT, false, false, true>(f, c, IJ.x, IJ.y, pj, accj, mj, ia);
+        MD_STAMP(1);
+        return;
+    }
+    lane_substeps<DPPX, true, true>(a, tab, (int)blockIdx.x - f.npairs);
+    MD_STAMP(1);
+}
+
+hipError_t launch_md_step(const N3Args& f, const SubstepArgs& a, const FastTab* tab, int variant, hipStream_t s,
+                          hipEvent_t ev0, hipEvent_t ev1) {
+    if (a.n <= 0 || f.npairs <= 0 || a.nsub <= 0 || a.nsub > MAXSUB || !a.arrive || !f.arrive || f.guard)
+        return hipErrorInvalidValue;
+    if (a.qc.model < 0 || a.qc.model >= NMODELS || variant < 0 || variant > 1) return hipErrorInvalidValue;
+    const dim3 gl(f.npairs + (a.n + kLaneWG / 16 - 1) / (kLaneWG / 16)), bl(kLaneWG);
+    const FastTab* lt = tab + 1;                      // by lane
+    if (a.qc.model == 0) {
+        if (variant == 1) launch_timed(k_md_step<true, 1>, gl, bl, s, ev0, ev1, f, a, lt);
+        else launch_timed(k_md_step<true, 0>, gl, bl, s, ev0, ev1, f, a, lt);
+    } else {
+        if (variant == 1) launch_timed(k_md_step<false, 1>, gl, bl, s, ev0, ev1, f, a, lt);
+        else launch_timed(k_md_step<false, 0>, gl, bl, s, ev0, ev1, f, a, lt);
+    }
+    return hipGetLastError();
 }
 
 #if defined(MDQT_EXPT_QTSTAMPS)

@@ -589,6 +589,45 @@ def test_norm_decay_and_partition_of_qt(eng):
 
 
 @pytest.mark.parametrize("N0", [500, 3500])
+def test_fused_md_step_bit_identical(eng, N0):
+    """one MD step as ONE launch (k_md_step: the tile pairs, then the QT workgroups waiting on the
+    per-tile arrival counts; option fused_step, default off) against forces() + substeps(ratio) as
+    two launches: bit for bit over MD steps with quantum jumps (the first step, t = 0, is never
+    fused — the non-moving drift branch)"""
+    out = []
+    for fu in (0, 1):
+        s = eng.Simulation(N0=N0, seed=73).init()
+        s.set_option("fused_step", fu)
+        assert s.const("fused_step") == fu
+        s.md_steps(30)
+        s.synchronize()
+        assert s.const("md_step_fused") == fu
+        out.append(s.get_state())
+        s.close()
+    a, b = out
+    for k in ("R", "V", "F", "psi", "tPart"):
+        assert np.array_equal(a[k], b[k]), k
+    assert (a["tPart"] < 30 * 0.002 - 1e-9).sum() > 0          # jumps happened
+
+
+def test_fused_md_step_run_files_identical(eng, tmp_path):
+    """mdqt_run (the reference's main loop) fuses whole intervals between outputs: the files of a
+    run are byte-identical with and without the fused launch"""
+    kw = dict(N0=300, tmax=0.3, sampleFreq=7, seed=5, job=2, rng_mode=1)
+    dirs = []
+    for fu in (0, 1):
+        s = eng.Simulation(saveDirectory=str(tmp_path / f"f{fu}") + "/", **kw)
+        s.set_option("fused_step", fu)
+        s.run()
+        dirs.append(s.save_directory)
+        s.close()
+    A, B = _read_dir(dirs[0]), _read_dir(dirs[1])
+    assert sorted(A) == sorted(B) and len(A) > 5
+    for f in A:
+        assert A[f] == B[f], f
+
+
+@pytest.mark.parametrize("N0", [500, 3500])
 def test_overlapped_md_step_bit_identical(eng, N0):
     """mdqt_md_steps with the force and QT launches overlapped (QT prologue on its own stream, a
     device-side arrival count instead of the kernel boundary, write-through partials) is the same

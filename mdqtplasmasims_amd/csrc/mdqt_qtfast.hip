@@ -62,6 +62,18 @@ __device__ __forceinline__ double lane_tree16(double v) {
     a = a + dpp<SHL(8)>(a);
     return dpp<BCAST(0)>(a);
 }
+#ifndef MDQT_NORM_Q
+#define MDQT_NORM_Q 1
+#endif
+// renormalisation sum of the ion's 16 lanes: quads Q_m = (v_4m + v_4m+1) + (v_4m+2 + v_4m+3),
+// then ((Q0 + Q1) + Q2) + Q3 (MDQT_NORM_Q; else the full DPP tree lane_tree16)
+__device__ __forceinline__ double tree16n(const double* v) {
+    if (!MDQT_NORM_Q) return tree16(v);
+    double q[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) q[m] = (v[4 * m] + v[4 * m + 1]) + (v[4 * m + 2] + v[4 * m + 3]);
+    return ((q[0] + q[1]) + q[2]) + q[3];
+}
 // (T2 + T3) + (T4 + T5) of the ion's lanes 2..5, in every lane of the row
 __device__ __forceinline__ double lane_sum_p(double T) {
     double a = T + dpp<SHL(1)>(T);
@@ -133,7 +145,7 @@ __device__ __forceinline__ double sq(cxd y) { return y.re * y.re + y.im * y.im; 
 // on lanes by kStateOfLane0 (see mdqt_internal.hpp), the other models on lane = state
 template <int MODEL>
 __device__ __forceinline__ double sum_p(const double* Tp) {     // Tp[q] of P state 2 + q
-    if constexpr (MODEL == 0) return (Tp[0] + Tp[2]) + (Tp[1] + Tp[3]);   // lanes 0 | 3 and 4 | 7
+    if constexpr (MODEL == 0) return ((Tp[0] + Tp[2]) + Tp[1]) + Tp[3];   // lanes 0, 3, 4, 7
     return (Tp[0] + Tp[1]) + (Tp[2] + Tp[3]);
 }
 template <int MODEL>
@@ -144,7 +156,7 @@ __device__ __forceinline__ double tree_lanes(const double* vs) {   // vs by stat
         const int st = MODEL == 0 ? state_of_lane0(l) : l;
         v[l] = st < NS ? vs[st] : 0.;
     }
-    return tree16(v);
+    return tree16n(v);
 }
 
 template <int MODEL>
@@ -288,10 +300,42 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
 // models): lane k = state k, slots gathered through LDS, lanes 12 / 13 hold y / z.  Lanes
 // without a state carry zero amplitudes and zero coefficients.  `tab` is indexed by lane.
 // ------------------------------------------------------------------------------------------
-// dp of model 0's layout: (T_lane0 + T_lane3) + (T_lane4 + T_lane7) = (T2 + T4) + (T3 + T5), in
-// every lane — four independent 64-bit broadcasts, then a two-level tree
-__device__ __forceinline__ double lane_sum_p8(double T) {
-    return (dpp<BCAST(0)>(T) + dpp<BCAST(3)>(T)) + (dpp<BCAST(4)>(T) + dpp<BCAST(7)>(T));
+// dp of model 0's layout: ((T_lane0 + T_lane3) + T_lane4) + T_lane7 = ((T2 + T4) + T3) + T5, in
+// every lane — one 64-bit broadcast, then three v_fmac_f64_dpp row_newbcast (the DP ALU takes a
+// row_newbcast operand: broadcast and add in one instruction; x * 1 + a is exactly x + a).  `one`
+// is 1.0 in a VGPR the compiler cannot see through, so the FMA is kept and the DPP move folds in.
+__device__ __forceinline__ double opaque_one() {
+    double o = 1.0;
+    asm volatile("" : "+v"(o));
+    return o;
+}
+// a + T[lane L of the row] * one as one v_fmac_f64_dpp (the compiler does not fold the 64-bit
+// DPP move into the FMA).  DPP read-after-VALU-write hazard: T is also the operand of the
+// compiler-emitted broadcast before the first of these, so the write is >= 2 states back.
+template <int L>
+__device__ __forceinline__ double fmac_bcast(double a, double T, double one) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(a) : "v"(T), "v"(one), "n"(L));
+    return a;
+#else
+    return fma(T, one, a);
+#endif
+}
+__device__ __forceinline__ double lane_norm16(double v, double one) {
+    if (!MDQT_NORM_Q) return lane_tree16(v);
+    double a = v + dpp<SHL(1)>(v);                  // lane 2m: v_2m + v_2m+1
+    a = a + dpp<SHL(2)>(a);                         // lane 4m: Q_m
+    double b = dpp<BCAST(0)>(a);
+    b = fmac_bcast<4>(b, a, one);
+    b = fmac_bcast<8>(b, a, one);
+    return fmac_bcast<12>(b, a, one);
+}
+__device__ __forceinline__ double lane_sum_p8(double T, double one) {
+    double a = dpp<BCAST(0)>(T);
+    a = fmac_bcast<3>(a, T, one);
+    a = fmac_bcast<4>(a, T, one);
+    return fmac_bcast<7>(a, T, one);
 }
 
 #if defined(MDQT_EXPT_QTSTAMPS)
@@ -350,6 +394,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     const double kw0 = tab->kw[0][k], kw1 = tab->kw[1][k], kw2 = tab->kw[2][k];
     const double cphi = tab->cphi, DT2 = tab->dt2;
     const double kmask = (c == 0) ? 1. : 0.;
+    const double one = opaque_one();
     // Prologue: every load is issued before any is consumed (one memory round trip), and the
     // lane-parallel Philox draws below run while they are in flight.
     double p = a.R[(size_t)c * S + i], v = a.V[(size_t)c * S + i], f;
@@ -511,12 +556,17 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         sincos_q<true>((u * cphi) * (tPart + qc.dtQ), sn, cs);   // substep's is formed with its phase)
         for (int s = 0; s < a.nsub; ++s) {
             tPart += qc.dtQ;
-            const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp) : lane_sum_p(nrm2(w) * hdp);
+            const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp, one) : lane_sum_p(nrm2(w) * hdp);
             const double u1 = su[grp][s][0], u2 = su[grp][s][1];
             cxd w0, w1, w2;
             exchange(w, w0, w1, w2);
             double kick;
+#if defined(MDQT_EXPT_NOJUMP)
+            const bool nojump = true;                 // timing-only diagnostic build: no jumps
+            (void)u1;
+#else
             const bool nojump = u1 > dp;
+#endif
             // substep s + 1's drift and phase, placed in the same basic block as the work they
             // overlap (straight-line: the last substep computes a harmless extra value, the
             // |phi| >= 2^20 library fallback is applied afterwards)
@@ -544,7 +594,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
             if (nojump) {
                 {                                 // kick terms on the P lanes (host table)
                     const double kt = kick_term(w, w0, w1, w2, kw0, kw1, kw2);
-                    kick = DPPX ? lane_sum_p8(kt) : lane_sum_p(kt);
+                    kick = DPPX ? lane_sum_p8(kt, one) : lane_sum_p(kt);
                 }
                 next_phase();
                 const cxd md = {mre, fma(mi1, u, mi0)};
@@ -555,7 +605,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                 for (int stg = 0; stg < 4; ++stg) {
                     double dpy = dp;
                     if (stg > 0) {
-                        dpy = DPPX ? lane_sum_p8(nrm2(y) * hdp) : lane_sum_p(nrm2(y) * hdp);
+                        dpy = DPPX ? lane_sum_p8(nrm2(y) * hdp, one) : lane_sum_p(nrm2(y) * hdp);
                         exchange(y, y0, y1, y2);
                     }
                     const double pref = rsq_nr(1. - dpy);
@@ -596,7 +646,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
             }
             if (!(fabs(phin) < 1048576.)) sincos(phin, &snn, &csn);
             if (qc.renorm) w = [&] {                      // :706-712
-                const double r = rsq_nr(lane_tree16(nrm2(w)));
+                const double r = rsq_nr(lane_norm16(nrm2(w), one));
                 return cxd{w.re * r, w.im * r};
             }();
             v = vn;

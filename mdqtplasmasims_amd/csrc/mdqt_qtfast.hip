@@ -340,11 +340,14 @@ __device__ __forceinline__ double lane_sum_p8(double T, double one) {
 
 #if defined(MDQT_EXPT_QTSTAMPS)
 // diagnostic build only: per-wave s_memtime at entry, loop start, loop end, exit + s_memrealtime
-// at entry and exit (tools/qt_stamps.py)
-__device__ unsigned long long g_qt_stamps[6 * 4096];
+// at entry and exit, s_memtime after the force-slot loads, and the number of substeps in which an
+// ion of the wave jumped (tools/qt_stamps.py)
+__device__ unsigned long long g_qt_stamps[8 * 4096];
 #define QT_STAMP(slot, v) (st_[slot] = (v))
+#define QT_JCOUNT(c) (st_[7] += (__builtin_amdgcn_ballot_w64(c) != 0))
 #else
 #define QT_STAMP(slot, v) ((void)0)
+#define QT_JCOUNT(c) ((void)0)
 #endif
 
 #if defined(MDQT_EXPT_MDSTAMPS)
@@ -371,7 +374,7 @@ __device__ unsigned long long g_md_stamps[4 * 4096];
 template <bool DPPX, bool FAST, bool FUSED>
 __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTab* __restrict__ tab, int blk) {
 #if defined(MDQT_EXPT_QTSTAMPS)
-    unsigned long long st_[6];
+    unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     QT_STAMP(0, __builtin_amdgcn_s_memtime());
     QT_STAMP(4, __builtin_amdgcn_s_memrealtime());
@@ -513,6 +516,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
             slot_add(t);
         }
     }
+    QT_STAMP(6, __builtin_amdgcn_s_memtime());
     if (FAST || nseg > 1) {
         const double fx = lane_tree16(qf[0]), fy = lane_tree16(qf[1]), fz = lane_tree16(qf[2]);
         f = c == 0 ? fx : c == 1 ? fy : fz;
@@ -567,6 +571,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
 #else
             const bool nojump = u1 > dp;
 #endif
+            QT_JCOUNT(!nojump);
             // substep s + 1's drift and phase, placed in the same basic block as the work they
             // overlap (straight-line: the last substep computes a harmless extra value, the
             // |phi| >= 2^20 library fallback is applied afterwards)
@@ -680,12 +685,12 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     st_[3] = __builtin_amdgcn_s_memtime();
     st_[5] = __builtin_amdgcn_s_memrealtime();
     const int wv = (int)(blk * (kLaneWG / 64) + (threadIdx.x >> 6));
-    if ((threadIdx.x & 63) < 6 && wv < 4096) {              // vector stores, one slot per lane
+    if ((threadIdx.x & 63) < 8 && wv < 4096) {              // vector stores, one slot per lane
         const int q = threadIdx.x & 63;
         unsigned long long v = st_[0];
 #pragma unroll
-        for (int m = 1; m < 6; ++m) v = (q == m) ? st_[m] : v;
-        g_qt_stamps[6 * wv + q] = v;
+        for (int m = 1; m < 8; ++m) v = (q == m) ? st_[m] : v;
+        g_qt_stamps[8 * wv + q] = v;
     }
 #endif
 }
@@ -756,7 +761,7 @@ hipError_t launch_md_step(const N3Args& f, const SubstepArgs& a, const FastTab* 
 
 #if defined(MDQT_EXPT_QTSTAMPS)
 extern "C" int mdqt_expt_qt_stamps(unsigned long long* out, int nwaves) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 6 * nwaves) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 8 * nwaves) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -19,10 +19,10 @@ s.substeps(25)
 s.synchronize()
 nw = (s.N + 3) // 4 // 4 * 4 + 4
 nw = min(nw, 4096)
-buf = (C.c_ulonglong * (6 * nw))()
+buf = (C.c_ulonglong * (8 * nw))()
 lib().mdqt_expt_qt_stamps.argtypes = [C.c_void_p, C.c_int]
 assert lib().mdqt_expt_qt_stamps(buf, nw) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 6).astype(np.int64)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8).astype(np.int64)
 a = a[a[:, 0] > 0]
 pro, loop, epi, tot = a[:, 1] - a[:, 0], a[:, 2] - a[:, 1], a[:, 3] - a[:, 2], a[:, 3] - a[:, 0]
 rt = (a[:, 5] - a[:, 4]) * 10e-3          # us
@@ -33,3 +33,12 @@ print(f"N={s.N} waves={len(a)} span {((a[:, 5].max() - t0) * 10e-3):.2f} us; sta
 for name, v in (("prologue", pro), ("loop", loop), ("epilogue", epi), ("total", tot)):
     p = np.percentile(v, [0, 50, 100])
     print(f"{name:9s} cycles min/med/max {p[0]:9.0f} {p[1]:9.0f} {p[2]:9.0f}   med {p[1] / np.median(clk) / 1e3:6.2f} us")
+
+ld = a[:, 6] - a[:, 0]
+p = np.percentile(ld, [0, 50, 100])
+print(f"prologue to the force-slot sum (loads + Philox) min/med/max {p[0]:.0f} {p[1]:.0f} {p[2]:.0f}")
+nj = a[:, 7]
+for j in range(int(nj.max()) + 1):
+    m = nj == j
+    if m.any():
+        print(f"waves with {j} jump substeps: {m.sum():4d}  loop cycles med {np.median(loop[m]):8.0f} max {loop[m].max():8.0f}")

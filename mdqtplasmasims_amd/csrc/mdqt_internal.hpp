@@ -210,6 +210,31 @@ __device__ __forceinline__ double exp_neg(double x) {
     return ldexp(p, (int)n);
 }
 
+// 2^t for t = -(r/lDeb) log2(e) <= 0 (the pair kernels' Yukawa factor e^(-r/lDeb) = 2^t, t formed
+// as r * (-log2(e)/lDeb)): n = rint(t), f = t - n exactly (|f| <= 1/2, no reduction constant to
+// round), then the degree-11 minimax-type polynomial of 2^f on [-1/2, 1/2] (Chebyshev fit in
+// 50-digit arithmetic, coefficients rounded to double; <= 1.14 ulp with double FMA Horner),
+// exponent shift.  Two operations fewer than exp_neg's Cody-Waite form; the only rounding before
+// the polynomial is t's own, the same size as x = -r/lDeb's in exp_neg.
+__device__ __forceinline__ double exp2_neg(double t) {
+    const double n = __builtin_rint(t);
+    const double f = t - n;
+    double p = 0x1.e9ec1fcb69a7fp-32;
+    p = fma(p, f, 0x1.e6228acd1c6e5p-28);
+    p = fma(p, f, 0x1.b524ebd13a55fp-24);
+    p = fma(p, f, 0x1.62bfc2c86d700p-20);
+    p = fma(p, f, 0x1.ffcbfc6da6ed1p-17);
+    p = fma(p, f, 0x1.430913112c61bp-13);
+    p = fma(p, f, 0x1.5d87fe78a3f9cp-10);
+    p = fma(p, f, 0x1.3b2ab6fb9f1a5p-7);
+    p = fma(p, f, 0x1.c6b08d704a0c6p-5);
+    p = fma(p, f, 0x1.ebfbdff82c5aep-3);
+    p = fma(p, f, 0x1.62e42fefa39efp-1);
+    p = fma(p, f, 1.0);
+    return ldexp(p, (int)n);
+}
+constexpr double kNegLog2e = -1.4426950408889634;   // -log2(e)
+
 // Canonical sum of nseg partials p[0], p[stride], ... : eight interleaved accumulators
 // (partial s goes to s % 8, ascending) combined as ((a0+a1)+(a2+a3))+((a4+a5)+(a6+a7)).  One
 // fixed order wherever it is evaluated (deterministic); independent loads, short chains.

@@ -234,6 +234,26 @@ __device__ __forceinline__ double exp2_neg(double t) {
     return ldexp(p, (int)n);
 }
 constexpr double kNegLog2e = -1.4426950408889634;   // -log2(e)
+// exp2_neg with a cutoff folded into the exponent shift: 0 (2^-1100 underflows) unless keep —
+// one 32-bit select instead of a 64-bit one on the result.  For finite t only (the caller's
+// r = 0 case must not occur: the Newton-3 tile kernels have no self pairs, distinct pad ions).
+__device__ __forceinline__ double exp2_neg_cut(double t, bool keep) {
+    const double n = __builtin_rint(t);
+    const double f = t - n;
+    double p = 0x1.e9ec1fcb69a7fp-32;
+    p = fma(p, f, 0x1.e6228acd1c6e5p-28);
+    p = fma(p, f, 0x1.b524ebd13a55fp-24);
+    p = fma(p, f, 0x1.62bfc2c86d700p-20);
+    p = fma(p, f, 0x1.ffcbfc6da6ed1p-17);
+    p = fma(p, f, 0x1.430913112c61bp-13);
+    p = fma(p, f, 0x1.5d87fe78a3f9cp-10);
+    p = fma(p, f, 0x1.3b2ab6fb9f1a5p-7);
+    p = fma(p, f, 0x1.c6b08d704a0c6p-5);
+    p = fma(p, f, 0x1.ebfbdff82c5aep-3);
+    p = fma(p, f, 0x1.62e42fefa39efp-1);
+    p = fma(p, f, 1.0);
+    return ldexp(p, keep ? (int)n : -1100);
+}
 
 // Canonical sum of nseg partials p[0], p[stride], ... : eight interleaved accumulators
 // (partial s goes to s % 8, ascending) combined as ((a0+a1)+(a2+a3))+((a4+a5)+(a6+a7)).  One

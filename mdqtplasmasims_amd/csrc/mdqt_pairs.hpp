@@ -99,8 +99,7 @@ __device__ __forceinline__ double pair_ft_scaled(double dx, double dy, double dz
     const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
     const double ri = rsq3(r2);
     const double dr = r2 * ri;
-    const double ft = ((ri + c.Lk) * exp2_neg(dr * c.Lk2)) * (ri * ri);
-    return (dr < 0.5) ? ft : 0.;               // r2 = 0 (coincident ions) gives dr = NaN: 0
+    return ((ri + c.Lk) * exp2_neg_cut(dr * c.Lk2, dr < 0.5)) * (ri * ri);   // 0 unless r' < 1/2
 }
 
 template <int VARIANT>
@@ -200,7 +199,9 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     if (q == 0) {                                   // stage the J tile (twice over)
         const int j = J * 64 + l;
         const bool vj = !RAGGED || j < N;
-        double xj = vj ? X[j] : 0., yj = vj ? Y[j] : 0., zj = vj ? Z[j] : 0.;
+        // pad ions (ragged last tile): distinct points (pad-pad pairs must have r > 0), weight 0
+        const double pad = (double)(l + 1) * 0x1p-10;
+        double xj = vj ? X[j] : pad, yj = vj ? Y[j] : pad, zj = vj ? Z[j] : pad;
         if (SC) { xj *= ps; yj *= ps; zj *= ps; }
         pj[0][l] = xj; pj[0][l + 64] = xj;
         pj[1][l] = yj; pj[1][l + 64] = yj;
@@ -211,7 +212,8 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
     const int i = I * 64 + l;
     const bool vi = !RAGGED || i < N;
-    double xi = vi ? X[i] : 0., yi = vi ? Y[i] : 0., zi = vi ? Z[i] : 0.;
+    const double padi = (double)(l + 1) * 0x1p-10;
+    double xi = vi ? X[i] : padi, yi = vi ? Y[i] : padi, zi = vi ? Z[i] : padi;
     if (SC) { xi *= ps; yi *= ps; zi *= ps; }
     const double mi = vi ? 1. : 0.;
     __syncthreads();

@@ -174,7 +174,7 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
     return Rall + (size_t)w * 3 * S + (g - w * S);
 }
 
-template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false>
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT>
 __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi, double zi, double mi,
                                          const double (*pj)[128], const double* mj, double* ax, double* ay,
                                          double* az, double& fx, double& fy, double& fz, const PairC& c,
@@ -183,7 +183,7 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
         for (int t0 = 0; t0 < 64; t0 += 16) {
 #pragma unroll
             for (int t = 0; t < 16; ++t)
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
                                                        c, nsh);
         }
     } else {
@@ -191,7 +191,7 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 const double m = (t0 + t == 32 && l >= 32) ? 0. : 1.;   // lane distance 32: once
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
                                                        c, nsh);
             }
         }
@@ -220,7 +220,8 @@ void k_pairs_n3b(N3BArgs a) {
     const bool srt = a.use_sort != 0;
     const int PS = srt ? a.Npad : S;
     auto tile_ptr = [&](int tile) { return srt ? a.Rs + tile * 64 : tile_base(a.Rall, tile, S); };
-    double xi = 0., yi = 0., zi = 0., mi = 0.;
+    const double pad = (double)(l + 1) * 0x1p-10;  // pad ions: distinct points (pair_ft_cut: r > 0)
+    double xi = pad, yi = pad, zi = pad, mi = 0.;
     if (vI && i < N) {
         const double* p = tile_ptr(I) + l;
         xi = p[0]; yi = p[PS]; zi = p[2 * PS]; mi = 1.;
@@ -275,7 +276,7 @@ void k_pairs_n3b(N3BArgs a) {
                 const int j = J * 64 + l;
                 const bool vj = j < N;
                 const double* p = tile_ptr(J) + l;
-                const double xj = vj ? p[0] : 0., yj = vj ? p[PS] : 0., zj = vj ? p[2 * PS] : 0.;
+                const double xj = vj ? p[0] : pad, yj = vj ? p[PS] : pad, zj = vj ? p[2 * PS] : pad;
                 pj[0][l] = xj; pj[0][l + 64] = xj;
                 pj[1][l] = yj; pj[1][l + 64] = yj;
                 pj[2][l] = zj; pj[2][l + 64] = zj;

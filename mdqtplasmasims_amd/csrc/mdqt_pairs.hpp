@@ -87,19 +87,14 @@ __device__ __forceinline__ double pair_u(double dx, double dy, double dz, const 
     }
 }
 
-// The fast variant in box units (MDQT_N3_SCALED, the Newton-3 tile kernel): positions staged as
-// x' = x / L, so the minimum image is dx' -= rint(dx') (two operations per axis instead of three)
-// and with r' = r / L, ri' = 1 / r':  F = L^-2 sum_j ft' dx',  ft' = (ri' + L/lDeb) 2^(r' t') ri'^2,
-// t' = -(L/lDeb) log2(e), the cutoff r' < 1/2.  The same law as pair_ft<1> up to rounding (the
-// 1e-13 force gate against the reference holds); the caller applies L^-2 per ion.
-struct PairS {
-    double Lk, Lk2;     // L / lDeb and L / lDeb * -log2(e)
-};
-__device__ __forceinline__ double pair_ft_scaled(double dx, double dy, double dz, const PairS& c) {
+// The fast variant for the Newton-3 tile kernels (no self pairs; pad ions at distinct points):
+// pair_ft<1> with the cutoff folded into the 2^t exponent shift (exp2_neg_cut: one 32-bit select
+// instead of a 64-bit select of the result; r = 0 must not occur).  Same values as pair_ft<1>.
+__device__ __forceinline__ double pair_ft_cut(double dx, double dy, double dz, const PairC& c) {
     const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
     const double ri = rsq3(r2);
     const double dr = r2 * ri;
-    return ((ri + c.Lk) * exp2_neg_cut(dr * c.Lk2, dr < 0.5)) * (ri * ri);   // 0 unless r' < 1/2
+    return ((ri + c.invlDeb) * exp2_neg_cut(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
 }
 
 template <int VARIANT>
@@ -124,24 +119,20 @@ __device__ __forceinline__ void accum(double& f, double d, double ft) {
 // idx; +f to the i accumulator (registers) and to the j accumulator (ds_add_f64, no return)
 // SHIFT (fast variant, spatial order): the tile pair's minimum-image multiples n (one per axis,
 // wave-uniform) are known to be those of every pair, so mic_r's rint(dx / L) is not recomputed
-template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool SC = false>
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
-                                        const double* nsh = nullptr, const PairS* cs = nullptr) {
+                                        const double* nsh = nullptr) {
     double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
-    if constexpr (SC) {                             // box units: dx' -= rint(dx')
-        dx -= __builtin_rint(dx);
-        dy -= __builtin_rint(dy);
-        dz -= __builtin_rint(dz);
-    } else if constexpr (SHIFT) {
+    if constexpr (SHIFT) {
         dx = fma(-nsh[0], c.L, dx);                 // = mic_r's fma(-rint(dx / L), L, dx)
         dy = fma(-nsh[1], c.L, dy);
         dz = fma(-nsh[2], c.L, dz);
     } else {
         mic_v<VARIANT, GUARD>(dx, dy, dz, c);
     }
-    double ft = SC ? pair_ft_scaled(dx, dy, dz, *cs) : pair_ft<VARIANT>(dx, dy, dz, c);
+    double ft = CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];
     ft *= m;
     const double px = dx * ft, py = dy * ft, pz = dz * ft;
@@ -180,17 +171,14 @@ __device__ __forceinline__ void slot_store(double* p, double v) {
     else *p = v;
 }
 
-#ifndef MDQT_N3_SCALED
-#define MDQT_N3_SCALED 1
+#ifndef MDQT_N3_CUT
+#define MDQT_N3_CUT 1
 #endif
 template <int VARIANT, bool GUARD, bool RAGGED, bool SIG>
 __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
                                         double (*ia)[3][64]) {
-    constexpr bool SC = VARIANT == 1 && !GUARD && MDQT_N3_SCALED;   // box units (pair_ft_scaled)
-    const double ps = SC ? c.invL : 1.;             // position scale at staging
-    const double fs = SC ? c.invL * c.invL : 1.;    // force scale L^-2 at the slot stores
-    const PairS cs = {c.L * c.invlDeb, (c.L * c.invlDeb) * kNegLog2e};
+    constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;   // pair_ft_cut
     const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int S = a.S, N = a.N;
     const double* X = a.R;
@@ -201,8 +189,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         const bool vj = !RAGGED || j < N;
         // pad ions (ragged last tile): distinct points (pad-pad pairs must have r > 0), weight 0
         const double pad = (double)(l + 1) * 0x1p-10;
-        double xj = vj ? X[j] : pad, yj = vj ? Y[j] : pad, zj = vj ? Z[j] : pad;
-        if (SC) { xj *= ps; yj *= ps; zj *= ps; }
+        const double xj = vj ? X[j] : pad, yj = vj ? Y[j] : pad, zj = vj ? Z[j] : pad;
         pj[0][l] = xj; pj[0][l + 64] = xj;
         pj[1][l] = yj; pj[1][l + 64] = yj;
         pj[2][l] = zj; pj[2][l + 64] = zj;
@@ -213,8 +200,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     const int i = I * 64 + l;
     const bool vi = !RAGGED || i < N;
     const double padi = (double)(l + 1) * 0x1p-10;
-    double xi = vi ? X[i] : padi, yi = vi ? Y[i] : padi, zi = vi ? Z[i] : padi;
-    if (SC) { xi *= ps; yi *= ps; zi *= ps; }
+    const double xi = vi ? X[i] : padi, yi = vi ? Y[i] : padi, zi = vi ? Z[i] : padi;
     const double mi = vi ? 1. : 0.;
     __syncthreads();
     double fx = 0., fy = 0., fz = 0.;
@@ -222,8 +208,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     double* ay = accj[q][1];
     double* az = accj[q][2];
     auto step = [&](int idx, double m) {
-        n3_step<VARIANT, GUARD, RAGGED, false, SC>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c,
-                                                   nullptr, &cs);
+        n3_step<VARIANT, GUARD, RAGGED, false, CUT>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
     };
     const bool diag = I == J;
     if (!diag) {
@@ -247,7 +232,6 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
 #pragma unroll
             for (int w = 1; w < N3W; ++w) v += ia[w][k][l];
             if (diag) v = v - n3_jsum(accj, k, l);
-            if (SC) v *= fs;
             if (i < S) slot_store<SIG>(&Pi[(size_t)k * S + i], v);
         }
     } else if (q == 1 && !diag) {                   // rows of J -> slot I
@@ -255,8 +239,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         const int j = J * 64 + l;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            double w = n3_jsum(accj, k, l);
-            if (SC) w *= fs;
+            const double w = n3_jsum(accj, k, l);
             if (j < S) slot_store<SIG>(&Pj[(size_t)k * S + j], -w);
         }
     }

@@ -304,8 +304,13 @@ void k_pairs_n3b(N3BArgs a) {
                     n3b_pair<VARIANT, GUARD, true>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
                 else if (VARIANT == 1 && cls > 0.) {
                     const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
-                    n3b_pair<VARIANT, GUARD, false, VARIANT == 1>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
-                                                                  tz, c, nsh);
+                    if (MDQT_SHIFT_I)                   // xi - n L once per tile pair (n3_step SHIFT)
+                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1>(diag, l, fma(-nsh[0], a.L, xi),
+                                                                      fma(-nsh[1], a.L, yi), fma(-nsh[2], a.L, zi), mi,
+                                                                      pj, mj, ax, ay, az, tx, ty, tz, c, nsh);
+                    else
+                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx,
+                                                                      ty, tz, c, nsh);
                 } else
                     n3b_pair<VARIANT, GUARD, false>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
                 bx += tx; by += ty; bz += tz;

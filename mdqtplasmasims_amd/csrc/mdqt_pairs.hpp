@@ -117,8 +117,13 @@ __device__ __forceinline__ void accum(double& f, double d, double ft) {
 // ------------------------------------------------------------------------------------------
 // one rotation step of a Newton-3 tile pair: lane's ion i against the J-tile ion at LDS index
 // idx; +f to the i accumulator (registers) and to the j accumulator (ds_add_f64, no return)
-// SHIFT (fast variant, spatial order): the tile pair's minimum-image multiples n (one per axis,
-// wave-uniform) are known to be those of every pair, so mic_r's rint(dx / L) is not recomputed
+// SHIFT (fast variant, spatial order): every pair of the tile pair has the same minimum-image
+// multiples n (one per axis), and the caller passes the i position already shifted, xi - n L
+// (MDQT_SHIFT_I; n = 0 on most axes, where it is the same value), so no per-pair image operation;
+// with MDQT_SHIFT_I 0 the multiples nsh are applied per pair, bit for bit mic_r's fma.
+#ifndef MDQT_SHIFT_I
+#define MDQT_SHIFT_I 1
+#endif
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
@@ -126,9 +131,11 @@ __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi,
                                         const double* nsh = nullptr) {
     double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
     if constexpr (SHIFT) {
-        dx = fma(-nsh[0], c.L, dx);                 // = mic_r's fma(-rint(dx / L), L, dx)
-        dy = fma(-nsh[1], c.L, dy);
-        dz = fma(-nsh[2], c.L, dz);
+        if (!MDQT_SHIFT_I) {
+            dx = fma(-nsh[0], c.L, dx);             // = mic_r's fma(-rint(dx / L), L, dx)
+            dy = fma(-nsh[1], c.L, dy);
+            dz = fma(-nsh[2], c.L, dz);
+        }
     } else {
         mic_v<VARIANT, GUARD>(dx, dy, dz, c);
     }

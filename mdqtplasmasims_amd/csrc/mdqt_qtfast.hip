@@ -558,7 +558,10 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         double sn, cs;
         double u = v * qc.pv2q + edt[0];              // vx on every state lane (carried: the next
         sincos_q<true>((u * cphi) * (tPart + qc.dtQ), sn, cs);   // substep's is formed with its phase)
-        for (int s = 0; s < a.nsub; ++s) {
+#ifndef MDQT_QT_UNROLL
+#define MDQT_QT_UNROLL 2
+#endif
+        auto substep = [&](int s) {
             tPart += qc.dtQ;
             const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp, one) : lane_sum_p(nrm2(w) * hdp);
             const double u1 = su[grp][s][0], u2 = su[grp][s][1];
@@ -659,6 +662,16 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
             u = un;
             sn = snn;
             cs = csn;
+        };
+        if (MDQT_QT_UNROLL == 2) {                    // two substeps per iteration (register copies)
+            int s = 0;
+            for (; s + 1 < a.nsub; s += 2) {
+                substep(s);
+                substep(s + 1);
+            }
+            if (s < a.nsub) substep(s);
+        } else {
+            for (int s = 0; s < a.nsub; ++s) substep(s);
         }
         if constexpr (FAST) {
             p = pre_p;

@@ -478,6 +478,9 @@ static void build_constants(mdqt_ctx* s) {
     // moves, col unused: self); the pumping models keep lane = state
     FastTab& fl = s->ftabL;
     fl = f;
+    q.im01 = 1;                                        // slots 0 and 1 purely imaginary (checked)
+    for (int k = 0; k < 16; ++k)
+        if (f.cre[0][k] != 0. || f.cre[1][k] != 0.) q.im01 = 0;
     if (p->qt_model == 0) {
         memset(&fl, 0, sizeof fl);
         fl.cphi = f.cphi; fl.dt2 = f.dt2;

@@ -41,6 +41,9 @@ struct QTConst {
     double thD[4][2];           // cumulative D-decay thresholds per P level (:612-697)
     double gs[18];
     int renorm;                 // reNormalizewvFns (:706-712)
+    int im01;                   // host: every static M entry of the lane table's slots 0 and 1 is
+                                // purely imaginary (Re == +-0: -i h H with real couplings), so the
+                                // FAST lane kernel drops their real-part FMAs (k_substeps_lanes_im)
     int model;                  // QT model (QTModel): level scheme, couplings and jump rule
     uint32_t seed, job;         // Philox key
 };

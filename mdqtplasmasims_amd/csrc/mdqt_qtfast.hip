@@ -46,6 +46,18 @@ __device__ __forceinline__ cxd row_r(cxd md, cxd y, cxd c0, cxd y0, cxd c1, cxd 
     return {re, im};
 }
 
+// row_r when the static slots 0 and 1 are purely imaginary (c.re = +-0): their real-part FMAs
+// add +-0 * y and are dropped — the same values up to the sign of an exact-zero result
+__device__ __forceinline__ cxd row_r_im01(cxd md, cxd y, double c0im, cxd y0, double c1im, cxd y1, cxd c2, cxd y2) {
+    double re = md.re * y.re, im = md.re * y.im;
+    re = fma(-md.im, y.im, re);  im = fma(md.im, y.re, im);
+    re = fma(-c0im, y0.im, re);  im = fma(c0im, y0.re, im);
+    re = fma(-c1im, y1.im, re);  im = fma(c1im, y1.re, im);
+    re = fma(c2.re, y2.re, re);  im = fma(c2.re, y2.im, im);
+    re = fma(-c2.im, y2.im, re); im = fma(c2.im, y2.re, im);
+    return {re, im};
+}
+
 __device__ __forceinline__ double kick_term(cxd w, cxd w0, cxd w1, cxd w2, double k0, double k1, double k2) {
     return fma(rho_im_r(w, w0), k0, fma(rho_im_r(w, w1), k1, rho_im_r(w, w2) * k2));
 }
@@ -371,7 +383,7 @@ __device__ unsigned long long g_md_stamps[4 * 4096];
 // FUSED (with FAST; the QT workgroups of k_md_step): the force partials of this launch's own
 // tile pairs are read after the arrival count of the ions' tile is complete, with L1-bypassing
 // loads (the tile pairs' slot stores are write-through: MI355X_MICROARCH.md, hand-off forms)
-template <bool DPPX, bool FAST, bool FUSED>
+template <bool DPPX, bool FAST, bool FUSED, bool IM01 = false>
 __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTab* __restrict__ tab, int blk) {
 #if defined(MDQT_EXPT_QTSTAMPS)
     unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -617,7 +629,8 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                         exchange(y, y0, y1, y2);
                     }
                     const double pref = rsq_nr(1. - dpy);
-                    const cxd ws = row_r(md, y, c0, y0, c1, y1, c2, y2);
+                    const cxd ws = IM01 ? row_r_im01(md, y, c0.im, y0, c1.im, y1, c2, y2)
+                                        : row_r(md, y, c0, y0, c1, y1, c2, y2);
                     const cxd d = {fma(pref, ws.re, -y.re), fma(pref, ws.im, -y.im)};
                     if (stg == 0) acc = d;
                     else if (stg < 3) acc = {fma(3., d.re, acc.re), fma(3., d.im, acc.im)};
@@ -712,6 +725,11 @@ template <bool DPPX, bool FAST>
 __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
     lane_substeps<DPPX, FAST, false>(a, tab, blockIdx.x);
 }
+// the FAST launch when QTConst::im01 (the production model-0 case)
+template <bool DPPX>
+__global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_im(SubstepArgs a, const FastTab* __restrict__ tab) {
+    lane_substeps<DPPX, true, false, true>(a, tab, blockIdx.x);
+}
 
 // ------------------------------------------------------------------------------------------
 // k_md_step: one MD step of one system (world 1, Newton-3 tiles, the lane QT kernel's FAST
@@ -788,8 +806,12 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
     if (mode == 2) {
         const uint64_t all = (1ull << a.nsub) - 1;
         const bool allmove = a.do_step && a.do_qt && a.nseg > 1 && !a.arrive && (a.movmask & all) == all;
+#ifndef MDQT_IM01
+#define MDQT_IM01 1
+#endif
         if (a.qc.model == 0) {
-            if (allmove) launch_timed(k_substeps_lanes_r<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+            if (allmove && a.qc.im01 && MDQT_IM01) launch_timed(k_substeps_lanes_im<true>, gl, bl, s, ev0, ev1, a, tab + 1);
+            else if (allmove) launch_timed(k_substeps_lanes_r<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
             else launch_timed(k_substeps_lanes_r<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
         } else {
             if (allmove) launch_timed(k_substeps_lanes_r<false, true>, gl, bl, s, ev0, ev1, a, tab + 1);

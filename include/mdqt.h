@@ -184,7 +184,10 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     rsq for 1/sqrt(1-dp), 2 = reassociated (default: fixed FMA chains per row
  *                     of M, folded constants; ~3x fewer instructions per substep).  1 and 2
  *                     differ from 0 by rounding only (1e-12 qstep gate); substep_kernel settings
- *                     are bit-identical to each other within one qt_math mode */
+ *                     are bit-identical to each other within one qt_math mode
+ *   "qt_im01":        1 (default where the table allows) = the lane kernel's production launch
+ *                     drops the real-part FMAs of the purely imaginary static coupling slots,
+ *                     0 = the general instance (bit-identical up to the sign of zero) */
 int         mdqt_set_option(mdqt_ctx* c, const char* name, int value);
 
 /* ---- streams, timing, multi-GPU plumbing ---- */

@@ -814,6 +814,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_scheme")) return s->use_n3b ? 3 : s->use_n3 ? 2 : 1;
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
     if (!strcmp(n, "fused_step")) return s->fused_opt;
+    if (!strcmp(n, "qt_im01")) return s->qc.im01;
     if (!strcmp(n, "md_step_fused")) return s->last_fused;     // 1: the last MD step was one k_md_step launch
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
@@ -2156,6 +2157,17 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (value < 0 || value > 1) return fail("expt_force_sig must be 0 or 1");   // step's signalling
         if (value && arrive_setup(s)) return -1;
         s->force_arrive = value ? s->dArrive : nullptr;
+        return 0;
+    }
+    if (!strcmp(name, "qt_im01")) {                    // 0: the general FAST lane instance (tests)
+        if (value < 0 || value > 1) return fail("qt_im01 must be 0 or 1");
+        if (value) {                                   // only where the table allows it
+            int ok = 1;
+            for (int k = 0; k < 16; ++k)
+                if (s->ftab.cre[0][k] != 0. || s->ftab.cre[1][k] != 0.) ok = 0;
+            if (!ok) return fail("qt_im01: the static coupling slots are not purely imaginary");
+        }
+        s->qc.im01 = value;
         return 0;
     }
     if (!strcmp(name, "fused_step")) {                 // one k_md_step launch per MD step (mdqt_md_steps)

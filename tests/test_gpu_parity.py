@@ -610,6 +610,27 @@ def test_fused_md_step_bit_identical(eng, N0):
     assert (a["tPart"] < 30 * 0.002 - 1e-9).sum() > 0          # jumps happened
 
 
+def test_lane_kernel_im01_instance_matches_general(eng):
+    """the FAST lane instance without the real-part FMAs of the purely imaginary static coupling
+    slots (QTConst::im01, the production model-0 launch) against the general FAST instance: the
+    dropped terms are +-0 * y, so the trajectories agree bit for bit (up to the sign of zero)
+    over MD steps with quantum jumps"""
+    out = []
+    for im in (1, 0):
+        s = eng.Simulation(N0=700, seed=91).init()
+        assert s.const("qt_im01") == 1                 # model 0: -i h H with real couplings
+        s.set_option("qt_im01", im)
+        assert s.const("qt_im01") == im
+        s.md_steps(30)
+        s.synchronize()
+        out.append(s.get_state())
+        s.close()
+    a, b = out
+    for k in ("R", "V", "F", "psi", "tPart"):
+        assert np.array_equal(a[k], b[k]), k
+    assert (a["tPart"] < 30 * 0.002 - 1e-9).sum() > 0          # jumps happened
+
+
 def test_fused_md_step_run_files_identical(eng, tmp_path):
     """mdqt_run (the reference's main loop) fuses whole intervals between outputs: the files of a
     run are byte-identical with and without the fused launch"""

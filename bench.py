@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--qt-math", type=int, default=2, choices=[0, 1, 2],
                     help="0: the reference's exact QT operations, 1: FMA-contracted, 2: reassociated "
                          "(option qt_math, the library default)")
+    ap.add_argument("--timed-launch", default="mid", choices=["mid", "first", "last"],
+                    help="which MD step of the timed window carries the one event-timed launch")
     ap.add_argument("--overlap", type=int, default=0, choices=[0, 1],
                     help="1: each MD step's QT launch overlaps its force launch (option overlap; "
                          "measured slower, DESIGN.md §8); 0: the sequential order (library default)")
@@ -277,7 +279,10 @@ def main():
     # event handling — kernel trace: gaps of 4.4 / 7.8 / 4.4 us around a timed force + QT pair,
     # none elsewhere); the other kernel is timed in a short window after it
     dom = 2 if qt else 1                           # kinds bit: 1 force, 2 fused substeps
-    sim.enable_timing(args.timing_period if args.timing_period > 0 else max(2, args.steps), dom)
+    if args.timing_period > 0 or args.timed_launch == "mid":
+        sim.enable_timing(args.timing_period if args.timing_period > 0 else max(2, args.steps), dom)
+    else:                                          # one launch: the window's first or last MD step
+        sim.enable_timing(args.steps + 1, dom, 0 if args.timed_launch == "first" else args.steps - 1)
     t0 = time.perf_counter()
     sim.md_steps(args.steps)
     barrier()                                      # torch.cuda.synchronize: every stream of the device

@@ -225,6 +225,9 @@ int         mdqt_enable_timing(mdqt_ctx* c, int period);
  * event-timed launch costs its MD step a few us, so a timed region may sample only its dominant
  * kernel) */
 int         mdqt_enable_timing_kinds(mdqt_ctx* c, int period, int kinds);
+/* the same with the bracketed launches at index `offset` mod period (0 <= offset < period;
+ * enable_timing_kinds takes period / 2) */
+int         mdqt_enable_timing_at(mdqt_ctx* c, int period, int kinds, int offset);
 int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
                                     int* nsub);
 

@@ -165,7 +165,8 @@ struct mdqt_ctx {
     // the launch stream while timing is on; summed by mdqt_kernel_time_totals
     bool timing = false;
     unsigned tkinds = 3;                        // bit 0: force launches, bit 1: fused-substep launches
-    unsigned tperiod = 1, tcount[2] = {0, 0};   // bracket launches k = tperiod/2 mod tperiod of each kind
+    unsigned tperiod = 1, tcount[2] = {0, 0};   // bracket launches k = toffset mod tperiod of each kind
+    unsigned toffset = 0;                        // tperiod / 2 unless mdqt_enable_timing_at
                                                 // (mid-period: not the first launch after a sync)
     std::vector<hipEvent_t> evpool[2];
     int evused[2] = {0, 0};
@@ -1106,7 +1107,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
     if (!s) return fail("NULL context");
     if (s->nloc == 0) return 0;
     HIPCHK(hipSetDevice(s->dev));
-    const bool tm = s->timing && (s->tkinds & 1u) && (s->tcount[0]++ % s->tperiod == s->tperiod / 2);
+    const bool tm = s->timing && (s->tkinds & 1u) && (s->tcount[0]++ % s->tperiod == s->toffset);
     // timing: the Newton-3 tile kernel (one launch) records its own timestamps; the other
     // schemes (several kernels, collectives) are bracketed by events on the stream
     const bool tm_marks = tm && !s->use_n3;
@@ -1209,7 +1210,7 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
             HIPCHK(launch_d48_resolve(r, s->stream));
             a.U = s->dU;
         }
-        const bool tm = s->timing && (s->tkinds & 2u) && (s->tcount[1]++ % s->tperiod == s->tperiod / 2);
+        const bool tm = s->timing && (s->tkinds & 2u) && (s->tcount[1]++ % s->tperiod == s->toffset);
         hipEvent_t e0 = nullptr, e1 = nullptr;       // timing: the kernel's own timestamps
         if (tm && (take_events(s, 1, &e0, &e1))) return -1;
         hipStream_t st = s->sub_stream ? s->sub_stream : s->stream;
@@ -1385,7 +1386,7 @@ static int md_step_fused(mdqt_ctx* s) {
         t += s->dtQ;                                   // qstep: t += dtQuant (:716)
     }
     if (a.movmask != (m >= 32 ? 0xFFFFFFFFu : (1u << m) - 1u)) return fail("md_step_fused: t <= 0 in the interval");
-    const bool tm = s->timing && (s->tkinds & 2u) && (s->tcount[1]++ % s->tperiod == s->tperiod / 2);
+    const bool tm = s->timing && (s->tkinds & 2u) && (s->tcount[1]++ % s->tperiod == s->toffset);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (tm && take_events(s, 1, &e0, &e1)) return -1;
     HIPCHK(launch_md_step(f, a, s->dFTab, s->force_variant, s->stream, e0, e1));
@@ -2230,15 +2231,20 @@ extern "C" int mdqt_positions_device(mdqt_ctx* s, void** dptr, int* S) {
     if (S) *S = s->S;
     return 0;
 }
-extern "C" int mdqt_enable_timing_kinds(mdqt_ctx* s, int on, int kinds) {
+extern "C" int mdqt_enable_timing_at(mdqt_ctx* s, int on, int kinds, int offset) {
     if (!s) return fail("NULL context");
-    if (kinds < 1 || kinds > 3) return fail("mdqt_enable_timing_kinds: kinds must be 1, 2 or 3");
+    if (kinds < 1 || kinds > 3) return fail("mdqt_enable_timing_at: kinds must be 1, 2 or 3");
+    if (on > 0 && (offset < 0 || offset >= on)) return fail("mdqt_enable_timing_at: offset must be in [0, period)");
     s->timing = on > 0;
     s->tperiod = on > 0 ? (unsigned)on : 1u;
+    s->toffset = on > 0 ? (unsigned)offset : 0u;
     s->tkinds = (unsigned)kinds;
     s->tcount[0] = s->tcount[1] = 0;
     s->evused[0] = s->evused[1] = 0;
     return 0;
+}
+extern "C" int mdqt_enable_timing_kinds(mdqt_ctx* s, int on, int kinds) {
+    return mdqt_enable_timing_at(s, on, kinds, on > 0 ? on / 2 : 0);
 }
 extern "C" int mdqt_enable_timing(mdqt_ctx* s, int on) { return mdqt_enable_timing_kinds(s, on, 3); }
 

@@ -315,10 +315,14 @@ class Simulation:
     def comm_init(self, uid: bytes):
         check(lib().mdqt_comm_init(self.h, uid, len(uid)), "comm_init")
 
-    def enable_timing(self, period: int = 1, kinds: int = 3):
+    def enable_timing(self, period: int = 1, kinds: int = 3, offset: int | None = None):
         """bracket every `period`-th hot-kernel launch with HIP events (0/False: off); kinds:
-        bit 0 force launches, bit 1 fused-substep launches"""
-        check(lib().mdqt_enable_timing_kinds(self.h, int(period), int(kinds)))
+        bit 0 force launches, bit 1 fused-substep launches; offset: which launch of each period
+        (default period // 2)"""
+        if offset is None:
+            check(lib().mdqt_enable_timing_kinds(self.h, int(period), int(kinds)))
+        else:
+            check(lib().mdqt_enable_timing_at(self.h, int(period), int(kinds), int(offset)))
 
     def kernel_time_totals(self):
         """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""

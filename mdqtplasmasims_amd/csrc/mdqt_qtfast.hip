@@ -383,7 +383,7 @@ __device__ unsigned long long g_md_stamps[4 * 4096];
 // FUSED (with FAST; the QT workgroups of k_md_step): the force partials of this launch's own
 // tile pairs are read after the arrival count of the ions' tile is complete, with L1-bypassing
 // loads (the tile pairs' slot stores are write-through: MI355X_MICROARCH.md, hand-off forms)
-template <bool DPPX, bool FAST, bool FUSED, bool IM01 = false>
+template <bool DPPX, bool FAST, bool FUSED, bool IM01 = false, bool EDZ = false>
 __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTab* __restrict__ tab, int blk) {
 #if defined(MDQT_EXPT_QTSTAMPS)
     unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -568,13 +568,16 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         if (FAST || a.do_step) drift(p, v, 0);
         double pre_p = p, pre_v = v;                  // FAST: the state after the last substep
         double sn, cs;
-        double u = v * qc.pv2q + edt[0];              // vx on every state lane (carried: the next
-        sincos_q<true>((u * cphi) * (tPart + qc.dtQ), sn, cs);   // substep's is formed with its phase)
+        // (EDZ: every expDet of the launch is 0 — fracOfSig = 0, the default — so u = vx pv2q: the
+        // + 0 and its LDS read dropped; the same values up to the sign of an exact zero)
+        double u = EDZ ? v * qc.pv2q : v * qc.pv2q + edt[0];   // vx on every state lane (carried: the
+        double tn = tPart + qc.dtQ;                   // next substep's is formed with its phase); tn:
+        sincos_q<true>((u * cphi) * tn, sn, cs);      // the next substep's tPart, formed once
 #ifndef MDQT_QT_UNROLL
 #define MDQT_QT_UNROLL 2
 #endif
         auto substep = [&](int s) {
-            tPart += qc.dtQ;
+            tPart = tn;                               // tPart += dtQ (formed in the last next_phase)
             const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp, one) : lane_sum_p(nrm2(w) * hdp);
             const double u1 = su[grp][s][0], u2 = su[grp][s][1];
             cxd w0, w1, w2;
@@ -607,8 +610,9 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                     pn = adv ? pd : pn;
                     vn = adv ? vd : vn;
                 }
-                un = vn * qc.pv2q + edt[s1];
-                phin = (un * cphi) * (tPart + qc.dtQ);
+                un = EDZ ? vn * qc.pv2q : vn * qc.pv2q + edt[s1];
+                tn = tPart + qc.dtQ;
+                phin = (un * cphi) * tn;
                 sincos_fast(phin, snn, csn);
             };
             if (nojump) {
@@ -660,8 +664,9 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                     randDir = dpp<BCAST(0)>(x1);
                     rand3 = dpp<BCAST(8)>(x0);
                 }
-                const int target = qc.model == 0 ? jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick)
-                                                 : jump_target_pump(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
+                const int target = (DPPX || qc.model == 0)   // DPPX: model 0
+                                       ? jump_target(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick)
+                                       : jump_target_pump(qc, n3, n4, n5, n6, u2, randDOrS, randDir, rand3, kick);
                 w = {st == target ? 1. : 0., 0.};
                 next_phase();
             }
@@ -725,10 +730,10 @@ template <bool DPPX, bool FAST>
 __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepArgs a, const FastTab* __restrict__ tab) {
     lane_substeps<DPPX, FAST, false>(a, tab, blockIdx.x);
 }
-// the FAST launch when QTConst::im01 (the production model-0 case)
-template <bool DPPX>
+// the FAST launch when QTConst::im01 (the production model-0 case); EDZ: expdet_zero
+template <bool DPPX, bool EDZ>
 __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_im(SubstepArgs a, const FastTab* __restrict__ tab) {
-    lane_substeps<DPPX, true, false, true>(a, tab, blockIdx.x);
+    lane_substeps<DPPX, true, false, true, EDZ>(a, tab, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -809,8 +814,14 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
 #ifndef MDQT_IM01
 #define MDQT_IM01 1
 #endif
+#ifndef MDQT_EDZ
+#define MDQT_EDZ 1
+#endif
         if (a.qc.model == 0) {
-            if (allmove && a.qc.im01 && MDQT_IM01) launch_timed(k_substeps_lanes_im<true>, gl, bl, s, ev0, ev1, a, tab + 1);
+            if (allmove && a.qc.im01 && MDQT_IM01) {
+                if (a.expdet_zero && MDQT_EDZ) launch_timed(k_substeps_lanes_im<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+                else launch_timed(k_substeps_lanes_im<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+            }
             else if (allmove) launch_timed(k_substeps_lanes_r<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
             else launch_timed(k_substeps_lanes_r<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
         } else {

@@ -89,23 +89,24 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r02b_c2_pmc.json")):
+def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r02c_c2_pmc.json")):
     """HBM bytes per launch of the kernel from the committed rocprofv3 --pmc summary of the same
     C2 workload (FETCH_SIZE and WRITE_SIZE in separate passes, kB -> B; no gfx950 x2 read
     correction: the kernel's loads are 8 B/lane, outside the guide's calibrated 16 B/lane case).
-    The production instance (the most dispatched one of the kernel family) is taken."""
+    The production instance (the most dispatched one of the kernel family) is taken; returns
+    (bytes, instance name) or (None, None)."""
     try:
         with open(path) as f:
             d = json.load(f)
     except OSError:
-        return None
-    best = None
+        return None, None
+    best, name = None, None
     for k, v in d.items():
         short = k.split("(")[0].replace("void ", "").replace("mdqt::", "")
         if short.startswith(kernel_prefix) and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             if best is None or v.get("dispatches", 0) > best.get("dispatches", 0):
-                best = v
-    return None if best is None else (best["FETCH_SIZE"] + best["WRITE_SIZE"]) * 1024.0
+                best, name = v, short
+    return (None, None) if best is None else ((best["FETCH_SIZE"] + best["WRITE_SIZE"]) * 1024.0, name)
 
 
 def cpu_threads():
@@ -317,12 +318,13 @@ def main():
             bytes_launch = B_Q_PER_ION * N
             ach = bytes_launch / s_avg / 1e9
             flops = F_Q_PER_QSTEP * N * nsub_per_launch
-            kname = ("k_substeps_lanes" if N < 98304 else "k_substeps") + ("_r" if args.qt_math == 2 else "")
+            kname = "k_substeps_lanes" if N < 98304 else "k_substeps_r"
+            traffic, kinst = pmc_traffic(kname)
             # The fused QT launch is bound by neither roof: one wave per SIMD runs a dependent chain of
             # ~330 VALU instructions per substep — "latency", with both fractions given.
             roof = {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kname),
-                    "kernel": f"{kname} (fused {nsub_per_launch:g} x step+qstep)",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                    "kernel": f"{kinst or kname} (fused {nsub_per_launch:g} x step+qstep)",
                     "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
                     "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS,
                     "hbm_frac": ach / HBM_PEAK_GBS}

@@ -670,8 +670,12 @@ __global__ __launch_bounds__(256) void k_tagged_kde(const double* __restrict__ V
     const int m = min(TKDE_CHUNK, N - i0);
     for (int k = 0; k < m; ++k) {
         if (!st[k]) continue;                                      // uniform over the workgroup
+        // a component whose term is exactly +0 on every bin of the wave (|vel - v| >= 0.0773:
+        // V2 d^2 >= 746.9, below exp's underflow) adds exact zeros there and is skipped
 #pragma unroll
-        for (int c = 0; c < 3; ++c) p[c] += exp(-V2 * (vel - sv[c][k]) * (vel - sv[c][k]));   // :1100-1102
+        for (int c = 0; c < 3; ++c)
+            if (__builtin_amdgcn_ballot_w64(!(fabs(vel - sv[c][k]) >= 0.0773)))
+                p[c] += exp(-V2 * (vel - sv[c][k]) * (vel - sv[c][k]));   // :1100-1102
     }
     if (j < TKDE_BINS)
 #pragma unroll

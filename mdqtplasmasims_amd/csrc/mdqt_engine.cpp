@@ -85,6 +85,9 @@ struct mdqt_ctx {
     hipStream_t own = nullptr, stream = nullptr;
     double *dR = nullptr, *dV = nullptr, *dF = nullptr, *dFpart = nullptr, *dPsi = nullptr,
            *dTp = nullptr, *dScr = nullptr, *dKde = nullptr, *dUrow = nullptr;
+    double* dUpart = nullptr;      // potential-row partials of its own (small systems, world 1)
+    size_t capUpart = 0;
+    double* dPack = nullptr;       // output()'s per-ion columns [4][S] (world 1)
     int kdeChunks = 0;
     LaneTab tab;                   // lane-per-state QT kernel tables (host copy)
     LaneTab* dTab = nullptr;       // device copy (uploaded once at create)
@@ -650,8 +653,10 @@ static int ensure_aux(mdqt_ctx* s) {
 }
 
 static void free_device(mdqt_ctx* s) {
-    double** ps[] = {&s->dR, &s->dV, &s->dF, &s->dFpart, &s->dPsi, &s->dTp, &s->dScr, &s->dKde, &s->dUrow, &s->dU};
+    double** ps[] = {&s->dR, &s->dV, &s->dF, &s->dFpart, &s->dPsi, &s->dTp, &s->dScr, &s->dKde, &s->dUrow, &s->dU,
+                     &s->dUpart, &s->dPack};
     for (double** q : ps) { if (*q) (void)hipFree(*q); *q = nullptr; }
+    s->capUpart = 0;
     if (s->dPairs) (void)hipFree(s->dPairs);
     s->dPairs = nullptr;
     s->capPairs = 0;
@@ -687,8 +692,9 @@ static int resize(mdqt_ctx* s, int N) {
         HIPCHK(hipMalloc(&s->dUrow, sz));
         if (s->p.rng_mode == 0) HIPCHK(hipMalloc(&s->dU, sz * 5));
         HIPCHK(hipMalloc(&s->dScr, (64 + 3 * NBINS) * sizeof(double)));
-        s->kdeChunks = 64;
-        HIPCHK(hipMalloc(&s->dKde, (size_t)s->kdeChunks * 3 * NBINS * sizeof(double)));
+        s->kdeChunks = 512;                            // chunks of >= 32 ions (the bins near v = 0 hold
+        HIPCHK(hipMalloc(&s->dKde, (size_t)s->kdeChunks * 3 * NBINS * sizeof(double)));   // the work)
+        HIPCHK(hipMalloc(&s->dPack, sz * 4));
         s->capS = S;
         HIPCHK(hipMemsetAsync(s->dR, 0, sz * 3 * W, s->stream));
         HIPCHK(hipMemsetAsync(s->dV, 0, sz * 3, s->stream));
@@ -1483,12 +1489,28 @@ extern "C" int mdqt_potentials_raw(int N, double L, double lDeb, const double* R
 // observables (Epotential :244-281, output :917-1032)
 // ---------------------------------------------------------------------------------------------
 
-// device: scratch[0] = sum over owned rows of the full-row pair potential
+// device: scratch[0] = sum over owned rows of the full-row pair potential.  World 1, partials up
+// to 64 MB: the potential rows get a buffer of their own, so pending force slots stay pending
+// (the next substep launch sums them in its prologue: no reduce launch, and that launch stays the
+// production instance); otherwise they reuse the force partials after settling them.
 static int potential_rows(mdqt_ctx* s, double* urow_dev) {
     if (s->nloc == 0) return 0;
-    if (settle_forces(s)) return -1;     // the potential rows reuse the partials buffer
-    HIPCHK(launch_potential_rows(force_args(s, s->dFpart), s->stream));
-    HIPCHK(launch_reduce_segments(s->dFpart, urow_dev, s->nseg, s->nloc, s->S, 1, s->stream));
+    double* buf = s->dFpart;
+    const size_t need = (size_t)s->nseg * 3 * s->S;
+    if (s->p.world_size == 1 && s->local.empty() && need * sizeof(double) <= ((size_t)64 << 20)) {
+        if (need > s->capUpart) {
+            if (s->dUpart) HIPCHK(hipFree(s->dUpart));
+            s->dUpart = nullptr;
+            s->capUpart = 0;
+            HIPCHK(hipMalloc(&s->dUpart, need * sizeof(double)));
+            s->capUpart = need;
+        }
+        buf = s->dUpart;
+    } else if (settle_forces(s)) {
+        return -1;
+    }
+    HIPCHK(launch_potential_rows(force_args(s, buf), s->stream));
+    HIPCHK(launch_reduce_segments(buf, urow_dev, s->nseg, s->nloc, s->S, 1, s->stream));
     return 0;
 }
 
@@ -1500,8 +1522,8 @@ extern "C" int mdqt_partial_observables(mdqt_ctx* s, double vxAvg, double out5[5
     HIPCHK(launch_sum_vx(s->dV, s->nloc, scr, s->stream));
     HIPCHK(hipMemcpyAsync(scr + 8, &vxAvg, sizeof(double), hipMemcpyHostToDevice, s->stream));
     HIPCHK(launch_energy_sums(s->dV, s->nloc, s->S, scr + 8, s->dUrow, scr + 16, s->stream));
-    int nch = s->nloc / 256;
-    if (nch < 1) nch = 1;
+    int nch = s->nloc / 32;                                 // cold ions sit in the first bins:
+    if (nch < 1) nch = 1;                                    // short chunks spread that work
     if (nch > s->kdeChunks) nch = s->kdeChunks;
     double* Pout = scr + 64;
     if (s->nloc > 0) HIPCHK(launch_kde(s->dV, s->nloc, s->S, scr + 8, s->dKde, nch, Pout, s->stream));
@@ -1528,8 +1550,53 @@ extern "C" int mdqt_epotential(mdqt_ctx* s, double* Epot) {   // Epotential(), :
     return 0;
 }
 
+// output()'s observables at world 1 in one device pass and one synchronisation: <vx> stays on
+// the device (k_sum_vx writes sum / N for the energy sums and the KDE), the per-ion columns
+// (vx, S / P / D populations) come from k_output_pack instead of a full wavefunction download.
+// Same operations as the general path below (the populations: the host loop's order).
+static int observables_w1(mdqt_ctx* s, double out7[7], double* Pvel, double* pops, double* vx) {
+    const int N = s->N;
+    double* scr = s->dScr;           // [0] sum vx, [8] vxAvg, [16..19] sums, [64..] KDE bins
+    HIPCHK(hipSetDevice(s->dev));
+    if (potential_rows(s, s->dUrow)) return -1;
+    HIPCHK(launch_sum_vx(s->dV, N, scr, s->stream, scr + 8, N));
+    HIPCHK(launch_energy_sums(s->dV, N, s->S, scr + 8, s->dUrow, scr + 16, s->stream));
+    int nch = N / 32;
+    if (nch < 1) nch = 1;
+    if (nch > s->kdeChunks) nch = s->kdeChunks;
+    HIPCHK(launch_kde(s->dV, N, s->S, scr + 8, s->dKde, nch, scr + 64, s->stream));
+    const bool pack = pops || vx;
+    if (pack) HIPCHK(launch_output_pack(s->dV, s->dPsi, N, s->S, s->p.qt_model, s->dPack, s->stream));
+    std::vector<double> h(64 + 3 * NBINS), col(pack ? (size_t)4 * N : 0);
+    HIPCHK(hipMemcpyAsync(h.data(), scr, h.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    if (pack) HIPCHK(hipMemcpyAsync(col.data(), s->dPack, col.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    const double velXAvg = h[8];
+    const double EkinX = h[16] / (double)N, EkinY = h[17] / (double)N, EkinZ = h[18] / (double)N;   // :945-947
+    s->Epot = (h[19] / 2.) / (double)N;                                                          // :948
+    out7[0] = s->t; out7[1] = EkinX; out7[2] = EkinY; out7[3] = EkinZ; out7[4] = s->Epot;
+    out7[5] = EkinX + EkinY + EkinZ + s->Epot - s->Epot0; out7[6] = velXAvg;                   // :954
+    if (Pvel) {
+        const double norm = (6.0 * sqrt(2 * M_PI * 0.002 * 0.002));                            // :975-978
+        for (int j = 0; j < 3 * NBINS; ++j) Pvel[j] = h[64 + j] / norm;
+    }
+    if (vx) memcpy(vx, col.data(), (size_t)N * sizeof(double));
+    if (pops)
+        for (int i = 0; i < N; i++) {
+            pops[3 * i + 0] = col[(size_t)N + i];
+            pops[3 * i + 1] = col[2 * (size_t)N + i];
+            pops[3 * i + 2] = col[3 * (size_t)N + i];
+        }
+    return 0;
+}
+
+static bool observables_w1_applies(const mdqt_ctx* s) {
+    return s->p.world_size == 1 && s->local.empty() && s->N > 0 && s->nloc == s->N;
+}
+
 extern "C" int mdqt_observables(mdqt_ctx* s, double out7[7], double* Pvel, double* pops) {
     if (!s) return fail("NULL context");
+    if (observables_w1_applies(s)) return observables_w1(s, out7, Pvel, pops, nullptr);
     const int N = s->N;
     double o[5];
     if (mdqt_allgather_positions(s)) return -1;          // collective when sharded
@@ -1639,9 +1706,13 @@ static int output_async(mdqt_ctx* s) {
     auto P = std::make_shared<std::vector<double>>((size_t)3 * NBINS);
     auto pops = std::make_shared<std::vector<double>>((size_t)3 * (N > 0 ? N : 1));
     auto V = std::make_shared<std::vector<double>>((size_t)3 * (N > 0 ? N : 1), 0.);
-    if (mdqt_observables(s, o, P->data(), pops->data())) return -1;
-    if (mdqt_get_state(s, nullptr, V->data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
-    if (mdqt_allreduce_sum(s, V->data(), (size_t)N)) return -1;      // vx column, zero-padded gather
+    if (observables_w1_applies(s)) {                                 // one pass, one synchronisation
+        if (observables_w1(s, o, P->data(), pops->data(), V->data())) return -1;
+    } else {
+        if (mdqt_observables(s, o, P->data(), pops->data())) return -1;
+        if (mdqt_get_state(s, nullptr, V->data(), nullptr, N, nullptr, nullptr, nullptr)) return -1;
+        if (mdqt_allreduce_sum(s, V->data(), (size_t)N)) return -1;  // vx column, zero-padded gather
+    }
     if (s->p.rank != 0) { s->counter++; return 0; }                 // files are rank 0's
     FILE* fa = open_in(s, "energies.dat", "a");                      // appended in order: here
     if (!fa) return -1;

@@ -461,7 +461,10 @@ hipError_t launch_md_step(const N3Args& f, const SubstepArgs& a, const FastTab* 
 hipError_t launch_tag_spin_up(const double* psi, int n, int S, uint64_t gid0, uint64_t q, const QTConst& qc,
                               int* tags, hipStream_t s);
 // deterministic sums: out[0] = sum vx; needs scratch >= 1024 doubles
-hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s);
+// avg (optional, world 1): also avg[0] = sum / N on the device
+hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s, double* avg = nullptr, int N = 0);
+hipError_t launch_output_pack(const double* V, const double* psi, int n, int S, int model, double* out,
+                              hipStream_t s);
 // out[0..2] = sum 0.5 (vx-avg)^2, 0.5 vy^2, 0.5 vz^2 ; out[3] = sum of rows[0..nrows) of
 // the potential partials reduced over segments (caller passes the reduced row buffer)
 hipError_t launch_energy_sums(const double* V, int n, int S, const double* vxAvg,

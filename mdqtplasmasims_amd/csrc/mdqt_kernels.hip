@@ -610,12 +610,45 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
     return r;
 }
 
-__global__ __launch_bounds__(RT) void k_sum_vx(const double* __restrict__ V, int n, double* out) {
+__global__ __launch_bounds__(RT) void k_sum_vx(const double* __restrict__ V, int n, double* out, double* avg,
+                                                int N) {
     __shared__ double sh[RT];
     double acc = 0.;
     for (int i = threadIdx.x; i < n; i += RT) acc += V[i];
     const double r = block_sum(acc, sh);
-    if (threadIdx.x == 0) out[0] = r;
+    if (threadIdx.x == 0) {
+        out[0] = r;
+        if (avg) avg[0] = N > 0 ? r / (double)N : 0.;   // velXAvg (:938) on the device (world 1)
+    }
+}
+
+// output()'s per-ion columns in one array [4][n]: vx and the S / P / D populations of
+// statePopulationsVsVTime (:1010-1024), the host loop's operations and order (pumping model 3:
+// P = 2, 3; D = 4)
+__global__ __launch_bounds__(256) void k_output_pack(const double* __restrict__ V, const double* __restrict__ psi,
+                                                     int n, int S, int model, double* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    auto nrm = [&](int k) {
+        const double re = psi[(size_t)(2 * k) * S + i], im = psi[(size_t)(2 * k + 1) * S + i];
+        return re * re + im * im;
+    };
+    out[i] = V[i];
+    out[(size_t)n + i] = nrm(0) + nrm(1);
+    if (model == 3) {
+        out[2 * (size_t)n + i] = nrm(2) + nrm(3);
+        out[3 * (size_t)n + i] = nrm(4);
+    } else {
+        out[2 * (size_t)n + i] = nrm(2) + nrm(3) + nrm(4) + nrm(5);
+        out[3 * (size_t)n + i] = nrm(6) + nrm(7) + nrm(8) + nrm(9) + nrm(10) + nrm(11);
+    }
+}
+
+hipError_t launch_output_pack(const double* V, const double* psi, int n, int S, int model, double* out,
+                              hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_output_pack, dim3((n + 255) / 256), dim3(256), 0, s, V, psi, n, S, model, out);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(RT) void k_energy_sums(const double* __restrict__ V, int n, int S,
@@ -638,8 +671,8 @@ __global__ __launch_bounds__(RT) void k_energy_sums(const double* __restrict__ V
     if (threadIdx.x == 0) { out[0] = rx; out[1] = ry; out[2] = rz; out[3] = ru; }
 }
 
-hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_sum_vx, dim3(1), dim3(RT), 0, s, V, n, out);
+hipError_t launch_sum_vx(const double* V, int n, double* out, hipStream_t s, double* avg, int N) {
+    hipLaunchKernelGGL(k_sum_vx, dim3(1), dim3(RT), 0, s, V, n, out, avg, N);
     return hipGetLastError();
 }
 

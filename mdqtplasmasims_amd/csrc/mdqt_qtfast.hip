@@ -383,6 +383,9 @@ __device__ unsigned long long g_md_stamps[4 * 4096];
 // FUSED (with FAST; the QT workgroups of k_md_step): the force partials of this launch's own
 // tile pairs are read after the arrival count of the ions' tile is complete, with L1-bypassing
 // loads (the tile pairs' slot stores are write-through: MI355X_MICROARCH.md, hand-off forms)
+// IM01 (with FAST): the static coupling slots 0 and 1 are purely imaginary (QTConst::im01), their
+// real-part FMAs are dropped.  EDZ: every expDetuning of the launch is 0 (u = vx pv2q).  The
+// production model-0 launch is k_substeps_lanes_im<true, true> (FAST + IM01 + EDZ).
 template <bool DPPX, bool FAST, bool FUSED, bool IM01 = false, bool EDZ = false>
 __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTab* __restrict__ tab, int blk) {
 #if defined(MDQT_EXPT_QTSTAMPS)

@@ -86,6 +86,7 @@ struct mdqt_ctx {
     double *dR = nullptr, *dV = nullptr, *dF = nullptr, *dFpart = nullptr, *dPsi = nullptr,
            *dTp = nullptr, *dScr = nullptr, *dKde = nullptr, *dUrow = nullptr;
     double* dUpart = nullptr;      // potential-row partials of its own (small systems, world 1)
+    int n3_potential = 1;          // option "potential_n3": 1 = Newton-3 tiles where the forces use them
     size_t capUpart = 0;
     double* dPack = nullptr;       // output()'s per-ion columns [4][S] (world 1)
     int kdeChunks = 0;
@@ -822,6 +823,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
     if (!strcmp(n, "fused_step")) return s->fused_opt;
     if (!strcmp(n, "qt_im01")) return s->qc.im01;
+    if (!strcmp(n, "potential_n3")) return s->n3_potential;
     if (!strcmp(n, "md_step_fused")) return s->last_fused;     // 1: the last MD step was one k_md_step launch
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
@@ -1495,6 +1497,31 @@ extern "C" int mdqt_potentials_raw(int N, double L, double lDeb, const double* R
 // production instance); otherwise they reuse the force partials after settling them.
 static int potential_rows(mdqt_ctx* s, double* urow_dev) {
     if (s->nloc == 0) return 0;
+    // world 1 with the Newton-3 tile scheme: each distinct pair's potential once (the tile kernel's
+    // POT mode), the ntiles slots of component 0 summed per ion (half the pair evaluations of the
+    // rows; the same per-ion row sums up to summation order)
+    if (s->use_n3 && !s->use_n3b && s->p.world_size == 1 && s->local.empty() && s->force_variant <= 1 &&
+        s->n3_potential) {
+        const size_t need = (size_t)s->nslots * 3 * s->S;
+        if (need > s->capUpart) {
+            if (s->dUpart) HIPCHK(hipFree(s->dUpart));
+            s->dUpart = nullptr;
+            s->capUpart = 0;
+            HIPCHK(hipMalloc(&s->dUpart, need * sizeof(double)));
+            s->capUpart = need;
+        }
+        N3Args a{};
+        a.R = s->dR; a.P = s->dUpart; a.pairs = s->dPairs;
+        a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs;
+        ForceArgs c = force_args(s, nullptr);
+        a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
+        a.micGuard = c.micGuard;
+        a.guard = c.guard;
+        a.arrive = nullptr;
+        HIPCHK(launch_potential_n3(a, s->force_variant, s->stream));
+        HIPCHK(launch_reduce_segments(s->dUpart, urow_dev, s->nslots, s->nloc, s->S, 1, s->stream));
+        return 0;
+    }
     double* buf = s->dFpart;
     const size_t need = (size_t)s->nseg * 3 * s->S;
     if (s->p.world_size == 1 && s->local.empty() && need * sizeof(double) <= ((size_t)64 << 20)) {
@@ -2229,6 +2256,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (value < 0 || value > 1) return fail("expt_force_sig must be 0 or 1");   // step's signalling
         if (value && arrive_setup(s)) return -1;
         s->force_arrive = value ? s->dArrive : nullptr;
+        return 0;
+    }
+    if (!strcmp(name, "potential_n3")) {               // Epotential on the Newton-3 tiles (1) or the rows (0)
+        if (value < 0 || value > 1) return fail("potential_n3 must be 0 or 1");
+        s->n3_potential = value;
         return 0;
     }
     if (!strcmp(name, "qt_im01")) {                    // 0: the general FAST lane instance (tests)

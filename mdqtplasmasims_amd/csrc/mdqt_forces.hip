@@ -131,6 +131,21 @@ __global__ __launch_bounds__(64 * N3W) void k_pairs_n3(N3Args a) {
 #endif
 }
 
+// Epotential() (:244-281) on the Newton-3 tiles: each distinct pair's u once, to both ions' rows
+// (slot component 0; the caller sums the ntiles slots per ion)
+template <int VARIANT, bool GUARD>
+__global__ __launch_bounds__(64 * N3W) void k_pairs_n3_pot(N3Args a) {
+    __shared__ double pj[3][128];
+    __shared__ double accj[N3W][3][128];
+    __shared__ double ia[N3W][3][64];
+    __shared__ double mj[128];
+    const int2 IJ = a.pairs[blockIdx.x];
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
+    const bool rag = (a.N & 63) && IJ.y == a.ntiles - 1;
+    if (rag) n3_tile<VARIANT, GUARD, true, false, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+    else n3_tile<VARIANT, GUARD, false, false, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
+}
+
 #if defined(MDQT_EXPT_STAMPS)
 extern "C" int mdqt_expt_n3_stamps(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_n3_stamps), sizeof(unsigned long long) * 6 * n) == hipSuccess ? 0 : -1;
@@ -415,6 +430,20 @@ hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEven
     } else {
         if (a.guard) launch_timed(k_pairs_n3<0, true>, grid, dim3(64 * N3W), s, ev0, ev1, a);
         else launch_timed(k_pairs_n3<0, false>, grid, dim3(64 * N3W), s, ev0, ev1, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s) {
+    if (a.npairs <= 0) return hipSuccess;
+    if (variant < 0 || variant > 1) return hipErrorInvalidValue;
+    const dim3 grid(a.npairs), blk(64 * N3W);
+    if (variant == 1) {
+        if (a.guard) hipLaunchKernelGGL((k_pairs_n3_pot<1, true>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_pairs_n3_pot<1, false>), grid, blk, 0, s, a);
+    } else {
+        if (a.guard) hipLaunchKernelGGL((k_pairs_n3_pot<0, true>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_pairs_n3_pot<0, false>), grid, blk, 0, s, a);
     }
     return hipGetLastError();
 }

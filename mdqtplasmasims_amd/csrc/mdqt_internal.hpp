@@ -426,6 +426,8 @@ hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s);
 hipError_t launch_forces(const ForceArgs& a, hipStream_t s);
 hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEvent_t ev0 = nullptr,
                             hipEvent_t ev1 = nullptr);
+// Epotential on the Newton-3 tiles (world 1): pair potentials into slot component 0 of a.P
+hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s);
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
                                   hipStream_t s);
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[seg][0][i]

@@ -124,7 +124,9 @@ __device__ __forceinline__ void accum(double& f, double d, double ft) {
 #ifndef MDQT_SHIFT_I
 #define MDQT_SHIFT_I 1
 #endif
-template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false>
+// POT: Epotential's pair potential u (pair_u) instead of the force: u to the i accumulator fx and
+// to the j accumulator ax only (both sides of a pair get +u)
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
@@ -138,6 +140,15 @@ __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi,
         }
     } else {
         mic_v<VARIANT, GUARD>(dx, dy, dz, c);
+    }
+    if constexpr (POT) {
+        double u = pair_u<VARIANT>(dx, dy, dz, c);
+        if (RAGGED) u *= mi * mj[idx];
+        u *= m;
+        fx += u;
+        __hip_atomic_fetch_add(&ax[idx], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        (void)ay; (void)az; (void)fy; (void)fz;
+        return;
     }
     double ft = CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];
@@ -181,7 +192,7 @@ __device__ __forceinline__ void slot_store(double* p, double v) {
 #ifndef MDQT_N3_CUT
 #define MDQT_N3_CUT 1
 #endif
-template <int VARIANT, bool GUARD, bool RAGGED, bool SIG>
+template <int VARIANT, bool GUARD, bool RAGGED, bool SIG, bool POT = false>
 __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
                                         double (*ia)[3][64]) {
@@ -215,7 +226,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     double* ay = accj[q][1];
     double* az = accj[q][2];
     auto step = [&](int idx, double m) {
-        n3_step<VARIANT, GUARD, RAGGED, false, CUT>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+        n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
     };
     const bool diag = I == J;
     if (!diag) {
@@ -231,23 +242,24 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     ia[q][0][l] = fx; ia[q][1][l] = fy; ia[q][2][l] = fz;
     __syncthreads();
     const size_t slab3 = (size_t)3 * S;
+    constexpr int NK = POT ? 1 : 3;                 // potential: component 0 only, j side not negated
     if (q == 0) {                                   // rows of I -> slot J (diagonal: I)
         double* Pi = a.P + (size_t)J * slab3;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < NK; ++k) {
             double v = ia[0][k][l];
 #pragma unroll
             for (int w = 1; w < N3W; ++w) v += ia[w][k][l];
-            if (diag) v = v - n3_jsum(accj, k, l);
+            if (diag) v = POT ? v + n3_jsum(accj, k, l) : v - n3_jsum(accj, k, l);
             if (i < S) slot_store<SIG>(&Pi[(size_t)k * S + i], v);
         }
     } else if (q == 1 && !diag) {                   // rows of J -> slot I
         double* Pj = a.P + (size_t)I * slab3;
         const int j = J * 64 + l;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < NK; ++k) {
             const double w = n3_jsum(accj, k, l);
-            if (j < S) slot_store<SIG>(&Pj[(size_t)k * S + j], -w);
+            if (j < S) slot_store<SIG>(&Pj[(size_t)k * S + j], POT ? w : -w);
         }
     }
     if constexpr (SIG) {                            // every storing wave drained, then one arrival

@@ -466,6 +466,20 @@ def test_observables_match_oracle(eng, orc):
     assert abs(s.Epotential() - o.epotential()) <= 1e-12 * abs(o.epotential())
 
 
+@pytest.mark.parametrize("N0", [500, 3500])
+def test_epotential_newton3_tiles_match_rows(eng, N0):
+    """Epotential() on the Newton-3 tiles (each distinct pair once, world 1 default) against the
+    owner-computes rows (every ordered pair): the same sum up to summation order"""
+    s = eng.Simulation(N0=N0, seed=29).init()
+    s.md_steps(2)
+    assert s.const("force_scheme") == 2 and s.const("potential_n3") == 1
+    e3 = s.Epotential()
+    s.set_option("potential_n3", 0)
+    er = s.Epotential()
+    s.close()
+    assert abs(e3 - er) <= 1e-14 * abs(er), (e3, er)
+
+
 def _read_dir(d):
     out = {}
     for f in sorted(os.listdir(d)):

@@ -1037,6 +1037,27 @@ static void fill_pair_consts(ForceArgs& a, double L, double lDeb, int variant) {
     a.variant = variant;
 }
 
+static ForceArgs force_args(mdqt_ctx* s, double* out);
+// the block-pair kernels' arguments for the current positions: with force_sort, the Hilbert order,
+// the sorted copy and the tile boxes are recomputed here (mdqt_sort.hip)
+static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
+    a = s->n3b;
+    ForceArgs c = force_args(s, nullptr);
+    a.Rall = s->dR; a.slots = s->dSlots; a.S = s->S;
+    a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
+    a.micGuard = c.micGuard; a.guard = c.guard;
+    a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr;
+    if (s->sort_mode) {                            // Hilbert order + tile boxes (mdqt_sort.hip)
+        SortArgs o;
+        o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
+        o.keys = s->dKeys; o.keys2 = s->dKeys + s->N; o.ion = s->dIon; o.perm = s->dIon + s->N;
+        o.tmp = s->dSortTmp; o.tmp_bytes = s->sortTmpBytes; o.Rs = s->dRs; o.boxes = s->dBoxes;
+        HIPCHK(launch_spatial_order(o, s->stream));
+        a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes;
+    }
+    return 0;
+}
+
 static ForceArgs force_args(mdqt_ctx* s, double* out) {
     ForceArgs a;
     a.Rall = s->dR;
@@ -1136,20 +1157,8 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         s->f_pending = true;       // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots;
     } else if (s->use_n3b) {
-        N3BArgs a = s->n3b;
-        ForceArgs c = force_args(s, nullptr);
-        a.Rall = s->dR; a.slots = s->dSlots; a.S = s->S;
-        a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
-        a.micGuard = c.micGuard; a.guard = c.guard;
-        a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr;
-        if (s->sort_mode) {                        // Hilbert order + tile boxes (mdqt_sort.hip)
-            SortArgs o;
-            o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
-            o.keys = s->dKeys; o.keys2 = s->dKeys + s->N; o.ion = s->dIon; o.perm = s->dIon + s->N;
-            o.tmp = s->dSortTmp; o.tmp_bytes = s->sortTmpBytes; o.Rs = s->dRs; o.boxes = s->dBoxes;
-            HIPCHK(launch_spatial_order(o, s->stream));
-            a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes;
-        }
+        N3BArgs a;
+        if (n3b_args(s, a)) return -1;
         const int W = s->p.world_size;
         HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream));
         if (W > 1) {
@@ -1520,6 +1529,15 @@ static int potential_rows(mdqt_ctx* s, double* urow_dev) {
         a.arrive = nullptr;
         HIPCHK(launch_potential_n3(a, s->force_variant, s->stream));
         HIPCHK(launch_reduce_segments(s->dUpart, urow_dev, s->nslots, s->nloc, s->S, 1, s->stream));
+        return 0;
+    }
+    // world 1 with Newton-3 blocks (N > 65,536): the block kernel's POT mode, per-ion row sums by
+    // k_n3b_reduce (the block slots are free between force calls: the force path reduces at once)
+    if (s->use_n3b && s->p.world_size == 1 && s->local.empty() && s->force_variant <= 1 && s->n3_potential) {
+        if (settle_forces(s)) return -1;
+        N3BArgs a;
+        if (n3b_args(s, a)) return -1;
+        HIPCHK(launch_potential_n3b(a, s->force_variant, urow_dev, s->stream));
         return 0;
     }
     double* buf = s->dFpart;

@@ -189,7 +189,8 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
     return Rall + (size_t)w * 3 * S + (g - w * S);
 }
 
-template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT>
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
+          bool POT = false>
 __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi, double zi, double mi,
                                          const double (*pj)[128], const double* mj, double* ax, double* ay,
                                          double* az, double& fx, double& fy, double& fz, const PairC& c,
@@ -198,7 +199,7 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
         for (int t0 = 0; t0 < 64; t0 += 16) {
 #pragma unroll
             for (int t = 0; t < 16; ++t)
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
                                                        c, nsh);
         }
     } else {
@@ -206,14 +207,15 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 const double m = (t0 + t == 32 && l >= 32) ? 0. : 1.;   // lane distance 32: once
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
                                                        c, nsh);
             }
         }
     }
 }
 
-template <int VARIANT, bool GUARD>
+// POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
+template <int VARIANT, bool GUARD, bool POT = false>
 // the fast variant fits 64 VGPRs (8 waves per SIMD); the exact one (libm exp, divisions) gets 128
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(VARIANT == 1 ? 8 : 4, VARIANT == 1 ? 8 : 4)))
 void k_pairs_n3b(N3BArgs a) {
@@ -315,27 +317,30 @@ void k_pairs_n3b(N3BArgs a) {
                 // in spatial order they arrive in coherent groups, and one serial chain would
                 // carry their rounding: momentum |sum F| / mean |F| 1.8e-8 -> 1e-10 at C4)
                 double tx = 0., ty = 0., tz = 0.;
+                constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
                 if (ragN && (I == T - 1 || J == T - 1))
-                    n3b_pair<VARIANT, GUARD, true>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
+                    n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
+                                                                    tz, c);
                 else if (VARIANT == 1 && cls > 0.) {
                     const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
                     if (MDQT_SHIFT_I)                   // xi - n L once per tile pair (n3_step SHIFT)
-                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1>(diag, l, fma(-nsh[0], a.L, xi),
-                                                                      fma(-nsh[1], a.L, yi), fma(-nsh[2], a.L, zi), mi,
-                                                                      pj, mj, ax, ay, az, tx, ty, tz, c, nsh);
+                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(
+                            diag, l, fma(-nsh[0], a.L, xi), fma(-nsh[1], a.L, yi), fma(-nsh[2], a.L, zi), mi, pj, mj,
+                            ax, ay, az, tx, ty, tz, c, nsh);
                     else
-                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx,
-                                                                      ty, tz, c, nsh);
+                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                                ay, az, tx, ty, tz, c, nsh);
                 } else
-                    n3b_pair<VARIANT, GUARD, false>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
+                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx,
+                                                                     ty, tz, c);
                 bx += tx; by += ty; bz += tz;
             }
             __syncthreads();
-            if (q < 3) {                            // j side of J's rows -> j-slot db
+            if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db
                 double v = 0.;
 #pragma unroll
                 for (int w = 0; w < BW; ++w) v = v + (accj[w][q][l] + accj[w][q][l + 64]);
-                a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = -v;
+                a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? v : -v;
             }
             __syncthreads();
         }
@@ -460,6 +465,22 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
         }
     }
     hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, a, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s) {
+    if (variant < 0 || variant > 1) return hipErrorInvalidValue;
+    const int nblk = (a.Phi - a.Plo) * a.R;
+    if (nblk > 0) {
+        if (variant == 1) {
+            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<1, true, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            else hipLaunchKernelGGL((k_pairs_n3b<1, false, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+        } else {
+            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<0, true, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            else hipLaunchKernelGGL((k_pairs_n3b<0, false, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+        }
+    }
+    hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 1), dim3(256), 0, s, a, out);   // component 0
     return hipGetLastError();
 }
 

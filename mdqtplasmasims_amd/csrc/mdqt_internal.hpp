@@ -428,6 +428,8 @@ hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEven
                             hipEvent_t ev1 = nullptr);
 // Epotential on the Newton-3 tiles (world 1): pair potentials into slot component 0 of a.P
 hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s);
+// Epotential on the Newton-3 blocks (world 1): per-ion row sums of u into out[S]
+hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
                                   hipStream_t s);
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[seg][0][i]

@@ -195,3 +195,21 @@ def test_sharded_newton3_blocks_above_64k_local_group(world, orc):
     for s in sims:
         s.close()
     ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sort", [1, 0])
+def test_epotential_newton3_blocks_match_rows(sort):
+    """Epotential() above 65,536 ions on the Newton-3 blocks (the block kernel's POT mode, world 1,
+    Hilbert order with tile-pair skipping or storage order) against the owner-computes rows"""
+    import mdqtplasmasims_amd as M
+    s = M.Simulation(N0=70000, seed=23, rng_mode=1).init()
+    s.set_option("force_sort", sort)
+    s.md_steps(1)
+    assert s.const("force_scheme") == 3 and s.const("potential_n3") == 1
+    e3 = s.Epotential()
+    s.set_option("potential_n3", 0)
+    er = s.Epotential()
+    s.close()
+    print(f"N0=70000 sort={sort}: Epot blocks {e3:.15e} rows {er:.15e}")
+    assert abs(e3 - er) <= 1e-13 * abs(er), (e3, er)

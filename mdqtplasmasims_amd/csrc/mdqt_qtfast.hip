@@ -377,7 +377,8 @@ __device__ unsigned long long g_md_stamps[4 * 4096];
 #define LANE_WPE_ATTR
 #endif
 // FAST: the production launch — step + qstep (do_step, do_qt), every substep with t > 0 (all but
-// the simulation's first launch), F from the force slots (nseg > 1), no arrival wait: step_R's
+// the simulation's first launch), F from the force slots (or F itself when nseg == 1), no arrival
+// wait: step_R's
 // non-moving branch (:360), the last substep's no-drift select and the other paths' loads and
 // branches are compiled out (straight-line prologue: one memory round trip)
 // FUSED (with FAST; the QT workgroups of k_md_step): the force partials of this launch's own
@@ -427,7 +428,8 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     // overlapped MD step (a.arrive): the partials are read after the arrival wait below, with
     // L1-bypassing loads; otherwise right here, with the other prologue loads
     auto slot_round = [&](int s0, double (*t)[3], bool sc1) {   // slots s0, s0 + 16, + 32, + 48
-        const double* base_p = a.Fpart + i;
+        // FAST with nseg == 1 (F already summed): slot 0 is F itself, the other lanes add zeros
+        const double* base_p = (FAST && nseg == 1 ? (const double*)a.F : a.Fpart) + i;
         const size_t plane = (size_t)3 * S;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -813,7 +815,7 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
     const dim3 gl((a.n + kLaneWG / 16 - 1) / (kLaneWG / 16)), bl(kLaneWG), gt((a.n + 255) / 256), b(256);
     if (mode == 2) {
         const uint64_t all = (1ull << a.nsub) - 1;
-        const bool allmove = a.do_step && a.do_qt && a.nseg > 1 && !a.arrive && (a.movmask & all) == all;
+        const bool allmove = a.do_step && a.do_qt && a.nseg >= 1 && !a.arrive && (a.movmask & all) == all;
 #ifndef MDQT_IM01
 #define MDQT_IM01 1
 #endif

@@ -187,7 +187,14 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     are bit-identical to each other within one qt_math mode
  *   "qt_im01":        1 (default where the table allows) = the lane kernel's production launch
  *                     drops the real-part FMAs of the purely imaginary static coupling slots,
- *                     0 = the general instance (bit-identical up to the sign of zero) */
+ *                     0 = the general instance (bit-identical up to the sign of zero)
+ *   "potential_n3":   1 (default) = Epotential on the Newton-3 tiles / blocks (each distinct
+ *                     pair once; world 1), 0 = the owner-computes potential rows (Epot within 1e-14 relative)
+ *   "init_threads":   init() rejection sampling: 0 = auto, 1 = sequential, k = k host threads
+ *                     (bit-identical positions, psi and drand48 state in every setting)
+ *   "fused_step", "overlap": 1 = the one-launch MD step / the two-stream MD step (measured and
+ *                     kept off by default; bit-identical to 0)
+ *   "expt_force_sig": diagnostic only (force launches with arrival counts, no consumer) */
 int         mdqt_set_option(mdqt_ctx* c, const char* name, int value);
 
 /* ---- streams, timing, multi-GPU plumbing ---- */

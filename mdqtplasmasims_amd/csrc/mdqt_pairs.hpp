@@ -183,9 +183,17 @@ __device__ __forceinline__ double n3_jsum(const double (*accj)[3][128], int k, i
 #ifndef MDQT_EXPT_SIGMODE
 #define MDQT_EXPT_SIGMODE 0     // diagnostic builds: 1 = no arrival atomics, 2 = plain slot stores
 #endif
+// Every tile-pair slot store is write-through (agent scope): the slots stream out while the
+// kernel runs instead of sitting dirty in the XCDs' L2s for the kernel-end write-back that makes
+// them visible to the QT launch's waves on other XCDs.  A/B at C2: force launch 16.8 -> 16.2 us,
+// MD step -0.6 us.  0: plain stores (A/B builds).
+#ifndef MDQT_SLOT_WT
+#define MDQT_SLOT_WT 1
+#endif
 template <bool SIG>
 __device__ __forceinline__ void slot_store(double* p, double v) {
-    if constexpr (SIG && MDQT_EXPT_SIGMODE != 2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr ((SIG && MDQT_EXPT_SIGMODE != 2) || MDQT_SLOT_WT)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
 }
 

@@ -350,6 +350,18 @@ __device__ __forceinline__ double lane_sum_p8(double T, double one) {
     return fmac_bcast<7>(a, T, one);
 }
 
+// the lane kernel's state stores (R, V, F, tPart, psi) write-through, like the force slots
+// (mdqt_pairs.hpp MDQT_SLOT_WT): waves that finish early stream their ions out before the last
+// wave ends, and the kernel-end L2 write-back has nothing left to do.  A/B at C2 on top of the
+// slot stores: QT launch -0.4 us, MD step -0.6 us.  0: plain stores (A/B builds).
+#ifndef MDQT_QT_WT
+#define MDQT_QT_WT 1
+#endif
+__device__ __forceinline__ void qt_store(double* p, double v) {
+    if constexpr (MDQT_QT_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 #if defined(MDQT_EXPT_QTSTAMPS)
 // diagnostic build only: per-wave s_memtime at entry, loop start, loop end, exit + s_memrealtime
 // at entry and exit, s_memtime after the force-slot loads, and the number of substeps in which an
@@ -537,7 +549,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     if (FAST || nseg > 1) {
         const double fx = lane_tree16(qf[0]), fy = lane_tree16(qf[1]), fz = lane_tree16(qf[2]);
         f = c == 0 ? fx : c == 1 ? fy : fz;
-        if (store && owner) a.F[(size_t)c * S + i] = f;
+        if (store && owner) qt_store(&a.F[(size_t)c * S + i], f);
     }
     if (threadIdx.x < MAXSUB) edt[threadIdx.x] = edv;
     __syncthreads();
@@ -704,15 +716,15 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     QT_STAMP(2, __builtin_amdgcn_s_memtime());
     if (store) {
         if (owner) {
-            a.R[(size_t)c * S + i] = p;
-            a.V[(size_t)c * S + i] = v;
+            qt_store(&a.R[(size_t)c * S + i], p);
+            qt_store(&a.V[(size_t)c * S + i], v);
             if (!(p >= -0.125 * L && p <= 1.125 * L)) *a.oor = 1;
         }
         if (FAST || a.do_qt) {
-            if (k == 0) a.tPart[i] = tPart;
+            if (k == 0) qt_store(&a.tPart[i], tPart);
             if (st < NS) {
-                a.psi[(size_t)(2 * st) * S + i] = w.re;
-                a.psi[(size_t)(2 * st + 1) * S + i] = w.im;
+                qt_store(&a.psi[(size_t)(2 * st) * S + i], w.re);
+                qt_store(&a.psi[(size_t)(2 * st + 1) * S + i], w.im);
             }
         }
     }

@@ -89,7 +89,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r02f_c2_pmc.json")):
+def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r02g_c2_pmc.json")):
     """HBM bytes per launch of the kernel from the committed rocprofv3 --pmc summary of the same
     C2 workload (FETCH_SIZE and WRITE_SIZE in separate passes, kB -> B; no gfx950 x2 read
     correction: the kernel's loads are 8 B/lane, outside the guide's calibrated 16 B/lane case).

@@ -14,18 +14,18 @@ timeout -k 10 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_ou
 echo "bench wall $(( $(date +%s) - start )) s"
 tail -1 gpurun_out/bench_full.log > gpurun_out/bench_full.json
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r02f" -o run -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$R/gpurun_out/prof_r02f.log" 2>&1 || { tail -5 "$R/gpurun_out/prof_r02f.log"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r02g" -o run -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$R/gpurun_out/prof_r02g.log" 2>&1 || { tail -5 "$R/gpurun_out/prof_r02g.log"; exit 1; }
 B="$R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --sharded-config none --million-config none --no-pump-lines --no-mcmd-lines --md-only-config none --no-e2e-line --no-replicas-line"
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/pmc_fetch" -o run -- python3 $B > "$R/gpurun_out/pmc_fetch.log" 2>&1 || exit $?
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/pmc_write" -o run -- python3 $B > "$R/gpurun_out/pmc_write.log" 2>&1 || exit $?
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$R/gpurun_out/pmc_sq" -o run -- python3 $B > "$R/gpurun_out/pmc_sq.log" 2>&1 || exit $?
 cd "$R"
-python3 tools/prof_summary.py $(ls gpurun_out/prof_r02f/*/*.db gpurun_out/prof_r02f/*.db 2>/dev/null | head -1) > gpurun_out/r02f_driver_cmd_kernel_stats.txt
-python3 tools/prof_mainline.py $(ls gpurun_out/prof_r02f/*/*.db gpurun_out/prof_r02f/*.db 2>/dev/null | head -1) 24 > gpurun_out/r02f_driver_cmd_headline_kernels.txt 2>&1 || true
-python3 tools/pmc_summary.py $(ls gpurun_out/pmc_fetch/*/*.db gpurun_out/pmc_fetch/*.db 2>/dev/null | head -1) $(ls gpurun_out/pmc_write/*/*.db gpurun_out/pmc_write/*.db 2>/dev/null | head -1) $(ls gpurun_out/pmc_sq/*/*.db gpurun_out/pmc_sq/*.db 2>/dev/null | head -1) > gpurun_out/r02f_c2_pmc.json
-grep "^{" gpurun_out/prof_r02f.log | tail -1 > gpurun_out/r02f_driver_cmd_bench_under_rocprof.json
-head -12 gpurun_out/r02f_driver_cmd_kernel_stats.txt
-head -12 gpurun_out/r02f_driver_cmd_headline_kernels.txt
+python3 tools/prof_summary.py $(ls gpurun_out/prof_r02g/*/*.db gpurun_out/prof_r02g/*.db 2>/dev/null | head -1) > gpurun_out/r02g_driver_cmd_kernel_stats.txt
+python3 tools/prof_mainline.py $(ls gpurun_out/prof_r02g/*/*.db gpurun_out/prof_r02g/*.db 2>/dev/null | head -1) 24 > gpurun_out/r02g_driver_cmd_headline_kernels.txt 2>&1 || true
+python3 tools/pmc_summary.py $(ls gpurun_out/pmc_fetch/*/*.db gpurun_out/pmc_fetch/*.db 2>/dev/null | head -1) $(ls gpurun_out/pmc_write/*/*.db gpurun_out/pmc_write/*.db 2>/dev/null | head -1) $(ls gpurun_out/pmc_sq/*/*.db gpurun_out/pmc_sq/*.db 2>/dev/null | head -1) > gpurun_out/r02g_c2_pmc.json
+grep "^{" gpurun_out/prof_r02g.log | tail -1 > gpurun_out/r02g_driver_cmd_bench_under_rocprof.json
+head -12 gpurun_out/r02g_driver_cmd_kernel_stats.txt
+head -12 gpurun_out/r02g_driver_cmd_headline_kernels.txt
 python3 -c "
 import json; d=json.load(open('gpurun_out/bench_full.json'))
 print(d['value'], d['ms_per_step'], d['config']['kernel_ms'])

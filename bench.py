@@ -244,18 +244,55 @@ def sharded_in_children(cfg, steps, rank, world, timeout):
     raise RuntimeError("sharded child printed no result")
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_launch_command(gpus, argv, env):
+    """The command that starts the `gpus` rank processes of `bench.py --gpus N` when no launcher did
+    (no WORLD_SIZE in the environment): torch.distributed.run, one process per GPU, on 127.0.0.1.
+    None when this process already is a rank (or N = 1)."""
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, env):
+    """--gpus N must be the launcher's world size: a run that silently measures fewer GPUs than it
+    was asked for is an error."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return world
+
+
 def main():
     args = parse()
     if args.child_sharded:
         return child_main(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # `python bench.py --gpus N` without a launcher: start the N ranks here, before this process
+    # touches the GPU (no HIP call has been made yet), and exit with their status
+    cmd = rank_launch_command(args.gpus, sys.argv[1:], os.environ)
+    if cmd is not None:
+        import subprocess
+        print(f"bench.py: starting {args.gpus} ranks: {' '.join(cmd[:6])} ...", file=sys.stderr, flush=True)
+        sys.exit(subprocess.run(cmd).returncode)
+    world = check_world(args.gpus, os.environ)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
+    comm_size = 1
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        comm_size = dist.get_world_size()
+        if comm_size != args.gpus:
+            raise SystemExit(f"bench.py: the RCCL group has {comm_size} ranks, --gpus {args.gpus}")
 
     import mdqtplasmasims_amd as M
     params, qt, desc = CONFIGS[args.config]
@@ -341,6 +378,7 @@ def main():
             "value": value,
             "unit": "particle-qsteps/s",
             "n_gpus": world,
+            "comm_size": comm_size,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": el_max / args.steps * 1e3,
@@ -644,6 +682,9 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
         obj = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         sim.comm_init(obj[0])
+    comm_size = sim.comm_size()                    # ncclCommCount of the product's communicator
+    if comm_size != world:
+        raise RuntimeError(f"RCCL communicator has {comm_size} ranks, world {world}")
     t0 = time.perf_counter()
     sim.init()                                     # collective: Epot0 over all slabs
     t_init = time.perf_counter() - t0
@@ -673,7 +714,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
              "note": "this rank's forces() incl. all-gather/reduce-scatter; flops = 30 x N(N-1)/2 (SURVEY 8d)"}
     return {"workload": desc + ", one system sharded over all ranks (RCCL position all-gather; "
                            "Newton-3 block-pair forces reduce-scattered)",
-            "N": N, "n_gpus": world, "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
+            "N": N, "n_gpus": world, "comm_size": comm_size, "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force,

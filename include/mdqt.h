@@ -214,6 +214,9 @@ int         mdqt_set_counters(mdqt_ctx* c, int c0, unsigned counter, double Epot
  * collectives (sum all-reduces; rank 0 writes the files). */
 int         mdqt_comm_unique_id(void* out, size_t len);
 int         mdqt_comm_init(mdqt_ctx* c, const void* uid, size_t len);
+/* ranks in this context's communicator: ncclCommCount of the RCCL communicator, the group size
+ * of an in-process group, 1 without either (the bench checks it against --gpus) */
+int         mdqt_comm_size(const mdqt_ctx* c, int* n);
 /* in-process group of world_size contexts (tests on one GPU): the all-gather becomes device
  * copies; the caller steps the ranks in lockstep (all all-gathers, then all forces ...) */
 int         mdqt_comm_init_local(mdqt_ctx* const* ctxs, int n);

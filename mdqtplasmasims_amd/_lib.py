@@ -138,6 +138,7 @@ SIGNATURES = [
     ("mdqt_comm_unique_id", C.c_int, [C.c_char_p, C.c_size_t]),
     ("mdqt_comm_init", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
     ("mdqt_comm_init_local", C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    ("mdqt_comm_size", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     ("mdqt_allgather_positions", C.c_int, [C.c_void_p]),
     ("mdqt_allreduce_sum", C.c_int, [C.c_void_p, _dp, C.c_size_t]),
     ("mdqt_kernel_time_totals", C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int), _dp, C.POINTER(C.c_int)]),

@@ -665,7 +665,7 @@ __global__ __launch_bounds__(256) void k_tagged_kde(const double* __restrict__ V
     }
     __syncthreads();
     const double vel = (double)(j + bin0) * 0.0025;                 // QTT:250 (bin0 = -2000)
-    const double V2 = 1. / (2. * 0.002 * 0.002);                   // QTT:1072
+    const double V2 = kKdeV2;                                      // 1 / (2 * 0.002^2), QTT:1072
     double p[3] = {0., 0., 0.};
     const int m = min(TKDE_CHUNK, N - i0);
     for (int k = 0; k < m; ++k) {
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(256) void k_tagged_kde(const double* __restrict__ V
         // V2 d^2 >= 746.9, below exp's underflow) adds exact zeros there and is skipped
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-            if (__builtin_amdgcn_ballot_w64(!(fabs(vel - sv[c][k]) >= 0.0773)))
+            if (__builtin_amdgcn_ballot_w64(!(fabs(vel - sv[c][k]) >= kKdeSkip)))
                 p[c] += exp(-V2 * (vel - sv[c][k]) * (vel - sv[c][k]));   // :1100-1102
     }
     if (j < TKDE_BINS)

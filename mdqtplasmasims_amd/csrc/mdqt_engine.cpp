@@ -109,6 +109,11 @@ struct mdqt_ctx {
     double* dFr = nullptr;         // sharded n3b: this rank's dense partial forces [world][3][S]
     // spatial order of the n3b scheme (mdqt_sort.hip; option "force_sort", default on)
     int sort_mode = 1;             // 0 off, 1 sorted + tile-pair skipping, 2 sorted, nothing skipped (tests)
+    // error-bounded force tail (option "force_tail_exp" k: eps = 10^-k, 0 = off): tile pairs whose
+    // boxes are >= r_t apart are skipped, r_t the smallest radius with (N - 1) g(r_t) <= eps,
+    // g(r) = (1/r + 1/lDeb) e^(-r/lDeb) / r the pair force magnitude (SpeedUp:224) — so no ion's
+    // force changes by more than eps; a no-op where r_t >= L/2 (every BASELINE size but N ~ 1e6)
+    int tail_exp = 12;
     uint32_t* dKeys = nullptr;     // [2][N] Hilbert keys, sorted keys
     int* dIon = nullptr;           // [2][N] identity, sorted index -> ion
     void* dSortTmp = nullptr;
@@ -129,6 +134,8 @@ struct mdqt_ctx {
     // §8): k_md_step, see md_step_fused
     int fused_opt = 0;
     int last_fused = 0;                    // the last MD step ran as one k_md_step launch
+    int last_qt_kernel = 0;                // QT kernel instance of the last substep launch (QTKernel codes)
+    int last_qt_nseg = 0;                  // force partials that launch summed in its prologue
     int* dSpinErr = nullptr;
     unsigned long long* force_arrive = nullptr;   // set around a force launch of an overlapped step
     hipStream_t sub_stream = nullptr;             // set around the QT launch of an overlapped step
@@ -807,6 +814,7 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     delete s;
 }
 
+static double tail_radius(int N, double L, double lDeb, int k, double* bound);
 extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "gamToEinsteinFreq")) return s->gamToE;
     if (!strcmp(n, "quantumTimestep")) return s->dtQ;
@@ -821,10 +829,19 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_segments")) return s->nseg;
     if (!strcmp(n, "force_scheme")) return s->use_n3b ? 3 : s->use_n3 ? 2 : 1;
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
+    if (!strcmp(n, "force_skip_radius") || !strcmp(n, "force_tail_bound")) {   // the tile-pair skip radius
+        double bound;                                  // and its force bound (0: exact, r = L/2)
+        const double r = (s->use_n3b && s->sort_mode == 1) ? tail_radius(s->N, s->L, s->lDeb, s->tail_exp, &bound)
+                                                           : (bound = 0., s->L / 2.);
+        return n[6] == 's' ? r : bound;
+    }
     if (!strcmp(n, "fused_step")) return s->fused_opt;
     if (!strcmp(n, "qt_im01")) return s->qc.im01;
     if (!strcmp(n, "potential_n3")) return s->n3_potential;
     if (!strcmp(n, "md_step_fused")) return s->last_fused;     // 1: the last MD step was one k_md_step launch
+    if (!strcmp(n, "qt_kernel")) return s->last_qt_kernel;     // instance of the last substep launch (QTKernel)
+    if (!strcmp(n, "qt_kernel_nseg")) return s->last_qt_nseg;  // force partials its prologue summed
+    if (!strcmp(n, "force_slots")) return s->nslots;           // Newton-3 tile slots (0: other schemes)
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
     return NAN;
@@ -1038,6 +1055,30 @@ static void fill_pair_consts(ForceArgs& a, double L, double lDeb, int variant) {
 }
 
 static ForceArgs force_args(mdqt_ctx* s, double* out);
+
+// The error-bounded tail radius: the smallest r in (0, L/2] with (N - 1) g(r) <= eps, where
+// g(r) = (1/r + 1/lDeb) exp(-r/lDeb) / r is |F| of one pair at distance r (SpeedUp:224 times r),
+// decreasing in r.  A skipped tile pair's boxes are >= r_t apart, so each of its pairs is, and the
+// pairs an ion loses number at most N - 1: |dF_i| <= (N - 1) g(r_t) <= eps (rigorous; the actual
+// tail is far smaller — its terms have random directions).  L/2 (exact: nothing extra skipped)
+// when eps = 0 or (N - 1) g(L/2) > eps.  bound = (N - 1) g(r_t) (0 when exact).
+static double tail_g(double r, double lDeb) { return (1. / r + 1. / lDeb) * exp(-r / lDeb) / r; }
+static double tail_radius(int N, double L, double lDeb, int k, double* bound) {
+    const double Rcut = L / 2.;
+    *bound = 0.;
+    if (k <= 0 || N < 2) return Rcut;
+    const double eps = pow(10., -k);
+    const double n1 = (double)(N - 1);
+    if (n1 * tail_g(Rcut, lDeb) > eps) return Rcut;
+    double lo = 0., hi = Rcut;                      // n1 g(hi) <= eps < n1 g(lo)
+    for (int it = 0; it < 200 && hi - lo > 1e-12 * Rcut; ++it) {
+        const double m = 0.5 * (lo + hi);
+        if (m > 0 && n1 * tail_g(m, lDeb) <= eps) hi = m; else lo = m;
+    }
+    *bound = n1 * tail_g(hi, lDeb);
+    return hi;
+}
+
 // the block-pair kernels' arguments for the current positions: with force_sort, the Hilbert order,
 // the sorted copy and the tile boxes are recomputed here (mdqt_sort.hip)
 static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
@@ -1047,6 +1088,8 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
     a.micGuard = c.micGuard; a.guard = c.guard;
     a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr;
+    double bound;
+    a.Rskip = tail_radius(s->N, s->L, s->lDeb, s->tail_exp, &bound);
     if (s->sort_mode) {                            // Hilbert order + tile boxes (mdqt_sort.hip)
         SortArgs o;
         o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
@@ -1144,7 +1187,10 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
     if (s->use_n3) {
         N3Args a{};                  // variant 2 (MCMD's exact pair set, rc2) is not used here
         if (s->force_variant > 1) return fail("mdqt_forces: force_kernel must be 0 or 1");
-        a.R = s->dR; a.P = s->dFpart; a.pairs = s->dPairs;
+        // one tile (N <= 64): its one slot has F's [3][S] layout, so the kernel writes F itself and
+        // nothing is pending (the substep kernels read F when nseg == 1)
+        const bool one_slot = s->nslots == 1;
+        a.R = s->dR; a.P = one_slot ? s->dF : s->dFpart; a.pairs = s->dPairs;
         a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs;
         ForceArgs c = force_args(s, nullptr);
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
@@ -1154,7 +1200,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         if (tm && take_events(s, 0, &e0, &e1)) return -1;
         a.arrive = s->force_arrive;                // overlapped MD step: count finished workgroups
         HIPCHK(launch_forces_n3(a, s->force_variant, s->stream, e0, e1));
-        s->f_pending = true;       // slots summed by the next substep launch (or settle_forces)
+        s->f_pending = !one_slot;  // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots;
     } else if (s->use_n3b) {
         N3BArgs a;
@@ -1231,8 +1277,11 @@ static int run_substeps(mdqt_ctx* s, int n, int do_step, int do_qt_flag, int adv
         hipEvent_t e0 = nullptr, e1 = nullptr;       // timing: the kernel's own timestamps
         if (tm && (take_events(s, 1, &e0, &e1))) return -1;
         hipStream_t st = s->sub_stream ? s->sub_stream : s->stream;
-        if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->sub_stream ? 2 : s->substep_mode, st, e0, e1));
-        else HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream, e0, e1));
+        int inst = 0;
+        if (s->qt_math == 2) HIPCHK(launch_substeps_r(a, s->dFTab, s->sub_stream ? 2 : s->substep_mode, st, e0, e1, &inst));
+        else HIPCHK(launch_substeps(a, s->dTab, s->substep_mode, s->qt_math, s->stream, e0, e1, &inst));
+        s->last_qt_kernel = inst;
+        s->last_qt_nseg = a.nseg;
         if (advance_t) {
             s->t = t;
             s->qidx += (uint64_t)m;
@@ -1278,7 +1327,7 @@ extern "C" int mdqt_substeps(mdqt_ctx* s, int n) {
 // The overlapped MD step applies to one unsharded system on the Newton-3 tile scheme with the
 // lane-per-state QT kernel (qt_math 2, Philox stream), one fused launch per MD interval.
 static bool overlap_applies(const mdqt_ctx* s) {
-    return s->overlap_opt && s->p.world_size == 1 && s->local.empty() && s->use_n3 && s->qt_math == 2 &&
+    return s->overlap_opt && s->p.world_size == 1 && s->local.empty() && s->use_n3 && s->nslots > 1 && s->qt_math == 2 &&
            s->p.qt_enabled && s->p.rng_mode == 1 && s->ratio <= MAXSUB && s->nloc > 0 &&
            (s->substep_mode == 2 || (s->substep_mode == 0 && s->nloc < kLaneKernelMaxIons));
 }
@@ -1358,7 +1407,7 @@ static int md_steps_overlapped(mdqt_ctx* s, int n) {
 // with the remaining tile pairs; the force work ends at 32-37 us instead of 18.  Kept as an option
 // (default off) with its bit-identity tests.
 static bool fused_applies(mdqt_ctx* s) {
-    if (!(s->fused_opt && !s->overlap_opt && s->p.world_size == 1 && s->local.empty() && s->use_n3 &&
+    if (!(s->fused_opt && !s->overlap_opt && s->p.world_size == 1 && s->local.empty() && s->use_n3 && s->nslots > 1 &&
           s->qt_math == 2 && s->p.qt_enabled && s->p.rng_mode == 1 && s->ratio <= MAXSUB && s->nloc > 0 &&
           s->t > 0 && s->force_variant <= 1 &&
           (s->substep_mode == 2 || (s->substep_mode == 0 && s->nloc < kLaneKernelMaxIons))))
@@ -1407,6 +1456,8 @@ static int md_step_fused(mdqt_ctx* s) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (tm && take_events(s, 1, &e0, &e1)) return -1;
     HIPCHK(launch_md_step(f, a, s->dFTab, s->force_variant, s->stream, e0, e1));
+    s->last_qt_kernel = QTK_MD_STEP;
+    s->last_qt_nseg = a.nseg;
     s->arriveEpoch += T;
     s->f_pending = false;                              // F written by the QT workgroups
     s->t = t;
@@ -1511,7 +1562,7 @@ static int potential_rows(mdqt_ctx* s, double* urow_dev) {
     // rows; the same per-ion row sums up to summation order)
     if (s->use_n3 && !s->use_n3b && s->p.world_size == 1 && s->local.empty() && s->force_variant <= 1 &&
         s->n3_potential) {
-        const size_t need = (size_t)s->nslots * 3 * s->S;
+        const size_t need = (size_t)s->nslots * s->S;   // one plane per slot (component 0)
         if (need > s->capUpart) {
             if (s->dUpart) HIPCHK(hipFree(s->dUpart));
             s->dUpart = nullptr;
@@ -1528,7 +1579,7 @@ static int potential_rows(mdqt_ctx* s, double* urow_dev) {
         a.guard = c.guard;
         a.arrive = nullptr;
         HIPCHK(launch_potential_n3(a, s->force_variant, s->stream));
-        HIPCHK(launch_reduce_segments(s->dUpart, urow_dev, s->nslots, s->nloc, s->S, 1, s->stream));
+        HIPCHK(launch_reduce_segments(s->dUpart, urow_dev, s->nslots, s->nloc, s->S, 1, s->stream, (size_t)s->S));
         return 0;
     }
     // world 1 with Newton-3 blocks (N > 65,536): the block kernel's POT mode, per-ion row sums by
@@ -2302,6 +2353,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         s->overlap_opt = value;
         return 0;
     }
+    if (!strcmp(name, "force_tail_exp")) {             // error-bounded tail: eps = 10^-value (0: exact)
+        if (value < 0 || value > 300) return fail("force_tail_exp must be 0 (exact) .. 300");
+        s->tail_exp = value;
+        return 0;
+    }
     if (!strcmp(name, "force_sort")) {                 // Newton-3 blocks: Hilbert order + tile-pair skipping
         if (value < 0 || value > 2) return fail("force_sort must be 0 (off), 1 (on) or 2 (sorted, no skipping)");
         if (settle_forces(s)) return -1;
@@ -2410,6 +2466,16 @@ extern "C" int mdqt_comm_init(mdqt_ctx* s, const void* uid, size_t len) {
     memcpy(&id, uid, sizeof id);
     HIPCHK(hipSetDevice(s->dev));
     NCCLCHK(ncclCommInitRank(&s->comm, s->p.world_size, id, s->p.rank));
+    return 0;
+}
+
+extern "C" int mdqt_comm_size(const mdqt_ctx* s, int* n) {
+    if (!s || !n) return fail("mdqt_comm_size: bad arguments");
+    if (s->comm) {
+        NCCLCHK(ncclCommCount(s->comm, n));
+    } else {
+        *n = s->local.empty() ? 1 : (int)s->local.size();
+    }
     return 0;
 }
 

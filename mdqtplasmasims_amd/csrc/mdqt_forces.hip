@@ -84,11 +84,11 @@ __global__ __launch_bounds__(FT) void k_pairs(ForceArgs a) {
 
 __global__ __launch_bounds__(256) void k_reduce_segments(const double* __restrict__ Fpart,
                                                          double* __restrict__ F, int nseg,
-                                                         int nrows, int S, int ncomp) {
+                                                         int nrows, int S, int ncomp, size_t plane) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int c = blockIdx.y;
     if (i >= nrows || c >= ncomp) return;
-    F[(size_t)c * S + i] = slot_sum16(Fpart + (size_t)c * S + i, (size_t)3 * S, nseg);
+    F[(size_t)c * S + i] = slot_sum16(Fpart + (size_t)c * S + i, plane, nseg);
 }
 
 #if defined(MDQT_EXPT_STAMPS)
@@ -253,7 +253,8 @@ void k_pairs_n3b(N3BArgs a) {
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
     __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class (-1 skip, 1 uniform, 0 per pair)
-    const double rc2 = a.Rcut * a.Rcut;
+    // skip below the cutoff only for the forces (error-bounded tail, mdqt_engine.cpp tail_radius)
+    const double rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
     auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
         const double* B = a.boxes;
         double g2 = 0.;
@@ -407,11 +408,13 @@ hipError_t launch_forces(const ForceArgs& a, hipStream_t s) { return launch_rows
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s) { return launch_rows<1>(a, s); }
 
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
-                                  hipStream_t s) {
+                                  hipStream_t s, size_t plane) {
     if (nrows <= 0) return hipSuccess;
     if (ncomp < 1 || ncomp > 3) return hipErrorInvalidValue;
+    if (plane == 0) plane = (size_t)3 * S;
+    if (plane < (size_t)ncomp * S) return hipErrorInvalidValue;
     dim3 grid((nrows + 255) / 256, ncomp);
-    hipLaunchKernelGGL(k_reduce_segments, grid, dim3(256), 0, s, Fpart, F, nseg, nrows, S, ncomp);
+    hipLaunchKernelGGL(k_reduce_segments, grid, dim3(256), 0, s, Fpart, F, nseg, nrows, S, ncomp, plane);
     return hipGetLastError();
 }
 

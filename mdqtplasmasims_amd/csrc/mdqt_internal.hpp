@@ -14,6 +14,13 @@ constexpr int NS = 12;          // numStates, SpeedUp:153
 constexpr int NBINS = 2001;     // SpeedUp:120-123
 constexpr int MAXSUB = 32;      // substeps fused into one launch (ratio = 25 at density 2)
 constexpr int NSTATIC = 20;     // static off-diagonal entries of M = I - i h H (App. A)
+// Gaussian KDE of the velocity distributions (SpeedUp:958-979; the tagging programs' QTT:1072):
+// exp(-V2 d^2), V2 = 1 / (2 0.002^2).  exp(x) is exactly +0 for x < -745.14 (below half the
+// smallest subnormal), so a term with |d| >= kKdeSkip (V2 d^2 >= 746.9) adds an exact zero and the
+// KDE kernels skip it; the assert ties the threshold to the bandwidth.
+constexpr double kKdeV2 = 1. / (2. * 0.002 * 0.002);
+constexpr double kKdeSkip = 0.0773;
+static_assert(kKdeV2 * kKdeSkip * kKdeSkip * (1. - 1e-12) >= 746.0, "KDE skip threshold must lie beyond exp's underflow");
 
 // Static couplings of the non-Hermitian Hamiltonian, as (row, col) of M; order of this
 // table is the index used by the kernels (SpeedUp:1206-1215, cs[] at :1163-1180).
@@ -330,6 +337,9 @@ struct N3BArgs {
     const double* Rs;   // [3][Npad] positions in sorted order
     const int* perm;    // sorted index -> ion
     const double* boxes;// [12][T]: tile center (x, y, z), half extents, raw coordinate min, max
+    double Rskip;       // force tile pairs whose boxes are >= Rskip apart are skipped (use_sort 1):
+                        // Rcut exactly (every skipped pair is beyond L/2), or the error-bounded tail
+                        // radius r_t < L/2 of mdqt_engine.cpp tail_radius (potentials: always Rcut)
 };
 struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]
@@ -426,12 +436,14 @@ hipError_t launch_d48_resolve(const D48Args& a, hipStream_t s);
 hipError_t launch_forces(const ForceArgs& a, hipStream_t s);
 hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEvent_t ev0 = nullptr,
                             hipEvent_t ev1 = nullptr);
-// Epotential on the Newton-3 tiles (world 1): pair potentials into slot component 0 of a.P
+// Epotential on the Newton-3 tiles (world 1): pair potentials into slot p of a.P, plane stride S
+// ([ntiles][S]: one component, a third of the force slots' memory)
 hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s);
 // Epotential on the Newton-3 blocks (world 1): per-ion row sums of u into out[S]
 hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
+// partial p of component c at Fpart + p * plane + c * S (plane 0: 3 S, the force layout)
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
-                                  hipStream_t s);
+                                  hipStream_t s, size_t plane = 0);
 hipError_t launch_potential_rows(const ForceArgs& a, hipStream_t s);   // Fpart[seg][0][i]
 // mode: 0 = auto (lane-per-state below kLaneKernelMaxIons ions, thread-per-ion above),
 //       1 = thread-per-ion, 2 = lane-per-state.  Both are bit-identical.
@@ -449,12 +461,28 @@ inline void launch_timed(F kernel, dim3 grid, dim3 block, hipStream_t s, hipEven
 }
 #endif
 
+// The substep kernel instance a launch ran (mdqt_get_const "qt_kernel"; the launchers report it
+// through `instance`): tests check which instance a configuration's production launch takes.
+enum QTKernel : int {
+    QTK_NONE = 0,
+    QTK_LANES_IM_EDZ = 1,      // k_substeps_lanes_im<true, true>: model 0 FAST + IM01 + EDZ (C2 production)
+    QTK_LANES_IM = 2,          // k_substeps_lanes_im<true, false>
+    QTK_LANES_R_FAST = 3,      // k_substeps_lanes_r<true, true>
+    QTK_LANES_R = 4,           // k_substeps_lanes_r<true, false>
+    QTK_LANES_R_PUMP_FAST = 5, // k_substeps_lanes_r<false, true>
+    QTK_LANES_R_PUMP = 6,      // k_substeps_lanes_r<false, false>
+    QTK_THREAD_R = 10,         // k_substeps_r<model>: 10 + model
+    QTK_MD_STEP = 20,          // k_md_step (one launch per MD step)
+    QTK_EXACT_LANES = 30,      // k_substeps_lanes<fast>: 30 + qt_math
+    QTK_EXACT_THREAD = 40,     // k_substeps<fast>: 40 + qt_math
+};
 // ev0/ev1 (optional): the kernel's own start/stop timestamps (hipExtLaunchKernelGGL)
 hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s,
-                           hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                           hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int* instance = nullptr);
 // qt_math 2: the reassociated kernels of mdqt_qtfast.hip (same modes as launch_substeps)
 hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s,
-                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);   // tab[0] by state, tab[1] by lane
+                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                             int* instance = nullptr);   // tab[0] by state, tab[1] by lane
 // one MD step in one launch: Newton-3 tile pairs + the FAST lane QT kernel (mdqt_qtfast.hip
 // k_md_step); f.arrive / a.arrive = the per-tile arrival counters, a.arrive_target their value
 // after this launch's tile pairs

@@ -578,9 +578,10 @@ __global__ __launch_bounds__(256) void k_substeps_lanes(SubstepArgs a, const Lan
 }
 
 hipError_t launch_substeps(const SubstepArgs& a, const LaneTab* tab, int mode, int fast, hipStream_t s,
-                           hipEvent_t ev0, hipEvent_t ev1) {
+                           hipEvent_t ev0, hipEvent_t ev1, int* instance) {
     if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
+    if (instance) *instance = (mode == 2 ? QTK_EXACT_LANES : QTK_EXACT_THREAD) + (fast ? 1 : 0);
     const dim3 gl((a.n + 15) / 16), gt((a.n + 255) / 256), b(256);
     if (fast) {
         if (mode == 2) launch_timed(k_substeps_lanes<true>, gl, b, s, ev0, ev1, a, tab);
@@ -692,7 +693,7 @@ __global__ __launch_bounds__(KT) void k_kde(const double* __restrict__ V, int n,
     const int j = blockIdx.x * KT + threadIdx.x;
     const int c = blockIdx.y;
     const int z = blockIdx.z;
-    const double V2 = 1. / (2. * 0.002 * 0.002);
+    const double V2 = kKdeV2;                                    // 1 / (2 * 0.002^2), :967
     const double b = (double)j * 0.0025;                         // vel[j], :340-344
     const double avg = (c == 0) ? vxAvg[0] : 0.;
     const int i0 = z * chunk, i1 = min(n, i0 + chunk);
@@ -711,7 +712,7 @@ __global__ __launch_bounds__(KT) void k_kde(const double* __restrict__ V, int n,
             // an ion whose two terms are 0 on every bin of the wave adds exact zeros there and is
             // skipped (a wave spans 0.16 of the 5.0 bin range, an ion's terms 2 x 0.155): the same
             // sums, ~15x fewer exp.  NaN velocities still take the exp path.
-            const bool near = !(fabs(b - v) >= 0.0773) || !(fabs(b + v) >= 0.0773);
+            const bool near = !(fabs(b - v) >= kKdeSkip) || !(fabs(b + v) >= kKdeSkip);
             if (!__builtin_amdgcn_ballot_w64(near)) continue;
             acc += exp(-V2 * (b - v) * (b - v)) + exp(-V2 * (b + v) * (b + v));
         }

@@ -192,7 +192,7 @@ __device__ __forceinline__ double n3_jsum(const double (*accj)[3][128], int k, i
 #endif
 template <bool SIG>
 __device__ __forceinline__ void slot_store(double* p, double v) {
-    if constexpr ((SIG && MDQT_EXPT_SIGMODE != 2) || MDQT_SLOT_WT)
+    if constexpr (MDQT_EXPT_SIGMODE != 2 && (SIG || MDQT_SLOT_WT))   // SIGMODE 2: plain stores
         __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
 }
@@ -249,7 +249,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     }
     ia[q][0][l] = fx; ia[q][1][l] = fy; ia[q][2][l] = fz;
     __syncthreads();
-    const size_t slab3 = (size_t)3 * S;
+    const size_t slab3 = POT ? (size_t)S : (size_t)3 * S;   // potential: [ntiles][S], one plane per slot
     constexpr int NK = POT ? 1 : 3;                 // potential: component 0 only, j side not negated
     if (q == 0) {                                   // rows of I -> slot J (diagonal: I)
         double* Pi = a.P + (size_t)J * slab3;
@@ -271,11 +271,15 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         }
     }
     if constexpr (SIG) {                            // every storing wave drained, then one arrival
+        // Release/acquire hand-off (the consumer polls with acquire, mdqt_qtfast.hip): the
+        // workgroup's slot stores happen-before its barrier, the barrier before thread 0's
+        // agent-scope release, so a consumer that acquires the count sees them.  On gfx950 the
+        // release is an L2 write-back — the price of these options (off by default, §8).
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (MDQT_EXPT_SIGMODE != 1 && threadIdx.x == 0) {   // one arrival per tile whose rows were written
-            __hip_atomic_fetch_add(a.arrive + I, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (J != I) __hip_atomic_fetch_add(a.arrive + J, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.arrive + I, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (J != I) __hip_atomic_fetch_add(a.arrive + J, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

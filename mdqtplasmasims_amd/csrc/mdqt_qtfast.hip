@@ -28,6 +28,15 @@ namespace mdqt {
 #endif
 constexpr int kLaneWG = MDQT_LANE_WG;
 static_assert(kLaneWG % 64 == 0 && kLaneWG <= 256, "lane kernel workgroup: whole waves, <= 256 threads");
+// ions per wave of the lane kernels (diagnostic A/B builds only: MDQT_EXPT_ROWS 1 or 2 leave rows
+// of 16 lanes idle — they shadow another row's ion without storing — so that a launch has 4 / 2x
+// the waves at the same instructions per wave; the product keeps 4)
+#ifndef MDQT_EXPT_ROWS
+#define MDQT_EXPT_ROWS 4
+#endif
+constexpr int kRows = MDQT_EXPT_ROWS;
+static_assert(kRows == 1 || kRows == 2 || kRows == 4, "ions per wave");
+constexpr int kLaneIons = kLaneWG / 64 * kRows;      // ions per workgroup
 
 __device__ __forceinline__ double rsq_nr(double x) { return rsq3(x); }   // 1/sqrt(x), mdqt_internal.hpp
 __device__ __forceinline__ double nrm2(cxd y) { return fma(y.re, y.re, y.im * y.im); }
@@ -408,8 +417,9 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     QT_STAMP(4, __builtin_amdgcn_s_memrealtime());
     const int k = threadIdx.x & 15;
     const int grp = threadIdx.x >> 4;
-    const int iraw = blk * (kLaneWG / 16) + grp;
-    const bool store = iraw < a.n;
+    const int iraw = kRows == 4 ? blk * (kLaneWG / 16) + grp
+                                : (blk * (kLaneWG / 64) + (grp >> 2)) * kRows + ((grp & 3) % kRows);
+    const bool store = iraw < a.n && (kRows == 4 || (grp & 3) < kRows);
     const int i = store ? iraw : a.n - 1;             // idle groups shadow the last ion
     const QTConst& qc = a.qc;
     const int S = a.S;
@@ -514,24 +524,26 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         if (threadIdx.x == 0) {
             int it = 0;
             const unsigned long long* cnt = a.arrive + (blk * (kLaneWG / 16)) / 64;   // the ions' tile
-            while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
+            while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
                 for (int z = 0; z < a.arrive_sleep; ++z) __builtin_amdgcn_s_sleep(1);
                 if (++it > (1 << 21)) { *a.spin_err = 1; break; }   // bounded: never hang the GPU
             }
         }
-        __syncthreads();
+        __syncthreads();                              // thread 0's acquire, then the workgroup's loads
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);       // (workgroup fence: no early slot load)
         if (nseg > 1) slot_partials(true);
     }
     if (FUSED) {                                      // this launch's tile pairs of the ions' tile
         if (threadIdx.x == 0) {
             const unsigned long long* cnt = a.arrive + (blk * (kLaneWG / 16)) / 64;
             int it = 0;
-            while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
+            while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < a.arrive_target) {
                 __builtin_amdgcn_s_sleep(2);
                 if (++it > (1 << 22)) { *a.spin_err = 1; break; }   // bounded: never hang the GPU
             }
         }
         __syncthreads();
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
 #if defined(MDQT_EXPT_MDSTAMPS)
         if (threadIdx.x == 0 && blockIdx.x < 4096) g_md_stamps[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -590,6 +602,9 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         double u = EDZ ? v * qc.pv2q : v * qc.pv2q + edt[0];   // vx on every state lane (carried: the
         double tn = tPart + qc.dtQ;                   // next substep's is formed with its phase); tn:
         sincos_q<true>((u * cphi) * tn, sn, cs);      // the next substep's tPart, formed once
+#if defined(MDQT_EXPT_PHASEROT)
+        double phi_c = (u * cphi) * tn;
+#endif
 #ifndef MDQT_QT_UNROLL
 #define MDQT_QT_UNROLL 2
 #endif
@@ -630,7 +645,21 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                 un = EDZ ? vn * qc.pv2q : vn * qc.pv2q + edt[s1];
                 tn = tPart + qc.dtQ;
                 phin = (un * cphi) * tn;
+#if defined(MDQT_EXPT_PHASEROT)
+                {   // timing-only diagnostic: e^(i phin) = e^(i phi) e^(i dphi), short Taylor series of
+                    // dphi without range reduction (wrong for large dphi and after a jump: NOT a product form)
+                    const double dph = phin - phi_c, z = dph * dph;
+                    const double sd = dph * fma(z, fma(z, fma(z, -1.984126984126984e-04, 8.333333333333333e-03),
+                                                       -1.666666666666667e-01), 1.0);
+                    const double cd = fma(z, fma(z, fma(z, fma(z, 2.48015873015873e-05, -1.388888888888889e-03),
+                                                        4.166666666666666e-02), -0.5), 1.0);
+                    snn = fma(sn, cd, cs * sd);
+                    csn = fma(cs, cd, -(sn * sd));
+                    phi_c = phin;
+                }
+#else
                 sincos_fast(phin, snn, csn);
+#endif
             };
             if (nojump) {
                 {                                 // kick terms on the P lanes (host table)
@@ -797,7 +826,7 @@ __global__ __launch_bounds__(256) void k_md_step(N3Args f, SubstepArgs a, const 
 
 hipError_t launch_md_step(const N3Args& f, const SubstepArgs& a, const FastTab* tab, int variant, hipStream_t s,
                           hipEvent_t ev0, hipEvent_t ev1) {
-    if (a.n <= 0 || f.npairs <= 0 || a.nsub <= 0 || a.nsub > MAXSUB || !a.arrive || !f.arrive || f.guard)
+    if (a.n <= 0 || f.npairs <= 0 || a.nsub <= 0 || a.nsub > MAXSUB || !a.arrive || !f.arrive || f.guard || kRows != 4)
         return hipErrorInvalidValue;
     if (a.qc.model < 0 || a.qc.model >= NMODELS || variant < 0 || variant > 1) return hipErrorInvalidValue;
     const dim3 gl(f.npairs + (a.n + kLaneWG / 16 - 1) / (kLaneWG / 16)), bl(kLaneWG);
@@ -819,12 +848,13 @@ extern "C" int mdqt_expt_qt_stamps(unsigned long long* out, int nwaves) {
 #endif
 
 hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode, hipStream_t s, hipEvent_t ev0,
-                             hipEvent_t ev1) {
+                             hipEvent_t ev1, int* instance) {
     if (a.n <= 0 || a.nsub <= 0) return hipSuccess;
     if (a.nsub > MAXSUB) return hipErrorInvalidValue;
     if (mode == 0) mode = (a.n < kLaneKernelMaxIons) ? 2 : 1;
     if (a.qc.model < 0 || a.qc.model >= NMODELS) return hipErrorInvalidValue;
-    const dim3 gl((a.n + kLaneWG / 16 - 1) / (kLaneWG / 16)), bl(kLaneWG), gt((a.n + 255) / 256), b(256);
+    const dim3 gl((a.n + kLaneIons - 1) / kLaneIons), bl(kLaneWG), gt((a.n + 255) / 256), b(256);
+    int inst = QTK_THREAD_R + a.qc.model;
     if (mode == 2) {
         const uint64_t all = (1ull << a.nsub) - 1;
         const bool allmove = a.do_step && a.do_qt && a.nseg >= 1 && !a.arrive && (a.movmask & all) == all;
@@ -836,20 +866,35 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
 #endif
         if (a.qc.model == 0) {
             if (allmove && a.qc.im01 && MDQT_IM01) {
-                if (a.expdet_zero && MDQT_EDZ) launch_timed(k_substeps_lanes_im<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
-                else launch_timed(k_substeps_lanes_im<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+                if (a.expdet_zero && MDQT_EDZ) {
+                    launch_timed(k_substeps_lanes_im<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+                    inst = QTK_LANES_IM_EDZ;
+                } else {
+                    launch_timed(k_substeps_lanes_im<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+                    inst = QTK_LANES_IM;
+                }
+            } else if (allmove) {
+                launch_timed(k_substeps_lanes_r<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+                inst = QTK_LANES_R_FAST;
+            } else {
+                launch_timed(k_substeps_lanes_r<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+                inst = QTK_LANES_R;
             }
-            else if (allmove) launch_timed(k_substeps_lanes_r<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
-            else launch_timed(k_substeps_lanes_r<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
         } else {
-            if (allmove) launch_timed(k_substeps_lanes_r<false, true>, gl, bl, s, ev0, ev1, a, tab + 1);
-            else launch_timed(k_substeps_lanes_r<false, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+            if (allmove) {
+                launch_timed(k_substeps_lanes_r<false, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+                inst = QTK_LANES_R_PUMP_FAST;
+            } else {
+                launch_timed(k_substeps_lanes_r<false, false>, gl, bl, s, ev0, ev1, a, tab + 1);
+                inst = QTK_LANES_R_PUMP;
+            }
         }
     }
     else if (a.qc.model == 0) launch_timed(k_substeps_r<0>, gt, b, s, ev0, ev1, a, tab);
     else if (a.qc.model == 1) launch_timed(k_substeps_r<1>, gt, b, s, ev0, ev1, a, tab);
     else if (a.qc.model == 2) launch_timed(k_substeps_r<2>, gt, b, s, ev0, ev1, a, tab);
     else launch_timed(k_substeps_r<3>, gt, b, s, ev0, ev1, a, tab);
+    if (instance) *instance = inst;
     return hipGetLastError();
 }
 

@@ -315,6 +315,12 @@ class Simulation:
     def comm_init(self, uid: bytes):
         check(lib().mdqt_comm_init(self.h, uid, len(uid)), "comm_init")
 
+    def comm_size(self) -> int:
+        """ranks of this context's communicator (ncclCommCount; 1 without one)"""
+        n = C.c_int(0)
+        check(lib().mdqt_comm_size(self.h, C.byref(n)), "comm_size")
+        return n.value
+
     def enable_timing(self, period: int = 1, kinds: int = 3, offset: int | None = None):
         """bracket every `period`-th hot-kernel launch with HIP events (0/False: off); kinds:
         bit 0 force launches, bit 1 fused-substep launches; offset: which launch of each period

@@ -4,6 +4,7 @@ the oracle on sampled ions (the full O(N^2) oracle is hours at N = 1e6).
   C3  N0 = 100,000  MD-only, Ge = 1/12 (kappa = 0.5)      Newton-3 block pairs, one GPU
   C4  N0 = 1,000,000 MD-only, Ge = 1/12                  Newton-3 block pairs, one GPU (~12 GB of slots)
   C5  N0 = 250,000  full MDQT, detuningDP = +1           Newton-3 block pairs + one fused 25-substep launch
+  1M  N0 = 1,000,000 full MDQT (C2's laser parameters)   north_star's second size: QT on at N = 1e6
 
 Per config:
   * forces() on the reference's init() state (C5: after 20 MD steps, so that the interval below
@@ -31,6 +32,7 @@ CONFIGS = {
     "C3": dict(N0=100000, Ge=1.0 / 12, qt_enabled=0),
     "C5": dict(N0=250000, detuningDP=1.0, qt_enabled=1),
     "C4": dict(N0=1000000, Ge=1.0 / 12, qt_enabled=0),
+    "1M": dict(N0=1000000, qt_enabled=1),
 }
 SEED = 12346
 
@@ -66,7 +68,7 @@ def test_forces_index_matches_full_rows(orc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["C3", "C5", "C4"])
+@pytest.mark.parametrize("cfg", ["C3", "C5", "C4", "1M"])
 def test_large_config_forces_and_interval(cfg, orc):
     import mdqtplasmasims_amd as M
     if M.device_count() < 1:
@@ -75,7 +77,7 @@ def test_large_config_forces_and_interval(cfg, orc):
     qt = kw["qt_enabled"]
     s = M.Simulation(seed=SEED, job=1, rng_mode=1, **kw).init()
     if qt:
-        s.md_steps(20)                                  # P populations build up: quantum jumps occur
+        s.md_steps(20 if cfg != "1M" else 8)            # P populations build up: quantum jumps occur
     N = s.N
     assert s.const("force_scheme") == 3                 # Newton-3 block pairs above 65,536 ions
     L, lDeb = s.const("L"), s.const("lDeb")
@@ -85,9 +87,15 @@ def test_large_config_forces_and_interval(cfg, orc):
     rng = np.random.default_rng(11)
     idx = sample_ions(N, 1024 if N < 500000 else 640, rng)
     G = orc.forces_index(R, idx, L, lDeb, nthreads=threads())
-    err = np.abs(F[:, idx] - G).max() / np.abs(G).max()
-    print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}")
+    dabs = np.abs(F[:, idx] - G).max()
+    err = dabs / np.abs(G).max()
+    # the error-bounded tail (force_tail_exp, default 12): tile pairs >= r_t apart are skipped, every
+    # ion's force moves by at most `bound` (mdqt_engine.cpp tail_radius; 0 where r_t = L/2)
+    rt, bound = s.const("force_skip_radius"), s.const("force_tail_bound")
+    print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}, "
+          f"max|dF| = {dabs:.3e}; skip radius {rt:.3f} (L/2 {L / 2:.3f}), tail bound {bound:.2e}")
     assert err <= 1e-12
+    assert dabs <= bound + 1e-13 * np.abs(G).max()
     mom = np.abs(F.sum(axis=1)).max() / (np.abs(F).sum() / N)
     print(f"{cfg}: |sum F| / mean|F| = {mom:.3e}")
     assert mom <= 1e-9
@@ -139,6 +147,44 @@ def test_spatial_order_tile_skipping_is_exact(orc):
     print(f"C3 sorted vs unsorted: max|dF|/max|F| = {err:.3e}")
     assert err <= 1e-13
     s.close()
+
+
+@pytest.mark.gpu
+def test_error_bounded_tail_at_1m():
+    """N = 1e6 (C4): the error-bounded skip radius r_t < L/2 (force_tail_exp 12) against the exact
+    L/2 skipping (force_tail_exp 0) on EVERY ion: |dF_i| <= (N - 1) g(r_t) <= 1e-12, the rigorous
+    bound the host computes (mdqt_engine.cpp tail_radius), plus the summation-order rounding;
+    a no-op at C3 and C5, where r_t would exceed L/2"""
+    import mdqtplasmasims_amd as M
+    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C4"]).init()
+    L = s.const("L")
+    rt, bound = s.const("force_skip_radius"), s.const("force_tail_bound")
+    assert 0 < bound <= 1e-12 and rt < L / 2
+    s.forces()
+    Ft = s.get_state()["F"]
+    s.set_option("force_tail_exp", 0)
+    assert s.const("force_skip_radius") == L / 2 and s.const("force_tail_bound") == 0
+    s.forces()
+    Fe = s.get_state()["F"]
+    d = np.abs(Ft - Fe).max()
+    print(f"C4 N={s.N}: r_t = {rt:.3f} (L/2 = {L / 2:.3f}), bound {bound:.2e}, max_i |dF_i| = {d:.3e}, "
+          f"max|F| = {np.abs(Fe).max():.3e}")
+    assert d <= bound + 1e-13 * np.abs(Fe).max()
+    s.close()
+    for cfg in ("C3", "C5"):                          # r_t >= L/2: exact skipping only
+        x = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg])
+        x.set_state(*_tiny_state(x))
+        assert x.const("force_tail_bound") == 0 and x.const("force_skip_radius") == x.const("L") / 2
+        x.close()
+
+
+def _tiny_state(x):
+    """a state of N = N0 ions (uniform positions) without init()'s sampling, for constant checks"""
+    N = int(x.params.N0)
+    rng = np.random.default_rng(0)
+    L = x.const("L")
+    psi = np.zeros((N, 12, 2)); psi[:, 0, 0] = 1.0
+    return rng.uniform(0, L, (3, N)), np.zeros((3, N)), psi, np.zeros(N), 0.0
 
 
 @pytest.mark.gpu

@@ -265,6 +265,70 @@ def test_md_steps_short_horizon(eng, orc, qt, qt_math):
         assert np.array_equal(a["tPart"] == 0, b["tPart"] == 0)
 
 
+QTK_LANES_IM_EDZ = 1         # mdqt_internal.hpp QTKernel: k_substeps_lanes_im<true, true>
+
+
+def test_c2_headline_qt_instance_matches_oracle(eng, orc):
+    """BASELINE configs[1] (C2) exactly as bench.py runs it — N0 = 3500, seed 12346, job 1,
+    Philox (rng_mode 1), every option at its default — against the oracle over 3 MD steps with
+    quantum jumps.  The production launch must be the one the headline number times:
+    k_substeps_lanes_im<true, true> (FAST + IM01 + EDZ) summing all 56 Newton-3 tile slots in its
+    lane-distributed prologue (lane k: slots k, k + 16, k + 32, k + 48 — all 16 lanes busy only
+    at >= 49 slots), so a slot-sum bug shared with the thread-per-ion kernel cannot hide behind
+    a self-comparison.  SpeedUp:438-717 (qstep), :1369-1377 (the MD step's cadence)."""
+    kw = dict(N0=3500, seed=12346, job=1, rng_mode=1)
+    s = eng.Simulation(**kw).init()
+    o = orc.OracleSim(nthreads=8, **kw).init()
+    assert s.N == o.N == 3573
+    s.md_steps(1); o.md_steps(1)            # t = 0 interval: the general instance (non-moving drift)
+    assert s.const("qt_kernel") != QTK_LANES_IM_EDZ
+    s.md_steps(2); o.md_steps(2)
+    assert s.const("force_scheme") == 2 and s.const("force_slots") == 56
+    assert s.const("qt_kernel") == QTK_LANES_IM_EDZ, s.const("qt_kernel")
+    assert s.const("qt_kernel_nseg") == 56
+    a, b = s.get_state(), o.get_state()
+    assert a["t"] == b["t"] and s.qstep_index == o.qstep_index == 75
+    jumped_a = a["tPart"] < 3 * 25 * 8e-5 - 1e-12
+    jumped_b = b["tPart"] < 3 * 25 * 8e-5 - 1e-12
+    assert jumped_b.sum() > 50                       # the jump branch ran in every launch
+    assert np.array_equal(jumped_a, jumped_b)
+    assert np.array_equal(a["tPart"] == 0, b["tPart"] == 0)
+    dR, dV = np.abs(a["R"] - b["R"]).max(), np.abs(a["V"] - b["V"]).max()
+    dpsi = np.abs(a["psi"] - b["psi"]).max()
+    dF = rel(a["F"], b["F"])
+    print(f"C2 headline instance: N={s.N} jumps={int(jumped_b.sum())} |dR|={dR:.2e} |dV|={dV:.2e} "
+          f"|dpsi|={dpsi:.2e} F rel={dF:.2e}")
+    assert dR <= 1e-10 and dV <= 1e-10
+    assert dpsi <= 1e-9
+    assert dF <= 1e-12
+    s.close()
+
+
+@pytest.mark.parametrize("N0", [30, 45])
+def test_newton3_tiles_single_slot(eng, N0):
+    """force_scheme 2 with one tile (N <= 64): the kernel writes F itself (no pending slot), so
+    every substep instance — including the production FAST launch, which takes nseg == 1 as
+    'F already summed' — integrates with this step's forces: equal to the rows scheme (one
+    segment: ascending j) up to summation order"""
+    out = []
+    for scheme in (1, 2):
+        s = eng.Simulation(N0=N0, seed=3).init()
+        s.set_option("force_scheme", scheme)
+        assert s.const("force_scheme") == scheme
+        if scheme == 2:
+            assert s.N <= 64 and s.const("force_slots") == 1
+        s.md_steps(4)
+        s.synchronize()
+        if scheme == 2:
+            assert s.const("qt_kernel") == QTK_LANES_IM_EDZ
+        out.append(s.get_state())
+        s.close()
+    a, b = out
+    assert rel(a["F"], b["F"]) < 1e-13
+    assert np.abs(a["V"] - b["V"]).max() < 1e-11
+    assert np.abs(a["R"] - b["R"]).max() < 1e-11
+
+
 PUMP = [(1, dict(Om=0.7, detuning=-2.5)), (2, dict(Om=2.0, detuning=0.0)), (3, dict(Om=1.3, detuning=-1.0))]
 
 

@@ -89,24 +89,62 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "r02g_c2_pmc.json")):
-    """HBM bytes per launch of the kernel from the committed rocprofv3 --pmc summary of the same
-    C2 workload (FETCH_SIZE and WRITE_SIZE in separate passes, kB -> B; no gfx950 x2 read
-    correction: the kernel's loads are 8 B/lane, outside the guide's calibrated 16 B/lane case).
-    The production instance (the most dispatched one of the kernel family) is taken; returns
-    (bytes, instance name) or (None, None)."""
+def kernel_source_hash():
+    """sha256 (16 hex) of the kernel sources (mdqtplasmasims_amd/csrc: .hip .hpp .cpp Makefile): a PMC
+    summary records the hash of the tree it was measured on, and the bench uses its counters only when
+    the hash matches its own tree — a kernel change makes the committed traffic figure stale, and the
+    line then says so instead of quoting it"""
+    import hashlib
+    d = os.path.join(ROOT, "mdqtplasmasims_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".hpp", ".cpp")) or f == "Makefile":
+            h.update(f.encode())
+            with open(os.path.join(d, f), "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def latest_pmc_file():
+    """the newest committed C2 PMC summary (profiles/r<round><letter>_c2_pmc.json)"""
+    d = os.path.join(ROOT, "profiles")
+    fs = sorted(f for f in os.listdir(d) if f.endswith("_c2_pmc.json") and f.startswith("r"))
+    return os.path.join(d, fs[-1]) if fs else None
+
+
+def pmc_traffic(kernel_prefix, path=None):
+    """HBM-side bytes per launch of the kernel (FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc
+    passes of the same C2 workload, kB -> B) from the newest committed PMC summary, corrected by the
+    calibration factors that summary carries (tools/fetch_calib.hip: FETCH_SIZE / known bytes of the
+    kernel's own access pattern).  The production instance (the most dispatched one of the kernel
+    family) is taken.  Returns (bytes or None, source dict): None when the summary was measured on
+    other kernel sources than this tree's (its src_hash), or has no such kernel."""
+    path = path or latest_pmc_file()
+    src = {"file": os.path.relpath(path, ROOT) if path else None, "src_hash": kernel_source_hash()}
     try:
         with open(path) as f:
             d = json.load(f)
-    except OSError:
-        return None, None
+    except (OSError, TypeError):
+        return None, dict(src, status="no PMC summary")
+    meta = d.get("_meta", {})
+    src["measured_src_hash"] = meta.get("src_hash")
+    if meta.get("src_hash") != src["src_hash"]:
+        return None, dict(src, status="stale: measured on other kernel sources")
     best, name = None, None
     for k, v in d.items():
+        if k == "_meta":
+            continue
         short = k.split("(")[0].replace("void ", "").replace("mdqt::", "")
         if short.startswith(kernel_prefix) and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             if best is None or v.get("dispatches", 0) > best.get("dispatches", 0):
                 best, name = v, short
-    return (None, None) if best is None else ((best["FETCH_SIZE"] + best["WRITE_SIZE"]) * 1024.0, name)
+    if best is None:
+        return None, dict(src, status="kernel not in the summary")
+    cf = meta.get("fetch_factor", 1.0)            # FETCH_SIZE / true bytes for this access pattern
+    cw = meta.get("write_factor", 1.0)
+    src.update(status="ok", instance=name, fetch_kB=best["FETCH_SIZE"], write_kB=best["WRITE_SIZE"],
+               fetch_factor=cf, write_factor=cw)
+    return (best["FETCH_SIZE"] / cf + best["WRITE_SIZE"] / cw) * 1024.0, src
 
 
 def cpu_threads():
@@ -356,11 +394,12 @@ def main():
             ach = bytes_launch / s_avg / 1e9
             flops = F_Q_PER_QSTEP * N * nsub_per_launch
             kname = "k_substeps_lanes" if N < 98304 else "k_substeps_r"
-            traffic, kinst = pmc_traffic(kname)
+            traffic, tsrc = pmc_traffic(kname)
+            kinst = tsrc.get("instance")
             # The fused QT launch is bound by neither roof: one wave per SIMD runs a dependent chain of
             # ~330 VALU instructions per substep — "latency", with both fractions given.
             roof = {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                    "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                     "kernel": f"{kinst or kname} (fused {nsub_per_launch:g} x step+qstep)",
                     "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
                     "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS,
@@ -704,6 +743,8 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el = float(tt[0])
     N = sim.N
+    L = sim.const("L")
+    rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
     sim.close()
     unit_steps = ratio if qt else 1
     f_avg = f_ms / max(nf, 1) * 1e-3
@@ -718,6 +759,10 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force,
+            "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail,
+                           "note": "tile pairs >= skip_radius apart are skipped; every ion's force is within "
+                                   "`bound` of the exact sum to L/2 ((N-1) g(r_t), mdqt_engine.cpp tail_radius; "
+                                   "0 = exact). fp64 rates count all N(N-1)/2 pairs (SURVEY 8d)"},
             "substeps_ms_per_md_step": s_ms / max(ns, 1) if ns else None}
 
 

@@ -8,8 +8,12 @@ averaged over the dispatches of each kernel.  Prints JSON {kernel: {counter: mea
 """
 import collections
 import json
+import os
 import sqlite3
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def load(db):
@@ -20,12 +24,21 @@ def load(db):
     return per
 
 
-def main(dbs):
+def main(args):
+    """args: the rocpd databases, then optionally --factors FETCH_FACTOR WRITE_FACTOR (the
+    calibration of tools/fetch_calib.hip for the kernel's access pattern)"""
+    from bench import kernel_source_hash
+    meta = {"src_hash": kernel_source_hash()}
+    dbs = list(args)
+    if "--factors" in dbs:
+        k = dbs.index("--factors")
+        meta["fetch_factor"], meta["write_factor"] = float(dbs[k + 1]), float(dbs[k + 2])
+        dbs = dbs[:k] + dbs[k + 3:]
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for db in dbs:
         for (k, d, n), v in load(db).items():
             agg[k][n].append(v)
-    out = {}
+    out = {"_meta": meta}
     for k, cs in agg.items():
         out[k] = {n: sum(v) / len(v) for n, v in cs.items()}
         out[k]["dispatches"] = max(len(v) for v in cs.values())

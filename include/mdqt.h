@@ -91,7 +91,12 @@ const char* mdqt_last_error(void);                           /* thread-local mes
 int         mdqt_device_count(void);                         /* HIP devices visible             */
 const char* mdqt_version(void);
 
-/* ---- derived constants (SpeedUp:79-85, :146-149, :295-297, :1181-1215) ---- */
+/* ---- derived constants (SpeedUp:79-85, :146-149, :295-297, :1181-1215) ----
+ * plus the engine's state: "force_scheme", "force_slots", "force_sort", "force_skip_radius",
+ * "force_tail_bound", "force_far_radius", "force_far_bound" (see the tuning knobs), "qt_kernel" /
+ * "qt_kernel_nseg" (the substep kernel instance of the last launch and the force partials it
+ * summed; codes of mdqt_internal.hpp QTKernel: 1 = the C2 production instance), "md_step_fused";
+ * NaN for an unknown name */
 double      mdqt_get_const(const mdqt_ctx* c, const char* name);
 
 /* ---- state ---- */
@@ -178,6 +183,17 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *   "force_sort":     block pairs only: 1 = Hilbert-curve order with exact skipping of tile
  *                     pairs >= L/2 apart (default), 2 = the same order, nothing skipped (bit-
  *                     identical to 1), 0 = storage order
+ *   "force_tail_exp": block pairs in spatial order: tile pairs whose boxes are >= r_t apart are
+ *                     skipped, r_t the smallest radius with (N - 1) g(r_t) <= 10^-k (g(r) one
+ *                     pair's |F| at distance r, SpeedUp:224): every ion's force within 10^-k of
+ *                     the exact sum to L/2; k = 12 default, 0 = exact (r_t = L/2); a no-op where
+ *                     r_t >= L/2 (every BASELINE size but N ~ 1e6).  mdqt_get_const
+ *                     "force_skip_radius" / "force_tail_bound" report r_t and (N - 1) g(r_t)
+ *   "force_far_exp":  block pairs in spatial order: tile pairs >= r_far apart evaluate their pairs
+ *                     within 3e-9 relative (rsq + one Newton step, degree-6 2^f), r_far the
+ *                     smallest radius with (N - 1) g(r_far) 3e-9 <= 10^-k: every ion's force
+ *                     within 10^-k more; k = 13 default, 0 = off.  "force_far_radius" /
+ *                     "force_far_bound" report r_far and the bound
  *   "qt_enabled":     1 = qstep() runs in the substeps, 0 = skipped (t still advances): the
  *                     pumping programs' pump window (randomFrozenStartTag408Linear.cpp main)
  *   "qt_math":        0 = the reference's exact operations, 1 = FMA-contracted with a refined

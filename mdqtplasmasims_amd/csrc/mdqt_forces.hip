@@ -190,28 +190,41 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
 }
 
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
-          bool POT = false>
+          bool POT = false, bool FAR = false>
 __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi, double zi, double mi,
                                          const double (*pj)[128], const double* mj, double* ax, double* ay,
                                          double* az, double& fx, double& fy, double& fz, const PairC& c,
                                          const double* nsh = nullptr) {
+    // every 16 steps the LDS arrays are re-based at the lane's index (an opaque register), so the
+    // 16 unrolled steps address them with immediate offsets t, 128 + t, 256 + t: without it the
+    // compiler's strength reduction moved the base past the arrays and spent a v_add_u32 per
+    // ds_add_f64 (3.5 VALU per pair, ~8 % of the block kernel's instructions)
+#define N3B_REBASE(b0)                                                                     \
+    int b_ = (b0);                                                                         \
+    asm volatile("" : "+v"(b_));                                                           \
+    const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);                    \
+    const double* mjb = mj + b_;                                                           \
+    double *axb = ax + b_, *ayb = ay + b_, *azb = az + b_
     if (!diag) {
         for (int t0 = 0; t0 < 64; t0 += 16) {
+            N3B_REBASE(l + t0);
 #pragma unroll
             for (int t = 0; t < 16; ++t)
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT>(l + t0 + t, 1., xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
-                                                       c, nsh);
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, 1., xi, yi, zi, mi, pjb, mjb, axb, ayb, azb,
+                                                                      fx, fy, fz, c, nsh);
         }
     } else {
         for (int t0 = 1; t0 < 33; t0 += 16) {
+            N3B_REBASE(l + t0);
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 const double m = (t0 + t == 32 && l >= 32) ? 0. : 1.;   // lane distance 32: once
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT>(l + t0 + t, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz,
-                                                       c, nsh);
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, m, xi, yi, zi, mi, pjb, mjb, axb, ayb, azb,
+                                                                      fx, fy, fz, c, nsh);
             }
         }
     }
+#undef N3B_REBASE
 }
 
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
@@ -252,9 +265,11 @@ void k_pairs_n3b(N3BArgs a) {
     //    of the two ends; equal ends = one minimum-image multiple per axis for every pair, bit for
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
-    __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class (-1 skip, 1 uniform, 0 per pair)
+    // class: -1 skip; otherwise bit 0 = uniform image, bit 1 = far (the far pair form, forces only)
+    __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class
     // skip below the cutoff only for the forces (error-bounded tail, mdqt_engine.cpp tail_radius)
     const double rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
+    const double rf2 = (POT || VARIANT != 1 || !(a.Rfar < a.Rcut)) ? INFINITY : a.Rfar * a.Rfar;
     auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
         const double* B = a.boxes;
         double g2 = 0.;
@@ -272,7 +287,8 @@ void k_pairs_n3b(N3BArgs a) {
             uni = uni && (nlo == nhi);
             n[c3] = nlo;
         }
-        const double cls = (a.use_sort == 1 && g2 > rc2) ? -1. : (VARIANT == 1 && uni) ? 1. : 0.;
+        const double cls = (a.use_sort == 1 && g2 > rc2) ? -1.
+                                                          : ((VARIANT == 1 && uni) ? 1. : 0.) + (g2 > rf2 ? 2. : 0.);
         return make_double4(n[0], n[1], n[2], cls);
     };
     // the run's i accumulator lives in LDS (read and written once per block distance) so that
@@ -322,15 +338,30 @@ void k_pairs_n3b(N3BArgs a) {
                 if (ragN && (I == T - 1 || J == T - 1))
                     n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
                                                                     tz, c);
-                else if (VARIANT == 1 && cls > 0.) {
+                else if (VARIANT == 1 && (cls == 1. || cls == 3.)) {
                     const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
-                    if (MDQT_SHIFT_I)                   // xi - n L once per tile pair (n3_step SHIFT)
-                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(
-                            diag, l, fma(-nsh[0], a.L, xi), fma(-nsh[1], a.L, yi), fma(-nsh[2], a.L, zi), mi, pj, mj,
-                            ax, ay, az, tx, ty, tz, c, nsh);
-                    else
-                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax,
+                    // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
+                    const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
+                    const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
+                    const double sz = MDQT_SHIFT_I ? fma(-nsh[2], a.L, zi) : zi;
+                    if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
+                        if (cls == 3.)              // far tile pair: the far pair form
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, true>(diag, l, sx, sy, sz, mi, pj, mj, ax,
+                                                                                  ay, az, tx, ty, tz, c, nsh);
+                        else
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
+                                                                            az, tx, ty, tz, c, nsh);
+                    } else {
+                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, l, sx, sy, sz, mi, pj, mj, ax,
                                                                                 ay, az, tx, ty, tz, c, nsh);
+                    }
+                } else if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
+                    if (cls == 2.)
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, true>(diag, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                               ay, az, tx, ty, tz, c);
+                    else
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az,
+                                                                         tx, ty, tz, c);
                 } else
                     n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx,
                                                                      ty, tz, c);

@@ -244,6 +244,35 @@ __device__ __forceinline__ double exp2_neg(double t) {
     return ldexp(p, (int)n);
 }
 constexpr double kNegLog2e = -1.4426950408889634;   // -log2(e)
+
+// Far tile pairs of the Newton-3 blocks (box gap >= the far radius, mdqt_engine.cpp far_radius):
+// every pair term there is below g(r_far), so a term error of relative size kFarRelErr is below
+// g(r_far) kFarRelErr and an ion's force moves by at most (N - 1) g(r_far) kFarRelErr (<= 1e-13 by
+// the choice of r_far).  Their pair form: rsq1 (v_rsq_f64 + ONE Newton step: 1e-14 relative) and
+// 2^f by a degree-6 Chebyshev fit on [-1/2, 1/2] (2.6e-9 relative in double Horner, mpmath fit,
+// measured on 4,001 points) — 6 operations fewer per pair than the exact form.
+constexpr double kFarRelErr = 3e-9;
+__device__ __forceinline__ double rsq1(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double q = __builtin_amdgcn_rsq(x);
+#else
+    const double q = 1. / sqrt(x);
+#endif
+    const double e = fma(-x, q * q, 1.0);
+    return fma(0.5 * q, e, q);
+}
+__device__ __forceinline__ double exp2_neg_cut6(double t, bool keep) {
+    const double n = __builtin_rint(t);
+    const double f = t - n;
+    double p = 0x1.443fffc90db59p-13;
+    p = fma(p, f, 0x1.5f48c04f62e50p-10);
+    p = fma(p, f, 0x1.3b2a1b7152befp-7);
+    p = fma(p, f, 0x1.c6aecc669b6ddp-5);
+    p = fma(p, f, 0x1.ebfbe045f4d3cp-3);
+    p = fma(p, f, 0x1.62e430d034702p-1);
+    p = fma(p, f, 1.0);
+    return ldexp(p, keep ? (int)n : -1100);
+}
 // exp2_neg with a cutoff folded into the exponent shift: 0 (2^-1100 underflows) unless keep —
 // one 32-bit select instead of a 64-bit one on the result.  For finite t only (the caller's
 // r = 0 case must not occur: the Newton-3 tile kernels have no self pairs, distinct pad ions).
@@ -337,6 +366,8 @@ struct N3BArgs {
     const double* Rs;   // [3][Npad] positions in sorted order
     const int* perm;    // sorted index -> ion
     const double* boxes;// [12][T]: tile center (x, y, z), half extents, raw coordinate min, max
+    double Rfar;        // tile pairs whose boxes are >= Rfar apart take the far pair form (kFarRelErr;
+                        // forces only, use_sort 1 or 2); >= Rcut: never
     double Rskip;       // force tile pairs whose boxes are >= Rskip apart are skipped (use_sort 1):
                         // Rcut exactly (every skipped pair is beyond L/2), or the error-bounded tail
                         // radius r_t < L/2 of mdqt_engine.cpp tail_radius (potentials: always Rcut)

@@ -97,6 +97,14 @@ __device__ __forceinline__ double pair_ft_cut(double dx, double dy, double dz, c
     return ((ri + c.invlDeb) * exp2_neg_cut(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
 }
 
+// pair_ft_cut of a far tile pair (Newton-3 blocks): rsq1 and the degree-6 2^f, within kFarRelErr
+__device__ __forceinline__ double pair_ft_cut_far(double dx, double dy, double dz, const PairC& c) {
+    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+    const double ri = rsq1(r2);
+    const double dr = r2 * ri;
+    return ((ri + c.invlDeb) * exp2_neg_cut6(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
+}
+
 template <int VARIANT>
 __device__ __forceinline__ void accum(double& f, double d, double ft) {
     if (VARIANT == 0) f += d * ft;        // the reference's F[i] += dx*ftotal (:225-230)
@@ -126,7 +134,8 @@ __device__ __forceinline__ void accum(double& f, double d, double ft) {
 #endif
 // POT: Epotential's pair potential u (pair_u) instead of the force: u to the i accumulator fx and
 // to the j accumulator ax only (both sides of a pair get +u)
-template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false>
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
+          bool FAR = false>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
@@ -150,7 +159,8 @@ __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi,
         (void)ay; (void)az; (void)fy; (void)fz;
         return;
     }
-    double ft = CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
+    static_assert(!FAR || (CUT && !POT), "the far pair form is the fast force variant's");
+    double ft = FAR ? pair_ft_cut_far(dx, dy, dz, c) : CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];
     ft *= m;
     const double px = dx * ft, py = dy * ft, pz = dz * ft;

@@ -107,18 +107,12 @@ __device__ __forceinline__ double lane_sum_p(double T) {
 __device__ __forceinline__ double half_drift(double p, double v, double f, bool moving, double DT,
                                              double DT2, double L) {
     p = moving ? p + DT * v : p + (DT * v + DT2 * f);
-    // if (p < 0) p += L; if (p > L) p -= L; — at most one applies (p < 0 gives p + L <= L), so
-    // p + m L with m = +1, -1 or 0 as ONE fma: fma(+-1, L, p) rounds p +- L exactly like the add,
-    // fma(0, L, p) = p (p is never -0: positions start in (0, L]); 2 compares, 2 selects of the
-    // high word and the fma instead of 2 x (compare, add, two 32-bit selects)
-#if defined(MDQT_EXPT_WRAPOLD)                       // A/B: the two conditional adds
+    // (measured: one fma p + m L with m = +1 / -1 / 0 instead of the two conditional adds issues 6
+    // instructions fewer per substep but lengthens the dependent chain — QT launch 21.3 -> 21.8 us,
+    // A/B round 3; the reference's two adds are kept)
     if (p < 0) p += L;
     if (p > L) p -= L;
     return p;
-#else
-    const double m = (p < 0) ? 1.0 : ((p > L) ? -1.0 : 0.0);
-    return fma(m, L, p);
-#endif
 }
 
 // the quantum jump (:573-703), the exact-mode operations of mdqt_kernels.hip

@@ -91,11 +91,14 @@ def test_large_config_forces_and_interval(cfg, orc):
     err = dabs / np.abs(G).max()
     # the error-bounded tail (force_tail_exp, default 12): tile pairs >= r_t apart are skipped, every
     # ion's force moves by at most `bound` (mdqt_engine.cpp tail_radius; 0 where r_t = L/2)
+    # and the far pair form (force_far_exp, default 13): <= far bound more
     rt, bound = s.const("force_skip_radius"), s.const("force_tail_bound")
+    rf, fbound = s.const("force_far_radius"), s.const("force_far_bound")
     print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}, "
-          f"max|dF| = {dabs:.3e}; skip radius {rt:.3f} (L/2 {L / 2:.3f}), tail bound {bound:.2e}")
+          f"max|dF| = {dabs:.3e}; skip radius {rt:.3f} (L/2 {L / 2:.3f}), tail bound {bound:.2e}; "
+          f"far radius {rf:.3f}, far bound {fbound:.2e}")
     assert err <= 1e-12
-    assert dabs <= bound + 1e-13 * np.abs(G).max()
+    assert dabs <= bound + fbound + 1e-13 * np.abs(G).max()
     mom = np.abs(F.sum(axis=1)).max() / (np.abs(F).sum() / N)
     print(f"{cfg}: |sum F| / mean|F| = {mom:.3e}")
     assert mom <= 1e-9
@@ -150,29 +153,39 @@ def test_spatial_order_tile_skipping_is_exact(orc):
 
 
 @pytest.mark.gpu
-def test_error_bounded_tail_at_1m():
-    """N = 1e6 (C4): the error-bounded skip radius r_t < L/2 (force_tail_exp 12) against the exact
-    L/2 skipping (force_tail_exp 0) on EVERY ion: |dF_i| <= (N - 1) g(r_t) <= 1e-12, the rigorous
-    bound the host computes (mdqt_engine.cpp tail_radius), plus the summation-order rounding;
-    a no-op at C3 and C5, where r_t would exceed L/2"""
+@pytest.mark.parametrize("cfg", ["C4", "C5"])
+def test_error_bounded_tail_and_far_form(cfg):
+    """The two error-bounded parts of the Newton-3 block forces against the exact sum to L/2 on EVERY
+    ion: the skip radius r_t < L/2 (force_tail_exp 12: |dF_i| <= (N - 1) g(r_t) <= 1e-12,
+    mdqt_engine.cpp tail_radius; active at N ~ 1e6) and the far pair form beyond r_far (force_far_exp
+    13: |dF_i| <= (N - 1) g(r_far) kFarRelErr <= 1e-13, far_radius; active at C4 and C5) — each
+    alone and together, plus the summation-order rounding; r_t is a no-op at C3 and C5"""
     import mdqtplasmasims_amd as M
-    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C4"]).init()
+    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg]).init()
     L = s.const("L")
-    rt, bound = s.const("force_skip_radius"), s.const("force_tail_bound")
-    assert 0 < bound <= 1e-12 and rt < L / 2
-    s.forces()
-    Ft = s.get_state()["F"]
-    s.set_option("force_tail_exp", 0)
-    assert s.const("force_skip_radius") == L / 2 and s.const("force_tail_bound") == 0
-    s.forces()
-    Fe = s.get_state()["F"]
-    d = np.abs(Ft - Fe).max()
-    print(f"C4 N={s.N}: r_t = {rt:.3f} (L/2 = {L / 2:.3f}), bound {bound:.2e}, max_i |dF_i| = {d:.3e}, "
-          f"max|F| = {np.abs(Fe).max():.3e}")
-    assert d <= bound + 1e-13 * np.abs(Fe).max()
+    rt, tb = s.const("force_skip_radius"), s.const("force_tail_bound")
+    rf, fb = s.const("force_far_radius"), s.const("force_far_bound")
+    assert 0 < fb <= 1e-13 and rf < L / 2
+    assert (0 < tb <= 1e-12 and rt < L / 2) if cfg == "C4" else (tb == 0 and rt == L / 2)
+    out = {}
+    for te, fe in ((12, 13), (0, 13), (12, 0), (0, 0)):
+        s.set_option("force_tail_exp", te)
+        s.set_option("force_far_exp", fe)
+        s.forces()
+        out[te, fe] = s.get_state()["F"]
+    assert s.const("force_skip_radius") == L / 2 and s.const("force_far_bound") == 0
+    Fe = out[0, 0]
+    scale = 1e-13 * np.abs(Fe).max()
+    d = {k: np.abs(v - Fe).max() for k, v in out.items()}
+    print(f"{cfg} N={s.N}: r_t {rt:.3f} (bound {tb:.2e}), r_far {rf:.3f} (bound {fb:.2e}), L/2 {L / 2:.3f}; "
+          f"max_i |dF_i|: both {d[12, 13]:.3e}, far only {d[0, 13]:.3e}, tail only {d[12, 0]:.3e}; "
+          f"max|F| {np.abs(Fe).max():.3e}")
+    assert d[12, 13] <= tb + fb + scale
+    assert d[0, 13] <= fb + scale
+    assert d[12, 0] <= tb + scale
     s.close()
-    for cfg in ("C3", "C5"):                          # r_t >= L/2: exact skipping only
-        x = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg])
+    if cfg == "C5":                                    # r_t >= L/2 at C3 too: exact skipping only
+        x = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C3"])
         x.set_state(*_tiny_state(x))
         assert x.const("force_tail_bound") == 0 and x.const("force_skip_radius") == x.const("L") / 2
         x.close()

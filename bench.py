@@ -746,6 +746,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     L = sim.const("L")
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
     rf, far = sim.const("force_far_radius"), sim.const("force_far_bound")
+    rv, vfar = sim.const("force_vfar_radius"), sim.const("force_vfar_bound")
     sim.close()
     unit_steps = ratio if qt else 1
     f_avg = f_ms / max(nf, 1) * 1e-3
@@ -761,11 +762,11 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force,
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail,
-                           "far_radius": rf, "far_bound": far,
-                           "note": "tile pairs >= skip_radius apart are skipped, tile pairs >= far_radius apart "
-                                   "take the far pair form (kFarRelErr 3e-9 per term); every ion's force is within "
-                                   "bound + far_bound of the exact sum to L/2 ((N-1) g(r), mdqt_engine.cpp "
-                                   "tail_radius / far_radius; 0 = exact). fp64 rates count all N(N-1)/2 pairs "
+                           "far_radius": rf, "far_bound": far, "vfar_radius": rv, "vfar_bound": vfar,
+                           "note": "tile pairs >= skip_radius apart are skipped, tile pairs >= far_radius / vfar_radius "
+                                   "apart take the far / very-far pair forms; every ion's force is within "
+                                   "bound + far_bound + vfar_bound of the exact sum to L/2 (mdqt_engine.cpp "
+                                   "tail_radius / far_radius_l; 0 = exact). fp64 rates count all N(N-1)/2 pairs "
                                    "(SURVEY 8d)"},
             "substeps_ms_per_md_step": s_ms / max(ns, 1) if ns else None}
 

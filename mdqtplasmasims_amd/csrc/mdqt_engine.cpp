@@ -118,6 +118,10 @@ struct mdqt_ctx {
     // >= r_far apart evaluate their pairs within kFarRelErr (rsq1, degree-6 2^f), r_far the smallest
     // radius with (N - 1) g(r_far) kFarRelErr <= eps — so no ion's force moves by more than eps
     int far_exp = 13;
+    // the very-far pair form (option "force_vfar_exp" k, 0 = off): tile pairs >= r_vfar apart use
+    // the raw rsq and a degree-5 2^f; r_vfar the smallest radius with
+    // (N - 1) g(r) ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) <= 10^-k
+    int vfar_exp = 13;
     uint32_t* dKeys = nullptr;     // [2][N] Hilbert keys, sorted keys
     int* dIon = nullptr;           // [2][N] identity, sorted index -> ion
     void* dSortTmp = nullptr;
@@ -820,6 +824,7 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
 
 static double tail_radius(int N, double L, double lDeb, int k, double* bound);
 static double far_radius(int N, double L, double lDeb, int k, double* bound);
+static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound);
 extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "gamToEinsteinFreq")) return s->gamToE;
     if (!strcmp(n, "quantumTimestep")) return s->dtQ;
@@ -845,6 +850,12 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
         const double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
                              ? far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound) : (bound = 0., s->L / 2.);
         return n[10] == 'r' ? r : bound;
+    }
+    if (!strcmp(n, "force_vfar_radius") || !strcmp(n, "force_vfar_bound")) {   // the very-far form's
+        double bound;                                  // radius and force bound (0: off, r = L/2)
+        const double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
+                             ? far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound) : (bound = 0., s->L / 2.);
+        return n[11] == 'r' ? r : bound;
     }
     if (!strcmp(n, "fused_step")) return s->fused_opt;
     if (!strcmp(n, "qt_im01")) return s->qc.im01;
@@ -1089,21 +1100,29 @@ static double tail_radius(int N, double L, double lDeb, int k, double* bound) {
     *bound = n1 * tail_g(hi, lDeb);
     return hi;
 }
-// the far radius: the smallest r with (N - 1) g(r) kFarRelErr <= 10^-k (L/2 = never, and bound 0,
-// when k = 0 or that r is >= L/2); bound = (N - 1) g(r_far) kFarRelErr
-static double far_radius(int N, double L, double lDeb, int k, double* bound) {
+// the far radii: the smallest r with (N - 1) g(r) err(r) <= 10^-k, err the relative error of a term
+// at distance r in the form (far: kFarRelErr; very far: (r/lDeb + 3) kRsqRawErr + kExp5RelErr) —
+// L/2 (= never) and bound 0 when k = 0 or that r is >= L/2; bound = (N - 1) g(r) err(r)
+static double far_err(double r, double lDeb, int level) {
+    return level == 2 ? (r / lDeb + 3.) * kRsqRawErr + kExp5RelErr : kFarRelErr;
+}
+static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound) {
     const double Rcut = L / 2.;
     *bound = 0.;
     if (k <= 0 || N < 2) return Rcut;
-    const double eps = pow(10., -k), n1 = (double)(N - 1) * kFarRelErr;
-    if (n1 * tail_g(Rcut, lDeb) > eps) return Rcut;
+    const double eps = pow(10., -k), n1 = (double)(N - 1);
+    auto b = [&](double r) { return n1 * tail_g(r, lDeb) * far_err(r, lDeb, level); };
+    if (b(Rcut) > eps) return Rcut;
     double lo = 0., hi = Rcut;
     for (int it = 0; it < 200 && hi - lo > 1e-12 * Rcut; ++it) {
         const double m = 0.5 * (lo + hi);
-        if (m > 0 && n1 * tail_g(m, lDeb) <= eps) hi = m; else lo = m;
+        if (m > 0 && b(m) <= eps) hi = m; else lo = m;
     }
-    *bound = n1 * tail_g(hi, lDeb);
+    *bound = b(hi);
     return hi;
+}
+static double far_radius(int N, double L, double lDeb, int k, double* bound) {
+    return far_radius_l(N, L, lDeb, k, 1, bound);
 }
 
 // the block-pair kernels' arguments for the current positions: with force_sort, the Hilbert order,
@@ -1118,6 +1137,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     double bound;
     a.Rskip = tail_radius(s->N, s->L, s->lDeb, s->tail_exp, &bound);
     a.Rfar = far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound);
+    a.Rvfar = far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound);
     if (s->sort_mode) {                            // Hilbert order + tile boxes (mdqt_sort.hip)
         SortArgs o;
         o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
@@ -2379,6 +2399,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     if (!strcmp(name, "overlap")) {                    // force || QT launches of an MD step (mdqt_md_steps)
         if (value < 0 || value > 1) return fail("overlap must be 0 or 1");
         s->overlap_opt = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_vfar_exp")) {             // very-far pair form: eps = 10^-value (0: off)
+        if (value < 0 || value > 300) return fail("force_vfar_exp must be 0 (off) .. 300");
+        s->vfar_exp = value;
         return 0;
     }
     if (!strcmp(name, "force_far_exp")) {              // far pair form: eps = 10^-value (0: off)

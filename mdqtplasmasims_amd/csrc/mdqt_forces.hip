@@ -189,8 +189,21 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
     return Rall + (size_t)w * 3 * S + (g - w * S);
 }
 
+// steps whose j-side terms are combined in registers before one LDS atomic (block kernel; 1 = every
+// step its own ds_add_f64)
+#ifndef MDQT_N3B_JCOMB
+#define MDQT_N3B_JCOMB 1
+#endif
+constexpr int kJComb = MDQT_N3B_JCOMB;
+static_assert(kJComb == 1 || kJComb == 2 || kJComb == 4 || kJComb == 8 || kJComb == 16, "j-side step groups");
+__device__ __forceinline__ double wave_rol1(double v) {   // lane l <- lane (l + 1) mod 64
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x134, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x134, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
-          bool POT = false, bool FAR = false>
+          bool POT = false, int FAR = 0>
 __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi, double zi, double mi,
                                          const double (*pj)[128], const double* mj, double* ax, double* ay,
                                          double* az, double& fx, double& fy, double& fz, const PairC& c,
@@ -205,7 +218,48 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
     const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);                    \
     const double* mjb = mj + b_;                                                           \
     double *axb = ax + b_, *ayb = ay + b_, *azb = az + b_
-    if (!diag) {
+    if constexpr (kJComb > 1) {
+        // j side combined over kJComb consecutive steps before one ds_add_f64 per component: at
+        // step t lane l's pair is with J index l + t, at step t + 1 lane l + 1's is too, so the
+        // running sum rotated one lane down (wave_rol:1, lane l reads lane l + 1) plus this step's
+        // term is the sum for lane l's current J index; lane 63 receives lane 0's sum, whose index
+        // differs by 64 — the same J ion (the tile sits in LDS twice, the halves summed at the end)
+        auto group = [&](auto&& pjb, const double* mjb, double* axb, double* ayb, double* azb, int t, double m,
+                         double& jx, double& jy, double& jz) {
+            double px, py, pz;
+            n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, m, xi, yi, zi, mi, pjb, mjb, fx, fy, fz, c, nsh,
+                                                                   px, py, pz);
+            if (t % kJComb == 0) {
+                jx = px; jy = py; jz = pz;
+            } else {
+                jx = wave_rol1(jx) + px;
+                if constexpr (!POT) { jy = wave_rol1(jy) + py; jz = wave_rol1(jz) + pz; }
+            }
+            if (t % kJComb == kJComb - 1) {
+                __hip_atomic_fetch_add(&axb[t], jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                if constexpr (!POT) {
+                    __hip_atomic_fetch_add(&ayb[t], jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    __hip_atomic_fetch_add(&azb[t], jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+            }
+        };
+        if (!diag) {
+            for (int t0 = 0; t0 < 64; t0 += 16) {
+                N3B_REBASE(l + t0);
+                double jx = 0., jy = 0., jz = 0.;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) group(pjb, mjb, axb, ayb, azb, t, 1., jx, jy, jz);
+            }
+        } else {
+            for (int t0 = 1; t0 < 33; t0 += 16) {
+                N3B_REBASE(l + t0);
+                double jx = 0., jy = 0., jz = 0.;
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    group(pjb, mjb, axb, ayb, azb, t, (t0 + t == 32 && l >= 32) ? 0. : 1., jx, jy, jz);
+            }
+        }
+    } else if (!diag) {
         for (int t0 = 0; t0 < 64; t0 += 16) {
             N3B_REBASE(l + t0);
 #pragma unroll
@@ -265,11 +319,13 @@ void k_pairs_n3b(N3BArgs a) {
     //    of the two ends; equal ends = one minimum-image multiple per axis for every pair, bit for
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
-    // class: -1 skip; otherwise bit 0 = uniform image, bit 1 = far (the far pair form, forces only)
+    // class: -1 skip; otherwise bit 0 = uniform image, + 2 x the far level (1 far pair form, 2 very
+    // far; forces only): 0 .. 5
     __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class
     // skip below the cutoff only for the forces (error-bounded tail, mdqt_engine.cpp tail_radius)
     const double rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
     const double rf2 = (POT || VARIANT != 1 || !(a.Rfar < a.Rcut)) ? INFINITY : a.Rfar * a.Rfar;
+    const double rv2 = (POT || VARIANT != 1 || !(a.Rvfar < a.Rcut)) ? INFINITY : a.Rvfar * a.Rvfar;
     auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
         const double* B = a.boxes;
         double g2 = 0.;
@@ -288,7 +344,8 @@ void k_pairs_n3b(N3BArgs a) {
             n[c3] = nlo;
         }
         const double cls = (a.use_sort == 1 && g2 > rc2) ? -1.
-                                                          : ((VARIANT == 1 && uni) ? 1. : 0.) + (g2 > rf2 ? 2. : 0.);
+                                                          : ((VARIANT == 1 && uni) ? 1. : 0.) +
+                                                                (g2 > rv2 ? 4. : g2 > rf2 ? 2. : 0.);
         return make_double4(n[0], n[1], n[2], cls);
     };
     // the run's i accumulator lives in LDS (read and written once per block distance) so that
@@ -338,16 +395,19 @@ void k_pairs_n3b(N3BArgs a) {
                 if (ragN && (I == T - 1 || J == T - 1))
                     n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
                                                                     tz, c);
-                else if (VARIANT == 1 && (cls == 1. || cls == 3.)) {
+                else if (VARIANT == 1 && (cls == 1. || cls == 3. || cls == 5.)) {
                     const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
                     // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
                     const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
                     const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
                     const double sz = MDQT_SHIFT_I ? fma(-nsh[2], a.L, zi) : zi;
                     if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                        if (cls == 3.)              // far tile pair: the far pair form
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, true>(diag, l, sx, sy, sz, mi, pj, mj, ax,
-                                                                                  ay, az, tx, ty, tz, c, nsh);
+                        if (cls == 5.)              // very far tile pair
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
+                                                                               az, tx, ty, tz, c, nsh);
+                        else if (cls == 3.)         // far tile pair: the far pair form
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 1>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
+                                                                               az, tx, ty, tz, c, nsh);
                         else
                             n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
                                                                             az, tx, ty, tz, c, nsh);
@@ -356,9 +416,12 @@ void k_pairs_n3b(N3BArgs a) {
                                                                                 ay, az, tx, ty, tz, c, nsh);
                     }
                 } else if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                    if (cls == 2.)
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, true>(diag, l, xi, yi, zi, mi, pj, mj, ax,
-                                                                               ay, az, tx, ty, tz, c);
+                    if (cls == 4.)
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                            az, tx, ty, tz, c);
+                    else if (cls == 2.)
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                            az, tx, ty, tz, c);
                     else
                         n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az,
                                                                          tx, ty, tz, c);

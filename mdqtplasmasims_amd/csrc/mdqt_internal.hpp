@@ -261,6 +261,25 @@ __device__ __forceinline__ double rsq1(double x) {
     const double e = fma(-x, q * q, 1.0);
     return fma(0.5 * q, e, q);
 }
+// The very-far tier (box gap >= r_vfar): the raw v_rsq_f64 (relative error <= kRsqRawErr: measured
+// 2^-24 by tools/rsq_precision.hip over r^2 in [1e-4, 1e6], checked by a GPU test; twice that here)
+// and a degree-5 fit of 2^f (1.02e-7 relative).  A term at distance r is then within
+// ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) of itself relatively — r/lDeb from t = r log2(e)/lDeb
+// carrying ri's error into 2^t, 3 from ri^3 — and g(r) times that factor decreases in r, so
+// (N - 1) g(r_vfar) ((r_vfar/lDeb + 3) kRsqRawErr + kExp5RelErr) bounds every ion (far_radius).
+constexpr double kRsqRawErr = 0x1p-23;
+constexpr double kExp5RelErr = 1.1e-7;
+__device__ __forceinline__ double exp2_neg_cut5(double t, bool keep) {
+    const double n = __builtin_rint(t);
+    const double f = t - n;
+    double p = 0x1.5f0890162a90ap-10;
+    p = fma(p, f, 0x1.3d10705276a1dp-7);
+    p = fma(p, f, 0x1.c6af6cdbbdcc7p-5);
+    p = fma(p, f, 0x1.ebf906e26e833p-3);
+    p = fma(p, f, 0x1.62e4302fc626ep-1);
+    p = fma(p, f, 0x1.0000014413897p+0);
+    return ldexp(p, keep ? (int)n : -1100);
+}
 __device__ __forceinline__ double exp2_neg_cut6(double t, bool keep) {
     const double n = __builtin_rint(t);
     const double f = t - n;
@@ -368,6 +387,7 @@ struct N3BArgs {
     const double* boxes;// [12][T]: tile center (x, y, z), half extents, raw coordinate min, max
     double Rfar;        // tile pairs whose boxes are >= Rfar apart take the far pair form (kFarRelErr;
                         // forces only, use_sort 1 or 2); >= Rcut: never
+    double Rvfar;       // >= Rvfar apart: the very-far form (raw rsq, degree-5 2^f); >= Rcut: never
     double Rskip;       // force tile pairs whose boxes are >= Rskip apart are skipped (use_sort 1):
                         // Rcut exactly (every skipped pair is beyond L/2), or the error-bounded tail
                         // radius r_t < L/2 of mdqt_engine.cpp tail_radius (potentials: always Rcut)

@@ -105,6 +105,18 @@ __device__ __forceinline__ double pair_ft_cut_far(double dx, double dy, double d
     return ((ri + c.invlDeb) * exp2_neg_cut6(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
 }
 
+// pair_ft_cut of a very far tile pair: the raw v_rsq_f64 and the degree-5 2^f (mdqt_internal.hpp)
+__device__ __forceinline__ double pair_ft_cut_vfar(double dx, double dy, double dz, const PairC& c) {
+    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double ri = __builtin_amdgcn_rsq(r2);
+#else
+    const double ri = 1. / sqrt(r2);
+#endif
+    const double dr = r2 * ri;
+    return ((ri + c.invlDeb) * exp2_neg_cut5(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
+}
+
 template <int VARIANT>
 __device__ __forceinline__ void accum(double& f, double d, double ft) {
     if (VARIANT == 0) f += d * ft;        // the reference's F[i] += dx*ftotal (:225-230)
@@ -134,12 +146,14 @@ __device__ __forceinline__ void accum(double& f, double d, double ft) {
 #endif
 // POT: Epotential's pair potential u (pair_u) instead of the force: u to the i accumulator fx and
 // to the j accumulator ax only (both sides of a pair get +u)
+// the pair terms of one rotation step: the lane's i ion against the J-tile ion at LDS index idx —
+// the force components (px, py, pz) to the i accumulator; returns them for the j side (POT: u in px)
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          bool FAR = false>
-__device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
-                                        const double (*pj)[128], const double* mj, double* ax, double* ay,
-                                        double* az, double& fx, double& fy, double& fz, const PairC& c,
-                                        const double* nsh = nullptr) {
+          int FAR = 0>
+__device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi, double zi, double mi,
+                                         const double (*pj)[128], const double* mj, double& fx, double& fy,
+                                         double& fz, const PairC& c, const double* nsh, double& px, double& py,
+                                         double& pz) {
     double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
     if constexpr (SHIFT) {
         if (!MDQT_SHIFT_I) {
@@ -155,22 +169,41 @@ __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi,
         if (RAGGED) u *= mi * mj[idx];
         u *= m;
         fx += u;
-        __hip_atomic_fetch_add(&ax[idx], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        (void)ay; (void)az; (void)fy; (void)fz;
+        px = u; py = 0.; pz = 0.;
+        (void)fy; (void)fz;
         return;
     }
     static_assert(!FAR || (CUT && !POT), "the far pair form is the fast force variant's");
-    double ft = FAR ? pair_ft_cut_far(dx, dy, dz, c) : CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
+    // FAR: 0 exact form, 1 far form, 2 very-far form (Newton-3 blocks, error-bounded)
+    double ft = FAR == 2 ? pair_ft_cut_vfar(dx, dy, dz, c)
+              : FAR == 1 ? pair_ft_cut_far(dx, dy, dz, c)
+              : CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];
     ft *= m;
-    const double px = dx * ft, py = dy * ft, pz = dz * ft;
+    px = dx * ft; py = dy * ft; pz = dz * ft;
     fx += px; fy += py; fz += pz;
+}
+
+// one rotation step: the pair terms, +f to the i accumulator (registers) and to the j accumulator
+// (ds_add_f64 at index idx, no return; one wave's LDS operations run in order, so the
+// accumulation order is fixed)
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
+          int FAR = 0>
+__device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
+                                        const double (*pj)[128], const double* mj, double* ax, double* ay,
+                                        double* az, double& fx, double& fy, double& fz, const PairC& c,
+                                        const double* nsh = nullptr) {
+    double px, py, pz;
+    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh, px, py,
+                                                           pz);
 #if defined(MDQT_EXPT_NOJACC)
     (void)ax; (void)ay; (void)az;
 #else
     __hip_atomic_fetch_add(&ax[idx], px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if constexpr (!POT) {
+        __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
 #endif
 }
 

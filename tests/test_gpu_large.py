@@ -97,8 +97,9 @@ def test_large_config_forces_and_interval(cfg, orc):
     print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}, "
           f"max|dF| = {dabs:.3e}; skip radius {rt:.3f} (L/2 {L / 2:.3f}), tail bound {bound:.2e}; "
           f"far radius {rf:.3f}, far bound {fbound:.2e}")
+    vbound = s.const("force_vfar_bound")
     assert err <= 1e-12
-    assert dabs <= bound + fbound + 1e-13 * np.abs(G).max()
+    assert dabs <= bound + fbound + vbound + 1e-13 * np.abs(G).max()
     mom = np.abs(F.sum(axis=1)).max() / (np.abs(F).sum() / N)
     print(f"{cfg}: |sum F| / mean|F| = {mom:.3e}")
     assert mom <= 1e-9
@@ -155,34 +156,39 @@ def test_spatial_order_tile_skipping_is_exact(orc):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["C4", "C5"])
 def test_error_bounded_tail_and_far_form(cfg):
-    """The two error-bounded parts of the Newton-3 block forces against the exact sum to L/2 on EVERY
+    """The error-bounded parts of the Newton-3 block forces against the exact sum to L/2 on EVERY
     ion: the skip radius r_t < L/2 (force_tail_exp 12: |dF_i| <= (N - 1) g(r_t) <= 1e-12,
-    mdqt_engine.cpp tail_radius; active at N ~ 1e6) and the far pair form beyond r_far (force_far_exp
-    13: |dF_i| <= (N - 1) g(r_far) kFarRelErr <= 1e-13, far_radius; active at C4 and C5) — each
-    alone and together, plus the summation-order rounding; r_t is a no-op at C3 and C5"""
+    mdqt_engine.cpp tail_radius; active at N ~ 1e6), the far pair form beyond r_far (force_far_exp
+    13: (N - 1) g(r_far) kFarRelErr <= 1e-13) and the very-far form beyond r_vfar (force_vfar_exp
+    13: (N - 1) g(r) ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) <= 1e-13) — each alone and all
+    together, plus the summation-order rounding; r_t is a no-op at C3 and C5"""
     import mdqtplasmasims_amd as M
     s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg]).init()
     L = s.const("L")
     rt, tb = s.const("force_skip_radius"), s.const("force_tail_bound")
     rf, fb = s.const("force_far_radius"), s.const("force_far_bound")
-    assert 0 < fb <= 1e-13 and rf < L / 2
+    rv, vb = s.const("force_vfar_radius"), s.const("force_vfar_bound")
+    assert 0 < fb <= 1e-13 and rf < L / 2 and 0 < vb <= 1e-13 and rf < rv < L / 2
     assert (0 < tb <= 1e-12 and rt < L / 2) if cfg == "C4" else (tb == 0 and rt == L / 2)
     out = {}
-    for te, fe in ((12, 13), (0, 13), (12, 0), (0, 0)):
+    for te, fe, ve in ((12, 13, 13), (0, 13, 0), (0, 0, 13), (12, 0, 0), (0, 0, 0)):
         s.set_option("force_tail_exp", te)
         s.set_option("force_far_exp", fe)
+        s.set_option("force_vfar_exp", ve)
         s.forces()
-        out[te, fe] = s.get_state()["F"]
+        out[te, fe, ve] = s.get_state()["F"]
     assert s.const("force_skip_radius") == L / 2 and s.const("force_far_bound") == 0
-    Fe = out[0, 0]
+    assert s.const("force_vfar_bound") == 0
+    Fe = out[0, 0, 0]
     scale = 1e-13 * np.abs(Fe).max()
     d = {k: np.abs(v - Fe).max() for k, v in out.items()}
-    print(f"{cfg} N={s.N}: r_t {rt:.3f} (bound {tb:.2e}), r_far {rf:.3f} (bound {fb:.2e}), L/2 {L / 2:.3f}; "
-          f"max_i |dF_i|: both {d[12, 13]:.3e}, far only {d[0, 13]:.3e}, tail only {d[12, 0]:.3e}; "
-          f"max|F| {np.abs(Fe).max():.3e}")
-    assert d[12, 13] <= tb + fb + scale
-    assert d[0, 13] <= fb + scale
-    assert d[12, 0] <= tb + scale
+    print(f"{cfg} N={s.N}: r_t {rt:.3f} (bound {tb:.2e}), r_far {rf:.3f} ({fb:.2e}), r_vfar {rv:.3f} ({vb:.2e}), "
+          f"L/2 {L / 2:.3f}; max_i |dF_i|: all {d[12, 13, 13]:.3e}, far only {d[0, 13, 0]:.3e}, very far only "
+          f"{d[0, 0, 13]:.3e}, tail only {d[12, 0, 0]:.3e}; max|F| {np.abs(Fe).max():.3e}")
+    assert d[12, 13, 13] <= tb + fb + vb + scale
+    assert d[0, 13, 0] <= fb + scale
+    assert d[0, 0, 13] <= vb + scale
+    assert d[12, 0, 0] <= tb + scale
     s.close()
     if cfg == "C5":                                    # r_t >= L/2 at C3 too: exact skipping only
         x = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C3"])
@@ -272,3 +278,18 @@ def test_epotential_newton3_blocks_match_rows(sort):
     s.close()
     print(f"N0=70000 sort={sort}: Epot blocks {e3:.15e} rows {er:.15e}")
     assert abs(e3 - er) <= 1e-13 * abs(er), (e3, er)
+
+
+@pytest.mark.gpu
+def test_raw_rsq_error_within_the_very_far_bound():
+    """The very-far pair form's bound assumes v_rsq_f64 is within kRsqRawErr = 2^-23 of 1/sqrt(x)
+    (mdqt_internal.hpp): tools/rsq_precision (built by __graft_entry__.build()) measures it on 4M
+    inputs over r^2 in [1e-4, 1e6] against a long-double reference"""
+    import re
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "rsq_precision")
+    assert os.path.exists(exe), "tools/rsq_precision missing: run __graft_entry__.build()"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
+    raw = float(re.search(r"raw ([0-9.e+-]+)", out).group(1))
+    print(out.strip())
+    assert raw <= 2.0 ** -23

@@ -530,6 +530,29 @@ def test_observables_match_oracle(eng, orc):
     assert abs(s.Epotential() - o.epotential()) <= 1e-12 * abs(o.epotential())
 
 
+def test_kde_skipping_matches_dense_sum(eng, orc):
+    """output()'s Gaussian KDE (SpeedUp:958-979) on the device skips, per wave, ions whose terms are
+    exact zeros on all its bins (|b -+ v| >= kKdeSkip = 0.0773, beyond exp's underflow for
+    V2 = 1/(2 0.002^2); mdqt_internal.hpp asserts the threshold against V2): against the oracle's
+    dense sum on velocities spread over and beyond the 2001 bins, with ions placed just inside and
+    just outside the skip distance of bin centres"""
+    kw = dict(N0=500, seed=8, rng_mode=1)
+    o = orc.OracleSim(nthreads=8, **kw).init()
+    st = o.get_state()
+    rng = np.random.default_rng(2)
+    V = rng.uniform(-5.3, 5.3, st["V"].shape)
+    n = V.shape[1] // 4
+    bins = rng.integers(0, 2001, (3, n)) * 0.0025
+    V[:, :n] = bins + rng.choice([-1.0, 1.0], (3, n)) * (0.0773 + rng.choice([-1e-4, 1e-4, 0.0], (3, n)))
+    s = eng.Simulation(**kw)
+    for x in (s, o):
+        x.set_state(st["R"], V, st["psi"], st["tPart"], st["t"])
+    _, aP, _ = s.observables(pops=False)
+    _, bP, _ = o.observables(pops=False)
+    assert rel(aP, bP) < 1e-12
+    s.close()
+
+
 @pytest.mark.parametrize("N0", [500, 3500])
 def test_epotential_newton3_tiles_match_rows(eng, N0):
     """Epotential() on the Newton-3 tiles (each distinct pair once, world 1 default) against the

@@ -747,6 +747,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
     rf, far = sim.const("force_far_radius"), sim.const("force_far_bound")
     rv, vfar = sim.const("force_vfar_radius"), sim.const("force_vfar_bound")
+    ru, ufar = sim.const("force_ufar_radius"), sim.const("force_ufar_bound")
     sim.close()
     unit_steps = ratio if qt else 1
     f_avg = f_ms / max(nf, 1) * 1e-3
@@ -763,9 +764,10 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "scaling": "strong", "init_s": t_init, "force": force,
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail,
                            "far_radius": rf, "far_bound": far, "vfar_radius": rv, "vfar_bound": vfar,
+                           "ufar_radius": ru, "ufar_bound": ufar,
                            "note": "tile pairs >= skip_radius apart are skipped, tile pairs >= far_radius / vfar_radius "
-                                   "apart take the far / very-far pair forms; every ion's force is within "
-                                   "bound + far_bound + vfar_bound of the exact sum to L/2 (mdqt_engine.cpp "
+                                   "apart take the far / very-far / ultra-far pair forms; every ion's force is "
+                                   "within bound + far_bound + vfar_bound + ufar_bound of the exact sum to L/2 (mdqt_engine.cpp "
                                    "tail_radius / far_radius_l; 0 = exact). fp64 rates count all N(N-1)/2 pairs "
                                    "(SURVEY 8d)"},
             "substeps_ms_per_md_step": s_ms / max(ns, 1) if ns else None}

@@ -122,6 +122,9 @@ struct mdqt_ctx {
     // the raw rsq and a degree-5 2^f; r_vfar the smallest radius with
     // (N - 1) g(r) ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) <= 10^-k
     int vfar_exp = 13;
+    // the ultra-far pair form (option "force_ufar_exp" k, 0 = off): raw rsq and v_exp_f32, r_ufar the
+    // smallest radius with (N - 1) g(r) ((r/lDeb) (kRsqRawErr + 2^-24) + 3 kRsqRawErr + kExp2fRelErr) <= 10^-k
+    int ufar_exp = 13;
     uint32_t* dKeys = nullptr;     // [2][N] Hilbert keys, sorted keys
     int* dIon = nullptr;           // [2][N] identity, sorted index -> ion
     void* dSortTmp = nullptr;
@@ -851,6 +854,13 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
                              ? far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound) : (bound = 0., s->L / 2.);
         return n[10] == 'r' ? r : bound;
     }
+    if (!strcmp(n, "force_ufar_radius") || !strcmp(n, "force_ufar_bound")) {   // the ultra-far form's
+        double bound;                                  // radius and force bound (0: off, r = L/2)
+        double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
+                       ? far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound) : (bound = 0., s->L / 2.);
+        if (r < s->L / 2. && s->L / 2. > 80. * s->lDeb) { r = s->L / 2.; bound = 0.; }
+        return n[11] == 'r' ? r : bound;
+    }
     if (!strcmp(n, "force_vfar_radius") || !strcmp(n, "force_vfar_bound")) {   // the very-far form's
         double bound;                                  // radius and force bound (0: off, r = L/2)
         const double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
@@ -1104,6 +1114,7 @@ static double tail_radius(int N, double L, double lDeb, int k, double* bound) {
 // at distance r in the form (far: kFarRelErr; very far: (r/lDeb + 3) kRsqRawErr + kExp5RelErr) —
 // L/2 (= never) and bound 0 when k = 0 or that r is >= L/2; bound = (N - 1) g(r) err(r)
 static double far_err(double r, double lDeb, int level) {
+    if (level == 3) return (r / lDeb) * (kRsqRawErr + 0x1p-24) + 3. * kRsqRawErr + kExp2fRelErr;
     return level == 2 ? (r / lDeb + 3.) * kRsqRawErr + kExp5RelErr : kFarRelErr;
 }
 static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound) {
@@ -1138,6 +1149,9 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.Rskip = tail_radius(s->N, s->L, s->lDeb, s->tail_exp, &bound);
     a.Rfar = far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound);
     a.Rvfar = far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound);
+    a.Rufar = far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound);
+    // f32's normal range: 2^t for t >= -126 (r <= 126 lDeb ln2 = 87 lDeb); never beyond it
+    if (a.Rufar < a.Rcut && a.Rcut > 80. * s->lDeb) a.Rufar = a.Rcut;
     if (s->sort_mode) {                            // Hilbert order + tile boxes (mdqt_sort.hip)
         SortArgs o;
         o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
@@ -2399,6 +2413,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     if (!strcmp(name, "overlap")) {                    // force || QT launches of an MD step (mdqt_md_steps)
         if (value < 0 || value > 1) return fail("overlap must be 0 or 1");
         s->overlap_opt = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_ufar_exp")) {             // ultra-far pair form: eps = 10^-value (0: off)
+        if (value < 0 || value > 300) return fail("force_ufar_exp must be 0 (off) .. 300");
+        s->ufar_exp = value;
         return 0;
     }
     if (!strcmp(name, "force_vfar_exp")) {             // very-far pair form: eps = 10^-value (0: off)

@@ -320,12 +320,13 @@ void k_pairs_n3b(N3BArgs a) {
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
     // class: -1 skip; otherwise bit 0 = uniform image, + 2 x the far level (1 far pair form, 2 very
-    // far; forces only): 0 .. 5
+    // far, 3 ultra far; forces only): 0 .. 7
     __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class
     // skip below the cutoff only for the forces (error-bounded tail, mdqt_engine.cpp tail_radius)
     const double rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
     const double rf2 = (POT || VARIANT != 1 || !(a.Rfar < a.Rcut)) ? INFINITY : a.Rfar * a.Rfar;
     const double rv2 = (POT || VARIANT != 1 || !(a.Rvfar < a.Rcut)) ? INFINITY : a.Rvfar * a.Rvfar;
+    const double ru2 = (POT || VARIANT != 1 || !(a.Rufar < a.Rcut)) ? INFINITY : a.Rufar * a.Rufar;
     auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
         const double* B = a.boxes;
         double g2 = 0.;
@@ -345,7 +346,7 @@ void k_pairs_n3b(N3BArgs a) {
         }
         const double cls = (a.use_sort == 1 && g2 > rc2) ? -1.
                                                           : ((VARIANT == 1 && uni) ? 1. : 0.) +
-                                                                (g2 > rv2 ? 4. : g2 > rf2 ? 2. : 0.);
+                                                                (g2 > ru2 ? 6. : g2 > rv2 ? 4. : g2 > rf2 ? 2. : 0.);
         return make_double4(n[0], n[1], n[2], cls);
     };
     // the run's i accumulator lives in LDS (read and written once per block distance) so that
@@ -395,14 +396,17 @@ void k_pairs_n3b(N3BArgs a) {
                 if (ragN && (I == T - 1 || J == T - 1))
                     n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
                                                                     tz, c);
-                else if (VARIANT == 1 && (cls == 1. || cls == 3. || cls == 5.)) {
+                else if (VARIANT == 1 && (cls == 1. || cls == 3. || cls == 5. || cls == 7.)) {
                     const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
                     // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
                     const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
                     const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
                     const double sz = MDQT_SHIFT_I ? fma(-nsh[2], a.L, zi) : zi;
                     if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                        if (cls == 5.)              // very far tile pair
+                        if (cls == 7.)              // ultra far tile pair
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
+                                                                               az, tx, ty, tz, c, nsh);
+                        else if (cls == 5.)         // very far tile pair
                             n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
                                                                                az, tx, ty, tz, c, nsh);
                         else if (cls == 3.)         // far tile pair: the far pair form
@@ -416,7 +420,7 @@ void k_pairs_n3b(N3BArgs a) {
                                                                                 ay, az, tx, ty, tz, c, nsh);
                     }
                 } else if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                    if (cls == 4.)
+                    if (cls >= 4.)                  // (ultra far with a per-pair image: rare, very-far form)
                         n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                             az, tx, ty, tz, c);
                     else if (cls == 2.)

@@ -269,6 +269,11 @@ __device__ __forceinline__ double rsq1(double x) {
 // (N - 1) g(r_vfar) ((r_vfar/lDeb + 3) kRsqRawErr + kExp5RelErr) bounds every ion (far_radius).
 constexpr double kRsqRawErr = 0x1p-23;
 constexpr double kExp5RelErr = 1.1e-7;
+// The ultra-far tier (box gap >= r_ufar): the raw v_rsq_f64 and 2^t by v_exp_f32 on t rounded to
+// float (relative 2^-24): a term is within (r/lDeb) (kRsqRawErr + 2^-24) + 3 kRsqRawErr +
+// kExp2fRelErr of itself (kExp2fRelErr: twice what tools/exp2f_precision measures, re-checked by a
+// GPU test).  f32's range holds 2^t down to t = -126: r <= 87 lDeb, beyond every L/2 it serves.
+constexpr double kExp2fRelErr = 0x1p-22;
 __device__ __forceinline__ double exp2_neg_cut5(double t, bool keep) {
     const double n = __builtin_rint(t);
     const double f = t - n;
@@ -388,6 +393,7 @@ struct N3BArgs {
     double Rfar;        // tile pairs whose boxes are >= Rfar apart take the far pair form (kFarRelErr;
                         // forces only, use_sort 1 or 2); >= Rcut: never
     double Rvfar;       // >= Rvfar apart: the very-far form (raw rsq, degree-5 2^f); >= Rcut: never
+    double Rufar;       // >= Rufar apart: the ultra-far form (raw rsq, v_exp_f32); >= Rcut: never
     double Rskip;       // force tile pairs whose boxes are >= Rskip apart are skipped (use_sort 1):
                         // Rcut exactly (every skipped pair is beyond L/2), or the error-bounded tail
                         // radius r_t < L/2 of mdqt_engine.cpp tail_radius (potentials: always Rcut)

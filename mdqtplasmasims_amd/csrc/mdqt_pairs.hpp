@@ -117,6 +117,25 @@ __device__ __forceinline__ double pair_ft_cut_vfar(double dx, double dy, double 
     return ((ri + c.invlDeb) * exp2_neg_cut5(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
 }
 
+// pair_ft_cut of an ultra-far tile pair: the raw v_rsq_f64 and 2^t by v_exp_f32 (t rounded to
+// float; the cutoff as t = -inf, whose 2^t is +0)
+__device__ __forceinline__ double pair_ft_cut_ufar(double dx, double dy, double dz, const PairC& c) {
+    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double ri = __builtin_amdgcn_rsq(r2);
+#else
+    const double ri = 1. / sqrt(r2);
+#endif
+    const double dr = r2 * ri;
+    const float tf = dr < c.Rcut ? (float)(dr * (c.invlDeb * kNegLog2e)) : -INFINITY;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double e = (double)__builtin_amdgcn_exp2f(tf);
+#else
+    const double e = (double)exp2f(tf);
+#endif
+    return ((ri + c.invlDeb) * e) * (ri * ri);
+}
+
 template <int VARIANT>
 __device__ __forceinline__ void accum(double& f, double d, double ft) {
     if (VARIANT == 0) f += d * ft;        // the reference's F[i] += dx*ftotal (:225-230)
@@ -174,8 +193,9 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
         return;
     }
     static_assert(!FAR || (CUT && !POT), "the far pair form is the fast force variant's");
-    // FAR: 0 exact form, 1 far form, 2 very-far form (Newton-3 blocks, error-bounded)
-    double ft = FAR == 2 ? pair_ft_cut_vfar(dx, dy, dz, c)
+    // FAR: 0 exact form, 1 far, 2 very far, 3 ultra far (Newton-3 blocks, error-bounded)
+    double ft = FAR == 3 ? pair_ft_cut_ufar(dx, dy, dz, c)
+              : FAR == 2 ? pair_ft_cut_vfar(dx, dy, dz, c)
               : FAR == 1 ? pair_ft_cut_far(dx, dy, dz, c)
               : CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];

@@ -97,7 +97,7 @@ def test_large_config_forces_and_interval(cfg, orc):
     print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}, "
           f"max|dF| = {dabs:.3e}; skip radius {rt:.3f} (L/2 {L / 2:.3f}), tail bound {bound:.2e}; "
           f"far radius {rf:.3f}, far bound {fbound:.2e}")
-    vbound = s.const("force_vfar_bound")
+    vbound = s.const("force_vfar_bound") + s.const("force_ufar_bound")
     assert err <= 1e-12
     assert dabs <= bound + fbound + vbound + 1e-13 * np.abs(G).max()
     mom = np.abs(F.sum(axis=1)).max() / (np.abs(F).sum() / N)
@@ -168,27 +168,33 @@ def test_error_bounded_tail_and_far_form(cfg):
     rt, tb = s.const("force_skip_radius"), s.const("force_tail_bound")
     rf, fb = s.const("force_far_radius"), s.const("force_far_bound")
     rv, vb = s.const("force_vfar_radius"), s.const("force_vfar_bound")
+    ru, ub = s.const("force_ufar_radius"), s.const("force_ufar_bound")
     assert 0 < fb <= 1e-13 and rf < L / 2 and 0 < vb <= 1e-13 and rf < rv < L / 2
+    assert 0 < ub <= 1e-13 and rf < ru < L / 2
     assert (0 < tb <= 1e-12 and rt < L / 2) if cfg == "C4" else (tb == 0 and rt == L / 2)
     out = {}
-    for te, fe, ve in ((12, 13, 13), (0, 13, 0), (0, 0, 13), (12, 0, 0), (0, 0, 0)):
+    for te, fe, ve, ue in ((12, 13, 13, 13), (0, 13, 0, 0), (0, 0, 13, 0), (0, 0, 0, 13), (12, 0, 0, 0),
+                           (0, 0, 0, 0)):
         s.set_option("force_tail_exp", te)
         s.set_option("force_far_exp", fe)
         s.set_option("force_vfar_exp", ve)
+        s.set_option("force_ufar_exp", ue)
         s.forces()
-        out[te, fe, ve] = s.get_state()["F"]
+        out[te, fe, ve, ue] = s.get_state()["F"]
     assert s.const("force_skip_radius") == L / 2 and s.const("force_far_bound") == 0
-    assert s.const("force_vfar_bound") == 0
-    Fe = out[0, 0, 0]
+    assert s.const("force_vfar_bound") == 0 and s.const("force_ufar_bound") == 0
+    Fe = out[0, 0, 0, 0]
     scale = 1e-13 * np.abs(Fe).max()
     d = {k: np.abs(v - Fe).max() for k, v in out.items()}
     print(f"{cfg} N={s.N}: r_t {rt:.3f} (bound {tb:.2e}), r_far {rf:.3f} ({fb:.2e}), r_vfar {rv:.3f} ({vb:.2e}), "
-          f"L/2 {L / 2:.3f}; max_i |dF_i|: all {d[12, 13, 13]:.3e}, far only {d[0, 13, 0]:.3e}, very far only "
-          f"{d[0, 0, 13]:.3e}, tail only {d[12, 0, 0]:.3e}; max|F| {np.abs(Fe).max():.3e}")
-    assert d[12, 13, 13] <= tb + fb + vb + scale
-    assert d[0, 13, 0] <= fb + scale
-    assert d[0, 0, 13] <= vb + scale
-    assert d[12, 0, 0] <= tb + scale
+          f"r_ufar {ru:.3f} ({ub:.2e}), L/2 {L / 2:.3f}; max_i |dF_i|: all {d[12, 13, 13, 13]:.3e}, far only "
+          f"{d[0, 13, 0, 0]:.3e}, very far only {d[0, 0, 13, 0]:.3e}, ultra far only {d[0, 0, 0, 13]:.3e}, tail only "
+          f"{d[12, 0, 0, 0]:.3e}; max|F| {np.abs(Fe).max():.3e}")
+    assert d[12, 13, 13, 13] <= tb + fb + vb + ub + scale
+    assert d[0, 13, 0, 0] <= fb + scale
+    assert d[0, 0, 13, 0] <= vb + scale
+    assert d[0, 0, 0, 13] <= ub + scale
+    assert d[12, 0, 0, 0] <= tb + scale
     s.close()
     if cfg == "C5":                                    # r_t >= L/2 at C3 too: exact skipping only
         x = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C3"])
@@ -293,3 +299,17 @@ def test_raw_rsq_error_within_the_very_far_bound():
     raw = float(re.search(r"raw ([0-9.e+-]+)", out).group(1))
     print(out.strip())
     assert raw <= 2.0 ** -23
+
+
+@pytest.mark.gpu
+def test_exp2f_error_within_the_ultra_far_bound():
+    """The ultra-far pair form's bound assumes v_exp_f32 is within kExp2fRelErr = 2^-22 of 2^x
+    (mdqt_internal.hpp): tools/exp2f_precision measures it on 16M inputs over x in [-70, 0]"""
+    import re
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp2f_precision")
+    assert os.path.exists(exe), "tools/exp2f_precision missing: run __graft_entry__.build()"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
+    err = float(re.search(r"exp2f: ([0-9.e+-]+)", out).group(1))
+    print(out.strip())
+    assert err <= 2.0 ** -22

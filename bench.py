@@ -144,6 +144,15 @@ def pmc_traffic(kernel_prefix, path=None):
     cw = meta.get("write_factor", 1.0)
     src.update(status="ok", instance=name, fetch_kB=best["FETCH_SIZE"], write_kB=best["WRITE_SIZE"],
                fetch_factor=cf, write_factor=cw)
+    if all(k in best for k in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES")) and best["SQ_WAVES"]:
+        # the launch's issue picture from the same PMC summary: per wave, VALU and SALU instructions and
+        # its lifetime (SQ_WAVE_CYCLES counts quad-cycles); one instruction per wave issues every 4
+        # cycles at most, so (VALU + SALU) x 4 / lifetime is the wave's issue-slot occupancy
+        w = best["SQ_WAVES"]
+        life = best["SQ_WAVE_CYCLES"] * 4.0 / w
+        src["issue"] = {"valu_per_wave": best["SQ_INSTS_VALU"] / w, "salu_per_wave": best["SQ_INSTS_SALU"] / w,
+                        "wave_cycles": life,
+                        "issue_slot_frac": (best["SQ_INSTS_VALU"] + best["SQ_INSTS_SALU"]) / w * 4.0 / life}
     return (best["FETCH_SIZE"] / cf + best["WRITE_SIZE"] / cw) * 1024.0, src
 
 

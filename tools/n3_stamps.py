@@ -53,3 +53,11 @@ for kk, es in last.items():
     by.setdefault(len(es), []).append(max(es))
 for nwg, ends in sorted(by.items()):
     print(f"CUs with {nwg} WGs: {len(ends)}, last end pct 0/50/100:", np.percentile(ends, [0, 50, 100]).round(2))
+# dispatch order: start time against the workgroup index (the tile-pair list order)
+idx = np.arange(n)
+for q in range(0, n, max(n // 8, 1)):
+    sl = slice(q, min(q + n // 8, n))
+    print(f"blocks {q:5d}..{min(q + n // 8, n) - 1:5d}: start med {np.median(st[sl]):.2f} max {st[sl].max():.2f}  "
+          f"end med {np.median(en[sl]):.2f} max {en[sl].max():.2f}")
+os.makedirs("gpurun_out", exist_ok=True)
+np.save("gpurun_out/n3_stamps_raw.npy", a)

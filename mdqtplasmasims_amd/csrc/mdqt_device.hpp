@@ -162,6 +162,75 @@ __device__ __forceinline__ void sincos_q(double x, double& sn, double& cs) {
     sincos_fast(x, sn, cs);
 }
 
+// e^(ix) through a 64-entry table (the qt_math 2 kernels' coupling phase, round 3): x = m (2 pi/64)
+// + r by the same FMA Cody-Waite reduction (three-part constant), |r| <= pi/64, then
+// e^(ix) = e^(2 pi i (m mod 64)/64) e^(ir) with e^(ir) by its Taylor series (sin to r^9, cos to
+// r^8: truncation below 1e-20) and the table entries correctly rounded (60-digit decimal
+// arithmetic).  22 VALU and one LDS read instead of sincos_fast's ~40; <= 2 ulp.  |x| < 2^20 (the
+// callers take the library beyond).  `tab`: kSinCos64 (cos, sin pairs) in LDS or global memory.
+#ifndef MDQT_QT_SCTAB
+#define MDQT_QT_SCTAB 1
+#endif
+static __constant__ const double kSinCos64[128] = {
+    0x1.0000000000000p+0, 0x0.0p+0, 0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4,
+    0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3, 0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2,
+    0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2, 0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2,
+    0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1, 0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1,
+    0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1, 0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1,
+    0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1, 0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1,
+    0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1, 0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1,
+    0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1, 0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1,
+    0x1.84054757668f0p-192, 0x1.0000000000000p+0, -0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1,
+    -0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1, -0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1,
+    -0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1, -0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1,
+    -0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1, -0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1,
+    -0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1, -0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1,
+    -0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1, -0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2,
+    -0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2, -0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2,
+    -0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3, -0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4,
+    -0x1.0000000000000p+0, 0x1.7e0478355de7fp-191, -0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4,
+    -0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3, -0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2,
+    -0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2, -0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2,
+    -0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1, -0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1,
+    -0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1, -0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1,
+    -0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1, -0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1,
+    -0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1, -0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1,
+    -0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1, -0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1,
+    -0x1.2a033eb3aa9dbp-190, -0x1.0000000000000p+0, 0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1,
+    0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1, 0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1,
+    0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1, 0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1,
+    0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1, 0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1,
+    0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1, 0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1,
+    0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1, 0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2,
+    0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2, 0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2,
+    0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3, 0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4,
+};
+__device__ __forceinline__ void sincos_tab(double x, const double* tab, double& sn, double& cs) {
+    const double m = __builtin_rint(x * 0x1.45f306dc9c883p+3);      // 64 / (2 pi)
+    double r = fma(-m, 0x1.921fb54442d18p-4, x);                      // 2 pi / 64 = C1 + C2 + C3
+    r = fma(-m, 0x1.1a62633145c07p-58, r);
+    r = fma(-m, -0x1.f1976b7ed8fbcp-114, r);
+    const int j = (int)m & 63;
+    const double tc = tab[2 * j], ts = tab[2 * j + 1];
+    const double z = r * r;
+    const double sr = fma(r * z, hfma(z, hfma(z, hfma(z, 2.7557319223985893e-06, -1.9841269841269841e-04),
+                                               8.3333333333333332e-03), -1.6666666666666666e-01), r);
+    const double cr = hfma(z, hfma(z, hfma(z, hfma(z, 2.4801587301587302e-05, -1.3888888888888889e-03),
+                                         4.1666666666666664e-02), -0.5), 1.0);
+    sn = fma(ts, cr, tc * sr);
+    cs = fma(tc, cr, -(ts * sr));
+}
+// the qt_math 2 kernels' phase: the table form (MDQT_QT_SCTAB) or sincos_fast, the library for
+// |x| >= 2^20
+__device__ __forceinline__ void sincos_q2(double x, const double* tab, double& sn, double& cs) {
+    if (!(fabs(x) < 1048576.)) {
+        sincos(x, &sn, &cs);
+        return;
+    }
+    if (MDQT_QT_SCTAB) sincos_tab(x, tab, sn, cs);
+    else sincos_fast(x, sn, cs);
+}
+
 __device__ __forceinline__ double rho_im(cxd a, cxd b) {   // Im(a * conj(b)), SpeedUp:490-502
     return a.re * (-b.im) + a.im * b.re;
 }

@@ -263,6 +263,9 @@ __device__ __forceinline__ void slot_store(double* p, double v) {
 #ifndef MDQT_N3_CUT
 #define MDQT_N3_CUT 1
 #endif
+#ifndef MDQT_N3_PRIO
+#define MDQT_N3_PRIO 0
+#endif
 template <int VARIANT, bool GUARD, bool RAGGED, bool SIG, bool POT = false>
 __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, int J,
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
@@ -300,16 +303,37 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
     };
     const bool diag = I == J;
+    // progress priority (MDQT_N3_PRIO): a SIMD's VALU issue goes to the highest-priority wave, then
+    // the oldest, so without it the oldest of a SIMD's 6-7 co-resident waves run ahead and the last
+    // ones finish alone, latency-bound (stamps: workgroup end times rise with the dispatch order).
+    // Each wave lowers its priority as it advances through its steps (3, 2, 1, 0 per quarter): the
+    // waves behind are issued first, the co-resident waves progress together and the SIMD stays
+    // full to the end.
+    auto prio = [&](int t, int n) {
+        if constexpr (MDQT_N3_PRIO) {
+            if (t == 0) __builtin_amdgcn_s_setprio(3);         // (immediate operands: t is a
+            else if (t == n / 4) __builtin_amdgcn_s_setprio(2);   // constant of the unrolled loop)
+            else if (t == n / 2) __builtin_amdgcn_s_setprio(1);
+            else if (t == 3 * n / 4) __builtin_amdgcn_s_setprio(0);
+        }
+    };
     if (!diag) {
         const int b = l + (64 / N3W) * q;
 #pragma unroll
-        for (int t = 0; t < 64 / N3W; ++t) step(b + t, 1.);
+        for (int t = 0; t < 64 / N3W; ++t) {
+            prio(t, 64 / N3W);
+            step(b + t, 1.);
+        }
     } else {
         const int b = l + 1 + (32 / N3W) * q;
 #pragma unroll
-        for (int t = 0; t < 32 / N3W - 1; ++t) step(b + t, 1.);
+        for (int t = 0; t < 32 / N3W - 1; ++t) {
+            prio(t, 32 / N3W);
+            step(b + t, 1.);
+        }
         step(b + 32 / N3W - 1, (q == N3W - 1 && l >= 32) ? 0. : 1.);  // lane distance 32: once per pair
     }
+    if constexpr (MDQT_N3_PRIO) __builtin_amdgcn_s_setprio(0);
     ia[q][0][l] = fx; ia[q][1][l] = fy; ia[q][2][l] = fz;
     __syncthreads();
     const size_t slab3 = POT ? (size_t)S : (size_t)3 * S;   // potential: [ntiles][S], one plane per slot

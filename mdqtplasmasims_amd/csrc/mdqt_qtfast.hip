@@ -28,6 +28,7 @@ namespace mdqt {
 #endif
 constexpr int kLaneWG = MDQT_LANE_WG;
 static_assert(kLaneWG % 64 == 0 && kLaneWG <= 256, "lane kernel workgroup: whole waves, <= 256 threads");
+static_assert(!MDQT_QT_SCTAB || kLaneWG >= 128, "the sincos table is staged by the first 128 threads");
 // ions per wave of the lane kernels (diagnostic A/B builds only: MDQT_EXPT_ROWS 1 or 2 leave rows
 // of 16 lanes idle — they shadow another row's ion without storing — so that a launch has 4 / 2x
 // the waves at the same instructions per wave; the product keeps 4)
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void k_substeps_r(SubstepArgs a, const FastTab
             kick = sum_p<MODEL>(kv + 2);                 // the kick terms sit on the P lanes
             const double phi = (u * T.cphi) * tPart;
             double sn, cs;
-            sincos_q<true>(phi, sn, cs);
+            sincos_q2(phi, kSinCos64, sn, cs);
             cxd md[NS], c2[NS];
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
@@ -513,6 +514,9 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     // for every load issued before it, which would stall the Philox draws behind the slot loads)
     const double edv = (threadIdx.x < MAXSUB && a.expdet_zero == 0 && (int)threadIdx.x < a.nsub)
                            ? a.expDet[threadIdx.x] : 0.;
+    // the coupling phase's e^(2 pi i j / 64) table (sincos_tab) in LDS, written with edt below
+    __shared__ double sct[128];
+    const double sctv = (MDQT_QT_SCTAB && threadIdx.x < 128) ? kSinCos64[threadIdx.x] : 0.;
     // u1, u2 of every substep of the launch staged in LDS: Philox draws computed lane-parallel
     // (lane k: substeps k, k + 16), or the rng_mode 0 uniforms of the single substep
     __shared__ double su[kLaneWG / 16][MAXSUB][2];
@@ -572,6 +576,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         if (store && owner) qt_store(&a.F[(size_t)c * S + i], f);
     }
     if (threadIdx.x < MAXSUB) edt[threadIdx.x] = edv;
+    if (MDQT_QT_SCTAB && threadIdx.x < 128) sct[threadIdx.x] = sctv;
     __syncthreads();
     __shared__ double2 xg[DPPX ? 1 : kLaneWG];
     auto exchange = [&](cxd y, cxd& y0, cxd& y1, cxd& y2) {
@@ -609,7 +614,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         // + 0 and its LDS read dropped; the same values up to the sign of an exact zero)
         double u = EDZ ? v * qc.pv2q : v * qc.pv2q + edt[0];   // vx on every state lane (carried: the
         double tn = tPart + qc.dtQ;                   // next substep's is formed with its phase); tn:
-        sincos_q<true>((u * cphi) * tn, sn, cs);      // the next substep's tPart, formed once
+        sincos_q2((u * cphi) * tn, sct, sn, cs);      // the next substep's tPart, formed once
 #if defined(MDQT_EXPT_PHASEROT)
         double phi_c = (u * cphi) * tn;
 #endif
@@ -666,7 +671,8 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                     phi_c = phin;
                 }
 #else
-                sincos_fast(phin, snn, csn);
+                if (MDQT_QT_SCTAB) sincos_tab(phin, sct, snn, csn);
+                else sincos_fast(phin, snn, csn);
 #endif
             };
             if (nojump) {

@@ -412,7 +412,9 @@ __device__ unsigned long long g_md_stamps[4 * 4096];
 // IM01 (with FAST): the static coupling slots 0 and 1 are purely imaginary (QTConst::im01), their
 // real-part FMAs are dropped.  EDZ: every expDetuning of the launch is 0 (u = vx pv2q).  The
 // production model-0 launch is k_substeps_lanes_im<true, true> (FAST + IM01 + EDZ).
-template <bool DPPX, bool FAST, bool FUSED, bool IM01 = false, bool EDZ = false>
+// NORN: reNormalizewvFns is off (the reference's default, SpeedUp:74) — the renormalisation and
+// its uniform branch compiled out, so one substep's tail and the next one's head share a basic block
+template <bool DPPX, bool FAST, bool FUSED, bool IM01 = false, bool EDZ = false, bool NORN = false>
 __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTab* __restrict__ tab, int blk) {
 #if defined(MDQT_EXPT_QTSTAMPS)
     unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -503,6 +505,11 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         f = a.F[(size_t)c * S + i];
     }
     const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
+    // the substep loop's tPart step and Doppler factor held in VGPRs: with every SGPR taken the
+    // compiler otherwise re-loads them from the kernel arguments inside the loop, and the
+    // s_waitcnt on that scalar load stalls every substep
+    double dtq_v = qc.dtQ, pv2q_v = qc.pv2q;
+    asm volatile("" : "+v"(dtq_v), "+v"(pv2q_v));
     const uint64_t gid = a.gid0 + (uint64_t)i;
     // per-substep constants out of kernel-argument loads inside the substep loop (a scalar load
     // indexed by the substep waits ~100+ cycles in every iteration): the moving flags as a bit
@@ -612,8 +619,8 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
         double sn, cs;
         // (EDZ: every expDet of the launch is 0 — fracOfSig = 0, the default — so u = vx pv2q: the
         // + 0 and its LDS read dropped; the same values up to the sign of an exact zero)
-        double u = EDZ ? v * qc.pv2q : v * qc.pv2q + edt[0];   // vx on every state lane (carried: the
-        double tn = tPart + qc.dtQ;                   // next substep's is formed with its phase); tn:
+        double u = EDZ ? v * pv2q_v : v * pv2q_v + edt[0];     // vx on every state lane (carried: the
+        double tn = tPart + dtq_v;                    // next substep's is formed with its phase); tn:
         sincos_q2((u * cphi) * tn, sct, sn, cs);      // the next substep's tPart, formed once
 #if defined(MDQT_EXPT_PHASEROT)
         double phi_c = (u * cphi) * tn;
@@ -655,8 +662,8 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                     pn = adv ? pd : pn;
                     vn = adv ? vd : vn;
                 }
-                un = EDZ ? vn * qc.pv2q : vn * qc.pv2q + edt[s1];
-                tn = tPart + qc.dtQ;
+                un = EDZ ? vn * pv2q_v : vn * pv2q_v + edt[s1];
+                tn = tPart + dtq_v;
                 phin = (un * cphi) * tn;
 #if defined(MDQT_EXPT_PHASEROT)
                 {   // timing-only diagnostic: e^(i phin) = e^(i phi) e^(i dphi), short Taylor series of
@@ -731,7 +738,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                 next_phase();
             }
             if (!(fabs(phin) < 1048576.)) sincos(phin, &snn, &csn);
-            if (qc.renorm) w = [&] {                      // :706-712
+            if (!NORN && qc.renorm) w = [&] {             // :706-712
                 const double r = rsq_nr(lane_norm16(nrm2(w), one));
                 return cxd{w.re * r, w.im * r};
             }();
@@ -791,9 +798,9 @@ __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_r(SubstepA
     lane_substeps<DPPX, FAST, false>(a, tab, blockIdx.x);
 }
 // the FAST launch when QTConst::im01 (the production model-0 case); EDZ: expdet_zero
-template <bool DPPX, bool EDZ>
+template <bool DPPX, bool EDZ, bool NORN = false>
 __global__ __launch_bounds__(256) LANE_WPE_ATTR void k_substeps_lanes_im(SubstepArgs a, const FastTab* __restrict__ tab) {
-    lane_substeps<DPPX, true, false, true, EDZ>(a, tab, blockIdx.x);
+    lane_substeps<DPPX, true, false, true, EDZ, NORN>(a, tab, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -878,9 +885,15 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
 #ifndef MDQT_EDZ
 #define MDQT_EDZ 1
 #endif
+#ifndef MDQT_NORN
+#define MDQT_NORN 1
+#endif
         if (a.qc.model == 0) {
             if (allmove && a.qc.im01 && MDQT_IM01) {
-                if (a.expdet_zero && MDQT_EDZ) {
+                if (a.expdet_zero && MDQT_EDZ && !a.qc.renorm && MDQT_NORN) {   // the production launch
+                    launch_timed(k_substeps_lanes_im<true, true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
+                    inst = QTK_LANES_IM_EDZ;
+                } else if (a.expdet_zero && MDQT_EDZ) {
                     launch_timed(k_substeps_lanes_im<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
                     inst = QTK_LANES_IM_EDZ;
                 } else {

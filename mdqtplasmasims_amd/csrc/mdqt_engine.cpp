@@ -501,6 +501,14 @@ static void build_constants(mdqt_ctx* s) {
     // moves, col unused: self); the pumping models keep lane = state
     FastTab& fl = s->ftabL;
     fl = f;
+    // one substep's kick is the recoil (vKick or vKickDP) or the optical kick sum_j kw_j Im(w conj(w_j))
+    // over the P lanes, |w| |w_j| <= 16 taken generously
+    {
+        double kw = 0.;
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 16; ++k) kw += fabs(f.kw[j][k]);
+        q.kickmax = fmax(fabs(q.vKick), fabs(q.vKickDP)) + 16. * kw;
+    }
     q.im01 = 1;                                        // slots 0 and 1 purely imaginary (checked)
     for (int k = 0; k < 16; ++k)
         if (f.cre[0][k] != 0. || f.cre[1][k] != 0.) q.im01 = 0;

@@ -47,6 +47,8 @@ struct QTConst {
     double thS3, thS4;          // gs[2]^2, gs[4]^2 (S-decay target thresholds)
     double thD[4][2];           // cumulative D-decay thresholds per P level (:612-697)
     double gs[18];
+    double kickmax;             // bound on one substep's velocity kick (recoil or optical, model 0;
+                                // |w|, |w_c| <= 4): the lane kernel's coupling-phase bound
     int renorm;                 // reNormalizewvFns (:706-712)
     int im01;                   // host: every static M entry of the lane table's slots 0 and 1 is
                                 // purely imaginary (Re == +-0: -i h H with real couplings), so the

@@ -20,6 +20,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 namespace mdqt {
 
 // threads per workgroup of the lane-per-state kernels (16 lanes per ion)
@@ -628,7 +630,22 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
 #ifndef MDQT_QT_UNROLL
 #define MDQT_QT_UNROLL 2
 #endif
-        auto substep = [&](int s) {
+#ifndef MDQT_PHASE_BOUND
+#define MDQT_PHASE_BOUND 1
+#endif
+        // Wave-uniform bound on every coupling phase of the launch (production instance): |v| grows
+        // by at most |dt f| + kickmax per substep and tPart by dtQ, so when the bound on |phi| is
+        // below 2^19 the per-substep |phi| >= 2^20 library fallback cannot trigger and is left out
+        // of the loop (it would split every substep's tail from the next one's head into separate
+        // basic blocks); otherwise the loop keeps it.  The same values either way.
+        bool phase_small = false;
+        if constexpr (FAST && EDZ && DPPX && MDQT_PHASE_BOUND) {
+            const double vb = fabs(v) + (double)(a.nsub + 1) * (fabs(dt * f) + qc.kickmax);
+            const double tb = fabs(tPart) + (double)(a.nsub + 1) * dtq_v;
+            const double pb = ((vb * fabs(pv2q_v)) * fabs(cphi)) * tb;
+            phase_small = __builtin_amdgcn_ballot_w64(!(pb < 524288.)) == 0;
+        }
+        auto substep = [&](int s, auto chk) {
             tPart = tn;                               // tPart += dtQ (formed in the last next_phase)
             const double dp = DPPX ? lane_sum_p8(nrm2(w) * hdp, one) : lane_sum_p(nrm2(w) * hdp);
             const double u1 = su[grp][s][0], u2 = su[grp][s][1];
@@ -737,7 +754,8 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
                 w = {st == target ? 1. : 0., 0.};
                 next_phase();
             }
-            if (!(fabs(phin) < 1048576.)) sincos(phin, &snn, &csn);
+            if constexpr (decltype(chk)::value)
+                if (!(fabs(phin) < 1048576.)) sincos(phin, &snn, &csn);
             if (!NORN && qc.renorm) w = [&] {             // :706-712
                 const double r = rsq_nr(lane_norm16(nrm2(w), one));
                 return cxd{w.re * r, w.im * r};
@@ -748,16 +766,20 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
             sn = snn;
             cs = csn;
         };
-        if (MDQT_QT_UNROLL == 2) {                    // two substeps per iteration (register copies)
-            int s = 0;
-            for (; s + 1 < a.nsub; s += 2) {
-                substep(s);
-                substep(s + 1);
+        auto loop = [&](auto chk) {
+            if (MDQT_QT_UNROLL == 2) {                // two substeps per iteration (register copies)
+                int s = 0;
+                for (; s + 1 < a.nsub; s += 2) {
+                    substep(s, chk);
+                    substep(s + 1, chk);
+                }
+                if (s < a.nsub) substep(s, chk);
+            } else {
+                for (int s = 0; s < a.nsub; ++s) substep(s, chk);
             }
-            if (s < a.nsub) substep(s);
-        } else {
-            for (int s = 0; s < a.nsub; ++s) substep(s);
-        }
+        };
+        if (phase_small) loop(std::false_type{});
+        else loop(std::true_type{});
         if constexpr (FAST) {
             p = pre_p;
             v = pre_v;

@@ -454,6 +454,32 @@ def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra, qt_math):
         assert np.array_equal(a[k], b[k]), (k, jumped)
 
 
+def test_lane_kernel_large_phase_fallback_bit_identical(eng):
+    """coupling phases (SpeedUp:508) beyond the table reduction's 2^20 (an ion long without a
+    jump): the production lane instance's wave-uniform phase bound must send those waves through
+    the loop with the library fallback — bit-identical to the thread kernel, which checks every
+    substep; the waves whose bound holds run the loop without it"""
+    sims = []
+    for mode in (1, 2):
+        s = eng.Simulation(N0=3500, seed=31).init()
+        s.md_steps(2)
+        st = s.get_state()
+        tp = st["tPart"].copy()
+        tp[::97] += 3.0e6                          # a few ions per few waves: |phi| far above 2^20
+        s.set_state(st["R"], st["V"], st["psi"], tp, st["t"])
+        s.set_option("substep_kernel", mode)
+        s.md_steps(2)
+        if mode == 2:
+            assert s.const("qt_kernel") == QTK_LANES_IM_EDZ
+        sims.append((s.get_state(), tp, s.const("plasVelToQuantVel"), s.const("gamToEinsteinFreq")))
+    (a, tp, pv2q, g), (b, _, _, _) = sims
+    cphi = 2. * (1. + 0.395) * g                    # FastTab::cphi (kRat 0.395, SpeedUp:146)
+    phi = np.abs(a["V"][0] * pv2q * cphi * tp)
+    assert (phi > 2. ** 21).sum() >= 10            # the fallback ran for these ions
+    for k in ("R", "V", "psi", "tPart"):
+        assert np.array_equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("N0,extra,qt_math", [(300, {}, 0), (500, dict(Om=3.0, OmDP=2.0), 0), (3500, {}, 0),
                                               (500, dict(Om=3.0, OmDP=2.0), 2)])
 def test_drand48_reference_order_matches_oracle(eng, orc, N0, extra, qt_math):

@@ -757,6 +757,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     rf, far = sim.const("force_far_radius"), sim.const("force_far_bound")
     rv, vfar = sim.const("force_vfar_radius"), sim.const("force_vfar_bound")
     ru, ufar = sim.const("force_ufar_radius"), sim.const("force_ufar_bound")
+    ru32 = sim.const("force_ufar32_radius")
     sim.close()
     unit_steps = ratio if qt else 1
     f_avg = f_ms / max(nf, 1) * 1e-3
@@ -773,7 +774,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "scaling": "strong", "init_s": t_init, "force": force,
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail,
                            "far_radius": rf, "far_bound": far, "vfar_radius": rv, "vfar_bound": vfar,
-                           "ufar_radius": ru, "ufar_bound": ufar,
+                           "ufar_radius": ru, "ufar_bound": ufar, "ufar32_radius": ru32,
                            "note": "tile pairs >= skip_radius apart are skipped, tile pairs >= far_radius / vfar_radius "
                                    "apart take the far / very-far / ultra-far pair forms; every ion's force is "
                                    "within bound + far_bound + vfar_bound + ufar_bound of the exact sum to L/2 (mdqt_engine.cpp "

@@ -867,7 +867,14 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
         double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
                        ? far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound) : (bound = 0., s->L / 2.);
         if (r < s->L / 2. && s->L / 2. > 80. * s->lDeb) { r = s->L / 2.; bound = 0.; }
-        return n[11] == 'r' ? r : bound;
+        double b32 = 0.;                               // + the f32 shell beyond force_ufar32_radius
+        if (r < s->L / 2. && MDQT_UFAR32) far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 4, &b32);
+        return n[11] == 'r' ? r : bound + b32;
+    }
+    if (!strcmp(n, "force_ufar32_radius")) {          // the f32 ultra-far form's radius (L/2: off)
+        double bound;
+        const double r3 = mdqt_get_const(s, "force_ufar_radius");
+        return (r3 < s->L / 2. && MDQT_UFAR32) ? far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 4, &bound) : s->L / 2.;
     }
     if (!strcmp(n, "force_vfar_radius") || !strcmp(n, "force_vfar_bound")) {   // the very-far form's
         double bound;                                  // radius and force bound (0: off, r = L/2)
@@ -1122,6 +1129,7 @@ static double tail_radius(int N, double L, double lDeb, int k, double* bound) {
 // at distance r in the form (far: kFarRelErr; very far: (r/lDeb + 3) kRsqRawErr + kExp5RelErr) —
 // L/2 (= never) and bound 0 when k = 0 or that r is >= L/2; bound = (N - 1) g(r) err(r)
 static double far_err(double r, double lDeb, int level) {
+    if (level == 4) return (r / lDeb) * kUfar32A + kUfar32B;   // the f32 ultra-far form (MDQT_UFAR32)
     if (level == 3) return (r / lDeb) * (kRsqRawErr + 0x1p-24) + 3. * kRsqRawErr + kExp2fRelErr;
     return level == 2 ? (r / lDeb + 3.) * kRsqRawErr + kExp5RelErr : kFarRelErr;
 }
@@ -1130,7 +1138,10 @@ static double far_radius_l(int N, double L, double lDeb, int k, int level, doubl
     *bound = 0.;
     if (k <= 0 || N < 2) return Rcut;
     const double eps = pow(10., -k), n1 = (double)(N - 1);
-    auto b = [&](double r) { return n1 * tail_g(r, lDeb) * far_err(r, lDeb, level); };
+    // level 4 (f32) decides the cutoff on its f32 r^2 (relative error <= 6 2^-24): pairs within
+    // 3 2^-24 Rcut of L/2 may land on either side, each at most g(Rcut (1 - 2^-20)) — a constant term
+    const double cut = level == 4 ? n1 * tail_g(Rcut * (1. - 0x1p-20), lDeb) : 0.;
+    auto b = [&](double r) { return n1 * tail_g(r, lDeb) * far_err(r, lDeb, level) + cut; };
     if (b(Rcut) > eps) return Rcut;
     double lo = 0., hi = Rcut;
     for (int it = 0; it < 200 && hi - lo > 1e-12 * Rcut; ++it) {
@@ -1158,8 +1169,11 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.Rfar = far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound);
     a.Rvfar = far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound);
     a.Rufar = far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound);
+    a.Rufar32 = MDQT_UFAR32 ? far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 4, &bound) : a.Rcut;
+    a.rc2 = a.Rcut * a.Rcut;
     // f32's normal range: 2^t for t >= -126 (r <= 126 lDeb ln2 = 87 lDeb); never beyond it
     if (a.Rufar < a.Rcut && a.Rcut > 80. * s->lDeb) a.Rufar = a.Rcut;
+    if (a.Rufar >= a.Rcut) a.Rufar32 = a.Rcut;
     if (s->sort_mode) {                            // Hilbert order + tile boxes (mdqt_sort.hip)
         SortArgs o;
         o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;

@@ -281,6 +281,47 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
 #undef N3B_REBASE
 }
 
+__device__ __forceinline__ float wave_rol1f(float v) {   // lane l <- lane (l + 1) mod 64
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xF, 0xF, false));
+}
+
+// An ultra-far tile pair (boxes >= r_ufar32 apart) with a uniform image, pair terms in f32
+// (MDQT_UFAR32; error analysis and bound in mdqt_internal.hpp kUfar32A/B): dx = fl32(xi - n L - xj)
+// from the f64 separation, v_rsq_f32, 2^t by v_exp_f32, the cutoff on the f32 r^2 (t = -inf).  Per 16-step group the i side is summed in f32 registers and then added to the
+// f64 partial, and the j side runs as MDQT_N3B_JCOMB does (the running sum rotated one lane down
+// each step, wave_rol:1 folded into the f32 add: lane l + 1's sum of the previous step has lane l's
+// current J index) and ends in one ds_add_f64 per component at the group's last index.  Off the
+// diagonal only (a tile's pair with itself is never ultra far).
+__device__ __forceinline__ void n3b_pair_uf32(int l, double xi, double yi, double zi, const double (*pj)[128],
+                                              double* ax, double* ay, double* az, double& fx, double& fy,
+                                              double& fz, float cf, float invlf, float rc2f) {
+    for (int t0 = 0; t0 < 64; t0 += 16) {
+        int b_ = l + t0;
+        asm volatile("" : "+v"(b_));                // immediate LDS offsets (N3B_REBASE)
+        const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);
+        float ix = 0.f, iy = 0.f, iz = 0.f, jx = 0.f, jy = 0.f, jz = 0.f;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const float dx = (float)(xi - pjb[0][t]), dy = (float)(yi - pjb[1][t]), dz = (float)(zi - pjb[2][t]);
+            const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+            const float ri = __builtin_amdgcn_rsqf(r2);
+            const float e = __builtin_amdgcn_exp2f(r2 < rc2f ? (r2 * ri) * cf : -INFINITY);
+            const float ft = ((ri + invlf) * e) * (ri * ri);
+            const float px = dx * ft, py = dy * ft, pz = dz * ft;
+            ix += px; iy += py; iz += pz;
+            if (t == 0) {
+                jx = px; jy = py; jz = pz;
+            } else {
+                jx = wave_rol1f(jx) + px; jy = wave_rol1f(jy) + py; jz = wave_rol1f(jz) + pz;
+            }
+        }
+        __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        fx += (double)ix; fy += (double)iy; fz += (double)iz;
+    }
+}
+
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
 template <int VARIANT, bool GUARD, bool POT = false>
 // the fast variant fits 64 VGPRs (8 waves per SIMD); the exact one (libm exp, divisions) gets 128
@@ -294,7 +335,7 @@ void k_pairs_n3b(N3BArgs a) {
     const int P = a.Plo + (int)blockIdx.x / a.R;
     const int run = (int)blockIdx.x % a.R;
     const int d0 = run * a.runlen, d1 = min(a.nd, d0 + a.runlen);
-    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L};
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
     const int T = a.T, N = a.N, S = a.S;
     const bool ragN = (N & 63) != 0;
     const int I = P * BW + q;
@@ -320,13 +361,16 @@ void k_pairs_n3b(N3BArgs a) {
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
     // class: -1 skip; otherwise bit 0 = uniform image, + 2 x the far level (1 far pair form, 2 very
-    // far, 3 ultra far; forces only): 0 .. 7
+    // far, 3 ultra far, 4 ultra far in f32; forces only): 0 .. 9
     __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class
     // skip below the cutoff only for the forces (error-bounded tail, mdqt_engine.cpp tail_radius)
     const double rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
     const double rf2 = (POT || VARIANT != 1 || !(a.Rfar < a.Rcut)) ? INFINITY : a.Rfar * a.Rfar;
     const double rv2 = (POT || VARIANT != 1 || !(a.Rvfar < a.Rcut)) ? INFINITY : a.Rvfar * a.Rvfar;
     const double ru2 = (POT || VARIANT != 1 || !(a.Rufar < a.Rcut)) ? INFINITY : a.Rufar * a.Rufar;
+    const double ru32 = (POT || VARIANT != 1 || !MDQT_UFAR32 || !(a.Rufar32 < a.Rcut)) ? INFINITY
+                                                                                      : a.Rufar32 * a.Rufar32;
+    const float cf32 = (float)(a.invlDeb * kNegLog2e), invl32 = (float)a.invlDeb, rc2f = (float)a.rc2;
     auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
         const double* B = a.boxes;
         double g2 = 0.;
@@ -346,7 +390,8 @@ void k_pairs_n3b(N3BArgs a) {
         }
         const double cls = (a.use_sort == 1 && g2 > rc2) ? -1.
                                                           : ((VARIANT == 1 && uni) ? 1. : 0.) +
-                                                                (g2 > ru2 ? 6. : g2 > rv2 ? 4. : g2 > rf2 ? 2. : 0.);
+                                                                (g2 > ru32 ? 8. : g2 > ru2 ? 6. : g2 > rv2 ? 4. :
+                                                                 g2 > rf2 ? 2. : 0.);
         return make_double4(n[0], n[1], n[2], cls);
     };
     // the run's i accumulator lives in LDS (read and written once per block distance) so that
@@ -377,7 +422,7 @@ void k_pairs_n3b(N3BArgs a) {
                     const double4 t4 = classify(P * BW + l, J);
                     tp[l][0] = t4.x; tp[l][1] = t4.y; tp[l][2] = t4.z; tp[l][3] = t4.w;
 #if defined(MDQT_EXPT_CLS)
-                    atomicAdd(&g_cls_count[(int)t4.w + 1], 1ull);
+                    atomicAdd(&g_cls_count[t4.w < 0. ? 0 : 1 + ((int)t4.w & 1)], 1ull);
 #endif
                 }
             }
@@ -387,6 +432,8 @@ void k_pairs_n3b(N3BArgs a) {
             const double cls = srt ? uniform_f64(tp[q][3]) : 0.;
             if (vI && (db > 0 || J >= I) && cls >= 0.) {
                 const bool diag = (db == 0 && J == I);
+                const int ci = (int)cls;            // bit 0 uniform image, bits 1-3 far level
+                const int fl = ci >> 1;
                 // blocked i accumulation: the tile pair's 64 steps into a fresh sum, those into the
                 // block distance's sum, those into the run's (a run is ~1e5 pair terms at N = 1e6;
                 // in spatial order they arrive in coherent groups, and one serial chain would
@@ -396,20 +443,25 @@ void k_pairs_n3b(N3BArgs a) {
                 if (ragN && (I == T - 1 || J == T - 1))
                     n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
                                                                     tz, c);
-                else if (VARIANT == 1 && (cls == 1. || cls == 3. || cls == 5. || cls == 7.)) {
+                else if (VARIANT == 1 && (ci & 1)) {       // uniform image
                     const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
                     // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
                     const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
                     const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
                     const double sz = MDQT_SHIFT_I ? fma(-nsh[2], a.L, zi) : zi;
                     if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                        if (cls == 7.)              // ultra far tile pair
+                        if (fl == 4) {              // ultra far in f32
+#if !defined(MDQT_EXPT_UFAR_SKIP)                   // (diagnostic build: skip them, wrong results)
+                            n3b_pair_uf32(l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
+#endif
+                        }
+                        else if (fl == 3)           // ultra far tile pair
                             n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
                                                                                az, tx, ty, tz, c, nsh);
-                        else if (cls == 5.)         // very far tile pair
+                        else if (fl == 2)           // very far tile pair
                             n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
                                                                                az, tx, ty, tz, c, nsh);
-                        else if (cls == 3.)         // far tile pair: the far pair form
+                        else if (fl == 1)           // far tile pair: the far pair form
                             n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 1>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
                                                                                az, tx, ty, tz, c, nsh);
                         else
@@ -420,10 +472,10 @@ void k_pairs_n3b(N3BArgs a) {
                                                                                 ay, az, tx, ty, tz, c, nsh);
                     }
                 } else if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                    if (cls >= 4.)                  // (ultra far with a per-pair image: rare, very-far form)
+                    if (fl >= 2)                    // (ultra far with a per-pair image: rare, very-far form)
                         n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                             az, tx, ty, tz, c);
-                    else if (cls == 2.)
+                    else if (fl == 1)
                         n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                             az, tx, ty, tz, c);
                     else

@@ -276,6 +276,25 @@ constexpr double kExp5RelErr = 1.1e-7;
 // kExp2fRelErr of itself (kExp2fRelErr: twice what tools/exp2f_precision measures, re-checked by a
 // GPU test).  f32's range holds 2^t down to t = -126: r <= 87 lDeb, beyond every L/2 it serves.
 constexpr double kExp2fRelErr = 0x1p-22;
+// The ultra-far tier in f32 (MDQT_UFAR32, round 3): a uniform-image tile pair whose boxes are
+// >= r_ufar32 apart evaluates its pair terms in f32 from the f64 separations: dx = fl32(xi - xj),
+// r^2 by f32 FMAs, v_rsq_f32 (<= kRsqF32RelErr = 1 ulp, measured by tools/rsq_precision and a GPU
+// test), t = (r^2 ri) cf with cf = fl32(-log2(e)/lDeb), v_exp_f32, then the force factor and the
+// three products in f32; the i side summed in f32 over 16 steps, then in f64; the j side rotated
+// along the wave over the same 16 steps (one ds_add_f64 per component).  Per term, to first order in
+// u = 2^-24: dx u, r^2 5u, ri 2u + 2.5u, r 10.5u, t 12.5u — so 2^t is within (r/lDeb) 12.5u +
+// kExp2fRelErr — the force factor 17.5u more, the product 2u; each 16-term f32 sum adds 15u: a term
+// is within (r/lDeb) 13u + 40u of itself (kUfar32A, kUfar32B, rounded up).  The cutoff is decided on
+// the f32 r^2 (<= 6u off): pairs within 3u Rcut of L/2 may land on either side, each at most
+// g(Rcut (1 - 2^-20)) — so far_radius_l's level 4 bounds every ion by (N - 1) g(r) err(r) +
+// (N - 1) g(Rcut (1 - 2^-20)), and the tier is off where that cannot meet 10^-k (C5: N g(L/2) is
+// ~1e-8; N = 1e6 at C2's parameters: ~5e-16).
+#ifndef MDQT_UFAR32
+#define MDQT_UFAR32 1
+#endif
+constexpr double kRsqF32RelErr = 0x1p-23;
+constexpr double kUfar32A = 13. * 0x1p-24;
+constexpr double kUfar32B = 40. * 0x1p-24;
 __device__ __forceinline__ double exp2_neg_cut5(double t, bool keep) {
     const double n = __builtin_rint(t);
     const double f = t - n;
@@ -396,6 +415,9 @@ struct N3BArgs {
                         // forces only, use_sort 1 or 2); >= Rcut: never
     double Rvfar;       // >= Rvfar apart: the very-far form (raw rsq, degree-5 2^f); >= Rcut: never
     double Rufar;       // >= Rufar apart: the ultra-far form (raw rsq, v_exp_f32); >= Rcut: never
+    double Rufar32;     // >= Rufar32 apart (uniform image): the ultra-far form in f32 (MDQT_UFAR32)
+    double rc2;         // Rcut^2: the very-far and ultra-far forms keep a pair iff r^2 < rc2 (r^2 in f64,
+                        // as exact as the exact form's r < Rcut), not on their low-precision r
     double Rskip;       // force tile pairs whose boxes are >= Rskip apart are skipped (use_sort 1):
                         // Rcut exactly (every skipped pair is beyond L/2), or the error-bounded tail
                         // radius r_t < L/2 of mdqt_engine.cpp tail_radius (potentials: always Rcut)

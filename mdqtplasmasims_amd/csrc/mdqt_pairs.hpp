@@ -105,7 +105,8 @@ __device__ __forceinline__ double pair_ft_cut_far(double dx, double dy, double d
     return ((ri + c.invlDeb) * exp2_neg_cut6(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
 }
 
-// pair_ft_cut of a very far tile pair: the raw v_rsq_f64 and the degree-5 2^f (mdqt_internal.hpp)
+// pair_ft_cut of a very far tile pair: the raw v_rsq_f64 and the degree-5 2^f (mdqt_internal.hpp);
+// the cutoff on r^2 (c.rc2 = Rcut^2), not on the raw rsq's r (2^-23: pairs at L/2 would flip)
 __device__ __forceinline__ double pair_ft_cut_vfar(double dx, double dy, double dz, const PairC& c) {
     const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -114,7 +115,7 @@ __device__ __forceinline__ double pair_ft_cut_vfar(double dx, double dy, double 
     const double ri = 1. / sqrt(r2);
 #endif
     const double dr = r2 * ri;
-    return ((ri + c.invlDeb) * exp2_neg_cut5(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
+    return ((ri + c.invlDeb) * exp2_neg_cut5(dr * (c.invlDeb * kNegLog2e), r2 < c.rc2)) * (ri * ri);
 }
 
 // pair_ft_cut of an ultra-far tile pair: the raw v_rsq_f64 and 2^t by v_exp_f32 (t rounded to
@@ -127,7 +128,7 @@ __device__ __forceinline__ double pair_ft_cut_ufar(double dx, double dy, double 
     const double ri = 1. / sqrt(r2);
 #endif
     const double dr = r2 * ri;
-    const float tf = dr < c.Rcut ? (float)(dr * (c.invlDeb * kNegLog2e)) : -INFINITY;
+    const float tf = r2 < c.rc2 ? (float)(dr * (c.invlDeb * kNegLog2e)) : -INFINITY;   // (as vfar)
 #if defined(__HIP_DEVICE_COMPILE__)
     const double e = (double)__builtin_amdgcn_exp2f(tf);
 #else

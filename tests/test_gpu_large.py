@@ -169,8 +169,9 @@ def test_error_bounded_tail_and_far_form(cfg):
     rf, fb = s.const("force_far_radius"), s.const("force_far_bound")
     rv, vb = s.const("force_vfar_radius"), s.const("force_vfar_bound")
     ru, ub = s.const("force_ufar_radius"), s.const("force_ufar_bound")
+    ru32 = s.const("force_ufar32_radius")             # the f32 ultra-far shell (its bound is in ub)
     assert 0 < fb <= 1e-13 and rf < L / 2 and 0 < vb <= 1e-13 and rf < rv < L / 2
-    assert 0 < ub <= 1e-13 and rf < ru < L / 2
+    assert 0 < ub <= 2e-13 and rf < ru < L / 2 and ru <= ru32 <= L / 2   # ub: f64 + f32 shells, 1e-13 each
     assert (0 < tb <= 1e-12 and rt < L / 2) if cfg == "C4" else (tb == 0 and rt == L / 2)
     out = {}
     for te, fe, ve, ue in ((12, 13, 13, 13), (0, 13, 0, 0), (0, 0, 13, 0), (0, 0, 0, 13), (12, 0, 0, 0),
@@ -187,7 +188,7 @@ def test_error_bounded_tail_and_far_form(cfg):
     scale = 1e-13 * np.abs(Fe).max()
     d = {k: np.abs(v - Fe).max() for k, v in out.items()}
     print(f"{cfg} N={s.N}: r_t {rt:.3f} (bound {tb:.2e}), r_far {rf:.3f} ({fb:.2e}), r_vfar {rv:.3f} ({vb:.2e}), "
-          f"r_ufar {ru:.3f} ({ub:.2e}), L/2 {L / 2:.3f}; max_i |dF_i|: all {d[12, 13, 13, 13]:.3e}, far only "
+          f"r_ufar {ru:.3f} ({ub:.2e}), r_ufar32 {ru32:.3f}, L/2 {L / 2:.3f}; max_i |dF_i|: all {d[12, 13, 13, 13]:.3e}, far only "
           f"{d[0, 13, 0, 0]:.3e}, very far only {d[0, 0, 13, 0]:.3e}, ultra far only {d[0, 0, 0, 13]:.3e}, tail only "
           f"{d[12, 0, 0, 0]:.3e}; max|F| {np.abs(Fe).max():.3e}")
     assert d[12, 13, 13, 13] <= tb + fb + vb + ub + scale
@@ -297,8 +298,10 @@ def test_raw_rsq_error_within_the_very_far_bound():
     assert os.path.exists(exe), "tools/rsq_precision missing: run __graft_entry__.build()"
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
     raw = float(re.search(r"raw ([0-9.e+-]+)", out).group(1))
+    f32 = float(re.search(r"rsq_f32: ([0-9.e+-]+)", out).group(1))
     print(out.strip())
     assert raw <= 2.0 ** -23
+    assert f32 <= 2.0 ** -23                         # kRsqF32RelErr: the f32 ultra-far form's bound
 
 
 @pytest.mark.gpu

@@ -1,9 +1,15 @@
 // v_rsq_f64 precision probe: max relative error of the raw instruction and after one and two
-// Newton steps, against a long-double reference computed on the host.
+// Newton steps, against a long-double reference computed on the host; and v_rsq_f32 on the same
+// inputs rounded to float (the f32 ultra-far pair form's kRsqF32RelErr, mdqt_internal.hpp).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+
+__global__ void kf(const float* x, float* r, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) r[i] = __builtin_amdgcn_rsqf(x[i]);
+}
 
 __global__ void k(const double* x, double* r0, double* r1, double* r2, double* r3, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -44,6 +50,17 @@ int main() {
         e3 = fmaxl(e3, fabsl(h3[i] / ref - 1));
     }
     printf("third-order step: %.3Le (2^%.1f)\n", e3, (double)log2l(e3));
+    {
+        float *xf = (float*)malloc(n * 4), *hf = (float*)malloc(n * 4), *dxf, *drf;
+        for (int i = 0; i < n; ++i) xf[i] = (float)x[i];
+        hipMalloc(&dxf, n * 4); hipMalloc(&drf, n * 4);
+        hipMemcpy(dxf, xf, n * 4, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(kf, dim3(n / 256), dim3(256), 0, 0, dxf, drf, n);
+        hipMemcpy(hf, drf, n * 4, hipMemcpyDeviceToHost);
+        long double ef = 0;
+        for (int i = 0; i < n; ++i) ef = fmaxl(ef, fabsl(hf[i] * sqrtl((long double)xf[i]) - 1));
+        printf("rsq_f32: %.3Le (2^%.1f)\n", ef, (double)log2l(ef));
+    }
     printf("max rel err: raw %.3Le (2^%.1f)  1 NR %.3Le (2^%.1f)  2 NR %.3Le (2^%.1f)\n", e0, (double)log2l(e0), e1,
            (double)log2l(e1), e2, (double)log2l(e2));
     return 0;

@@ -281,6 +281,9 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
 #undef N3B_REBASE
 }
 
+#ifndef MDQT_UFAR32_PK
+#define MDQT_UFAR32_PK 0   // packed f32 (v_pk_*): measured slower at N = 1M (329.6-330.5 vs 325.6-327.2 ms, A/B)
+#endif
 __device__ __forceinline__ float wave_rol1f(float v) {   // lane l <- lane (l + 1) mod 64
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xF, 0xF, false));
 }
@@ -300,6 +303,34 @@ __device__ __forceinline__ void n3b_pair_uf32(int l, double xi, double yi, doubl
         asm volatile("" : "+v"(b_));                // immediate LDS offsets (N3B_REBASE)
         const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);
         float ix = 0.f, iy = 0.f, iz = 0.f, jx = 0.f, jy = 0.f, jz = 0.f;
+#if MDQT_UFAR32_PK
+        // two steps per iteration in packed f32 (v_pk_mul/add/fma_f32: two lanes' worth per
+        // instruction); the i side in two interleaved sums, combined at the group's end
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 ix2 = {0.f, 0.f}, iy2 = {0.f, 0.f}, iz2 = {0.f, 0.f};
+        const f2 cf2 = {cf, cf}, il2 = {invlf, invlf};
+#pragma unroll
+        for (int t = 0; t < 16; t += 2) {
+            const f2 dx = {(float)(xi - pjb[0][t]), (float)(xi - pjb[0][t + 1])};
+            const f2 dy = {(float)(yi - pjb[1][t]), (float)(yi - pjb[1][t + 1])};
+            const f2 dz = {(float)(zi - pjb[2][t]), (float)(zi - pjb[2][t + 1])};
+            const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
+            const f2 ri = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
+            const f2 tt = (r2 * ri) * cf2;
+            const f2 e = {__builtin_amdgcn_exp2f(r2.x < rc2f ? tt.x : -INFINITY),
+                          __builtin_amdgcn_exp2f(r2.y < rc2f ? tt.y : -INFINITY)};
+            const f2 ft = ((ri + il2) * e) * (ri * ri);
+            const f2 px = dx * ft, py = dy * ft, pz = dz * ft;
+            ix2 += px; iy2 += py; iz2 += pz;
+            if (t == 0) {
+                jx = px.x; jy = py.x; jz = pz.x;
+            } else {
+                jx = wave_rol1f(jx) + px.x; jy = wave_rol1f(jy) + py.x; jz = wave_rol1f(jz) + pz.x;
+            }
+            jx = wave_rol1f(jx) + px.y; jy = wave_rol1f(jy) + py.y; jz = wave_rol1f(jz) + pz.y;
+        }
+        ix = ix2.x + ix2.y; iy = iy2.x + iy2.y; iz = iz2.x + iz2.y;
+#else
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const float dx = (float)(xi - pjb[0][t]), dy = (float)(yi - pjb[1][t]), dz = (float)(zi - pjb[2][t]);
@@ -315,6 +346,7 @@ __device__ __forceinline__ void n3b_pair_uf32(int l, double xi, double yi, doubl
                 jx = wave_rol1f(jx) + px; jy = wave_rol1f(jy) + py; jz = wave_rol1f(jz) + pz;
             }
         }
+#endif
         __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);

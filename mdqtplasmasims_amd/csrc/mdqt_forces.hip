@@ -102,12 +102,14 @@ __global__ __launch_bounds__(64 * N3W) void k_pairs_n3(N3Args a) {
     __shared__ double accj[N3W][3][128];
     __shared__ double ia[N3W][3][64];
     __shared__ double mj[128];
+    __shared__ double etab[64];
 #if defined(MDQT_EXPT_STAMPS)
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
+    stage_exp_tab(etab);
     const int2 IJ = a.pairs[blockIdx.x];
-    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2, etab};
     const bool rag = (a.N & 63) && IJ.y == a.ntiles - 1;
     if (a.arrive) {
         if (rag) n3_tile<VARIANT, GUARD, true, true>(a, c, IJ.x, IJ.y, pj, accj, mj, ia);
@@ -363,11 +365,13 @@ void k_pairs_n3b(N3BArgs a) {
     __shared__ double mj[128];
     __shared__ double accj[BW][3][128];
     __shared__ double irun[BW][3][64];
+    __shared__ double etab[64];
+    stage_exp_tab(etab);
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;   // q: wave-uniform
     const int P = a.Plo + (int)blockIdx.x / a.R;
     const int run = (int)blockIdx.x % a.R;
     const int d0 = run * a.runlen, d1 = min(a.nd, d0 + a.runlen);
-    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2};
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2, etab};
     const int T = a.T, N = a.N, S = a.S;
     const bool ragN = (N & 63) != 0;
     const int I = P * BW + q;

@@ -10,7 +10,53 @@ namespace mdqt {
 struct PairC {
     double L, T, G, Rcut, lDeb, invlDeb, invL;
     double rc2;         // VARIANT 2: pair kept iff r2 < rc2 (= sqrt(r2) < Rcut exactly)
+    const double* etab; // the Newton-3 kernels' 2^(j/64) table in LDS (pair_ft_cut, MDQT_EXP_TAB)
 };
+
+// 2^t of the Newton-3 kernels' exact pair form by a 64-entry table (round 3, MDQT_EXP_TAB):
+// t64 = 64 t (the multiplier scaled by 64: exact), m = rint(t64), g = t64 - m (exact, |g| <= 1/2),
+// 2^t = 2^(m >> 6) 2^((m & 63)/64) 2^(g/64) with the table entry correctly rounded (60-digit decimal
+// arithmetic) and 2^(g/64) = e^(g ln2/64) by its degree-5 Taylor series (|g ln2/64| <= 0.0055:
+// truncation 3.5e-17); <= 2 ulp.  Five FMAs instead of eleven for three integer operations and one
+// LDS read; the cutoff folded into the exponent as in exp2_neg_cut.
+#ifndef MDQT_EXP_TAB
+#define MDQT_EXP_TAB 0   // A/B (round 3): C2 MD step -0.2 us, C5 -2 %, N = 1M +7 % (block-kernel spills): off
+#endif
+static __constant__ const double kExp2Tab64[64] = {
+    0x1.0000000000000p+0, 0x1.02c9a3e778061p+0, 0x1.059b0d3158574p+0, 0x1.0874518759bc8p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0e3ec32d3d1a2p+0, 0x1.11301d0125b51p+0, 0x1.1429aaea92de0p+0,
+    0x1.172b83c7d517bp+0, 0x1.1a35beb6fcb75p+0, 0x1.1d4873168b9aap+0, 0x1.2063b88628cd6p+0,
+    0x1.2387a6e756238p+0, 0x1.26b4565e27cddp+0, 0x1.29e9df51fdee1p+0, 0x1.2d285a6e4030bp+0,
+    0x1.306fe0a31b715p+0, 0x1.33c08b26416ffp+0, 0x1.371a7373aa9cbp+0, 0x1.3a7db34e59ff7p+0,
+    0x1.3dea64c123422p+0, 0x1.4160a21f72e2ap+0, 0x1.44e086061892dp+0, 0x1.486a2b5c13cd0p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4f9b2769d2ca7p+0, 0x1.5342b569d4f82p+0, 0x1.56f4736b527dap+0,
+    0x1.5ab07dd485429p+0, 0x1.5e76f15ad2148p+0, 0x1.6247eb03a5585p+0, 0x1.6623882552225p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6dfb23c651a2fp+0, 0x1.71f75e8ec5f74p+0, 0x1.75feb564267c9p+0,
+    0x1.7a11473eb0187p+0, 0x1.7e2f336cf4e62p+0, 0x1.82589994cce13p+0, 0x1.868d99b4492edp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8f1ae99157736p+0, 0x1.93737b0cdc5e5p+0, 0x1.97d829fde4e50p+0,
+    0x1.9c49182a3f090p+0, 0x1.a0c667b5de565p+0, 0x1.a5503b23e255dp+0, 0x1.a9e6b5579fdbfp+0,
+    0x1.ae89f995ad3adp+0, 0x1.b33a2b84f15fbp+0, 0x1.b7f76f2fb5e47p+0, 0x1.bcc1e904bc1d2p+0,
+    0x1.c199bdd85529cp+0, 0x1.c67f12e57d14bp+0, 0x1.cb720dcef9069p+0, 0x1.d072d4a07897cp+0,
+    0x1.d5818dcfba487p+0, 0x1.da9e603db3285p+0, 0x1.dfc97337b9b5fp+0, 0x1.e502ee78b3ff6p+0,
+    0x1.ea4afa2a490dap+0, 0x1.efa1bee615a27p+0, 0x1.f50765b6e4540p+0, 0x1.fa7c1819e90d8p+0,
+};
+__device__ __forceinline__ double exp2_neg_cut_tab(double t64, bool keep, const double* tab) {
+    const double m = __builtin_rint(t64);
+    const double g = t64 - m;
+    const int mi = (int)m;
+    double p = 0x1.5d87fe78a6731p-40;
+    p = fma(p, g, 0x1.3b2ab6fba4e77p-31);
+    p = fma(p, g, 0x1.c6b08d704a0c0p-23);
+    p = fma(p, g, 0x1.ebfbdff82c58fp-15);
+    p = fma(p, g, 0x1.62e42fefa39efp-7);
+    p = fma(p, g, 1.0);
+    return ldexp(p * tab[mi & 63], keep ? (mi >> 6) : -1100);
+}
+// stage the table (threads 0..63 of the workgroup; before the kernel's first barrier)
+__device__ __forceinline__ void stage_exp_tab(double* etab) {
+    if (MDQT_EXP_TAB && threadIdx.x < 64) etab[threadIdx.x] = kExp2Tab64[threadIdx.x];
+    (void)etab;
+}
 
 __device__ __forceinline__ const double* pos_base(const double* Rall, int g, int S) {
     const int w = g / S;
@@ -94,6 +140,9 @@ __device__ __forceinline__ double pair_ft_cut(double dx, double dy, double dz, c
     const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
     const double ri = rsq3(r2);
     const double dr = r2 * ri;
+    if constexpr (MDQT_EXP_TAB)
+        return ((ri + c.invlDeb) * exp2_neg_cut_tab(dr * (c.invlDeb * (64. * kNegLog2e)), dr < c.Rcut, c.etab)) *
+               (ri * ri);
     return ((ri + c.invlDeb) * exp2_neg_cut(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
 }
 

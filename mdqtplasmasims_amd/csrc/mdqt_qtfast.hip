@@ -855,8 +855,10 @@ __global__ __launch_bounds__(256) void k_md_step(N3Args f, SubstepArgs a, const 
         __shared__ double accj[N3W][3][128];
         __shared__ double ia[N3W][3][64];
         __shared__ double mj[128];
+        __shared__ double etab[64];
+        stage_exp_tab(etab);
         const int2 IJ = f.pairs[blockIdx.x];
-        const PairC c = {f.L, f.micT, f.micGuard, f.Rcut, f.lDeb, f.invlDeb, 1. / f.L, f.rc2};
+        const PairC c = {f.L, f.micT, f.micGuard, f.Rcut, f.lDeb, f.invlDeb, 1. / f.L, f.rc2, etab};
         const bool rag = (f.N & 63) && IJ.y == f.ntiles - 1;
         if (rag) n3_tile<VARIANT, false, true, true>(f, c, IJ.x, IJ.y, pj, accj, mj, ia);
         else n3_tile<VARIANT, false, false, true>(f, c, IJ.x, IJ.y, pj, accj, mj, ia);

@@ -341,10 +341,11 @@ __device__ __forceinline__ void n3b_pair_uf32(int l, double xi, double yi, doubl
             const float e = __builtin_amdgcn_exp2f(r2 < rc2f ? (r2 * ri) * cf : -INFINITY);
             const float ft = ((ri + invlf) * e) * (ri * ri);
             const float px = dx * ft, py = dy * ft, pz = dz * ft;
-            ix += px; iy += py; iz += pz;
             if (t == 0) {
+                ix = px; iy = py; iz = pz;
                 jx = px; jy = py; jz = pz;
             } else {
+                ix += px; iy += py; iz += pz;
                 jx = wave_rol1f(jx) + px; jy = wave_rol1f(jy) + py; jz = wave_rol1f(jz) + pz;
             }
         }
@@ -406,7 +407,11 @@ void k_pairs_n3b(N3BArgs a) {
     const double ru2 = (POT || VARIANT != 1 || !(a.Rufar < a.Rcut)) ? INFINITY : a.Rufar * a.Rufar;
     const double ru32 = (POT || VARIANT != 1 || !MDQT_UFAR32 || !(a.Rufar32 < a.Rcut)) ? INFINITY
                                                                                       : a.Rufar32 * a.Rufar32;
-    const float cf32 = (float)(a.invlDeb * kNegLog2e), invl32 = (float)a.invlDeb, rc2f = (float)a.rc2;
+    // the f32 form's constants as wave-uniform SGPR values (in VGPRs they were spilled and reloaded
+    // inside the pair loop at the kernel's 64-VGPR budget)
+    auto sgpr_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    const float cf32 = sgpr_f((float)(a.invlDeb * kNegLog2e)), invl32 = sgpr_f((float)a.invlDeb),
+                rc2f = sgpr_f((float)a.rc2);
     auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
         const double* B = a.boxes;
         double g2 = 0.;

@@ -379,9 +379,10 @@ __device__ __forceinline__ void qt_store(double* p, double v) {
 
 #if defined(MDQT_EXPT_QTSTAMPS)
 // diagnostic build only: per-wave s_memtime at entry, loop start, loop end, exit + s_memrealtime
-// at entry and exit, s_memtime after the force-slot loads, and the number of substeps in which an
-// ion of the wave jumped (tools/qt_stamps.py)
-__device__ unsigned long long g_qt_stamps[8 * 4096];
+// at entry and exit, s_memtime after the force-slot loads (6), after the prologue's loads are
+// issued (9) and after the Philox draws (8), and the number of substeps in which an ion of the
+// wave jumped (7) (tools/qt_stamps.py)
+__device__ unsigned long long g_qt_stamps[16 * 4096];
 #define QT_STAMP(slot, v) (st_[slot] = (v))
 #define QT_JCOUNT(c) (st_[7] += (__builtin_amdgcn_ballot_w64(c) != 0))
 #else
@@ -419,7 +420,7 @@ __device__ unsigned long long g_md_stamps[4 * 4096];
 template <bool DPPX, bool FAST, bool FUSED, bool IM01 = false, bool EDZ = false, bool NORN = false>
 __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTab* __restrict__ tab, int blk) {
 #if defined(MDQT_EXPT_QTSTAMPS)
-    unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_[16] = {};
 #endif
     QT_STAMP(0, __builtin_amdgcn_s_memtime());
     QT_STAMP(4, __builtin_amdgcn_s_memrealtime());
@@ -506,6 +507,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     } else {
         f = a.F[(size_t)c * S + i];
     }
+    QT_STAMP(9, __builtin_amdgcn_s_memtime());
     const double L = a.L, dt = qc.dtQ, DT = 0.5 * dt;
     // the substep loop's tPart step and Doppler factor held in VGPRs: with every SGPR taken the
     // compiler otherwise re-loads them from the kernel arguments inside the loop, and the
@@ -541,6 +543,7 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
             }
         }
     }
+    QT_STAMP(8, __builtin_amdgcn_s_memtime());
     if (!FAST && a.arrive) {                          // wait for the concurrent force launch
         if (threadIdx.x == 0) {
             int it = 0;
@@ -805,12 +808,12 @@ __device__ __forceinline__ void lane_substeps(const SubstepArgs& a, const FastTa
     st_[3] = __builtin_amdgcn_s_memtime();
     st_[5] = __builtin_amdgcn_s_memrealtime();
     const int wv = (int)(blk * (kLaneWG / 64) + (threadIdx.x >> 6));
-    if ((threadIdx.x & 63) < 8 && wv < 4096) {              // vector stores, one slot per lane
+    if ((threadIdx.x & 63) < 16 && wv < 4096) {             // vector stores, one slot per lane
         const int q = threadIdx.x & 63;
         unsigned long long v = st_[0];
 #pragma unroll
-        for (int m = 1; m < 8; ++m) v = (q == m) ? st_[m] : v;
-        g_qt_stamps[8 * wv + q] = v;
+        for (int m = 1; m < 16; ++m) v = (q == m) ? st_[m] : v;
+        g_qt_stamps[16 * wv + q] = v;
     }
 #endif
 }
@@ -888,7 +891,7 @@ hipError_t launch_md_step(const N3Args& f, const SubstepArgs& a, const FastTab* 
 
 #if defined(MDQT_EXPT_QTSTAMPS)
 extern "C" int mdqt_expt_qt_stamps(unsigned long long* out, int nwaves) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 8 * nwaves) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 16 * nwaves) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -19,10 +19,10 @@ s.substeps(25)
 s.synchronize()
 nw = (s.N + 3) // 4 // 4 * 4 + 4
 nw = min(nw, 4096)
-buf = (C.c_ulonglong * (8 * nw))()
+buf = (C.c_ulonglong * (16 * nw))()
 lib().mdqt_expt_qt_stamps.argtypes = [C.c_void_p, C.c_int]
 assert lib().mdqt_expt_qt_stamps(buf, nw) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8).astype(np.int64)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
 a = a[a[:, 0] > 0]
 pro, loop, epi, tot = a[:, 1] - a[:, 0], a[:, 2] - a[:, 1], a[:, 3] - a[:, 2], a[:, 3] - a[:, 0]
 rt = (a[:, 5] - a[:, 4]) * 10e-3          # us
@@ -34,9 +34,11 @@ for name, v in (("prologue", pro), ("loop", loop), ("epilogue", epi), ("total", 
     p = np.percentile(v, [0, 50, 100])
     print(f"{name:9s} cycles min/med/max {p[0]:9.0f} {p[1]:9.0f} {p[2]:9.0f}   med {p[1] / np.median(clk) / 1e3:6.2f} us")
 
-ld = a[:, 6] - a[:, 0]
-p = np.percentile(ld, [0, 50, 100])
-print(f"prologue to the force-slot sum (loads + Philox) min/med/max {p[0]:.0f} {p[1]:.0f} {p[2]:.0f}")
+for name, v in (("start -> loads issued", a[:, 9] - a[:, 0]), ("loads issued -> Philox done", a[:, 8] - a[:, 9]),
+                ("Philox done -> force-slot sum", a[:, 6] - a[:, 8]), ("force-slot sum -> loop", a[:, 1] - a[:, 6]),
+                ("prologue to the force-slot sum (loads + Philox)", a[:, 6] - a[:, 0])):
+    p = np.percentile(v, [0, 50, 100])
+    print(f"{name:48s} min/med/max {p[0]:6.0f} {p[1]:6.0f} {p[2]:6.0f}")
 nj = a[:, 7]
 for j in range(int(nj.max()) + 1):
     m = nj == j

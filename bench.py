@@ -754,6 +754,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     N = sim.N
     L = sim.const("L")
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
+    tmode, tmodel = int(sim.const("force_tail_mode")), sim.const("force_tail_model_bound")
     rf, far = sim.const("force_far_radius"), sim.const("force_far_bound")
     rv, vfar = sim.const("force_vfar_radius"), sim.const("force_vfar_bound")
     ru, ufar = sim.const("force_ufar_radius"), sim.const("force_ufar_bound")
@@ -773,9 +774,13 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force,
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail,
+                           "tail_mode": "measured" if tmode == 1 and world == 1 else "a priori",
+                           "tail_model_bound": tmodel if tmode == 1 and world == 1 else None,
                            "far_radius": rf, "far_bound": far, "vfar_radius": rv, "vfar_bound": vfar,
                            "ufar_radius": ru, "ufar_bound": ufar, "ufar32_radius": ru32,
-                           "note": "tile pairs >= skip_radius apart are skipped, tile pairs >= far_radius / vfar_radius "
+                           "note": "tile pairs >= skip_radius apart are skipped (tail_mode measured: bound is the largest "
+                                   "per-tile sum over the skipped tile pairs of n_J g(box distance) the force calls met; "
+                                   "a priori: (N - 1) g(skip_radius)), tile pairs >= far_radius / vfar_radius "
                                    "apart take the far / very-far / ultra-far pair forms; every ion's force is "
                                    "within bound + far_bound + vfar_bound + ufar_bound of the exact sum to L/2 (mdqt_engine.cpp "
                                    "tail_radius / far_radius_l; 0 = exact). fp64 rates count all N(N-1)/2 pairs "

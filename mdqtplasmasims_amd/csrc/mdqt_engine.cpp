@@ -69,6 +69,9 @@ inline cx cx_conj(cx a) { return {a.re, -a.im}; }
 
 }  // namespace
 
+#ifndef MDQT_TAIL_MODE
+#define MDQT_TAIL_MODE 1
+#endif
 struct mdqt_ctx {
     mdqt_params p;
     // derived constants (SpeedUp:79-85, :146-149, :295-297)
@@ -114,6 +117,13 @@ struct mdqt_ctx {
     // g(r) = (1/r + 1/lDeb) e^(-r/lDeb) / r the pair force magnitude (SpeedUp:224) — so no ion's
     // force changes by more than eps; a no-op where r_t >= L/2 (every BASELINE size but N ~ 1e6)
     int tail_exp = 12;
+    // how r_t is bounded (option "force_tail_mode"): 0 a priori, (N - 1) g(r_t) <= eps; 1 (default,
+    // one rank) measured: r_t from the density model's sum over tile pairs (tail_radius_sum), and
+    // every force call sums, per tile, n_J g(box distance) over its skipped tile pairs on the device
+    // (k_pairs_n3b) — the bound the call actually met, kept as a running maximum in dTail[T]
+    int tail_mode = MDQT_TAIL_MODE;
+    double* dTail = nullptr;       // [T + 1]: the per-tile bounds of the current call, then the running max
+    mutable double tail_key[4] = {0, 0, 0, 0}, tail_val[2] = {0, 0};   // tail_radius_sum memo (N, L, lDeb, k)
     // the far pair form (option "force_far_exp" k: eps = 10^-k, 0 = off): tile pairs whose boxes are
     // >= r_far apart evaluate their pairs within kFarRelErr (rsq1, degree-6 2^f), r_far the smallest
     // radius with (N - 1) g(r_far) kFarRelErr <= eps — so no ion's force moves by more than eps
@@ -652,6 +662,14 @@ static int ensure_aux(mdqt_ctx* s) {
             HIPCHK(hipMalloc(&s->dSortTmp, s->sortTmpBytes));
             HIPCHK(hipMalloc(&s->dRs, (size_t)3 * Tc * 64 * sizeof(double)));
             HIPCHK(hipMalloc(&s->dBoxes, (size_t)12 * Tc * sizeof(double)));
+            double keep = 0.;                            // the running maximum survives a reallocation
+            if (s->dTail) {
+                HIPCHK(hipMemcpy(&keep, s->dTail + (s->capSortN + 63) / 64, sizeof(double), hipMemcpyDeviceToHost));
+                HIPCHK(hipFree(s->dTail));
+            }
+            HIPCHK(hipMalloc(&s->dTail, (size_t)(Tc + 1) * sizeof(double)));
+            HIPCHK(hipMemset(s->dTail, 0, (size_t)Tc * sizeof(double)));
+            HIPCHK(hipMemcpy(s->dTail + Tc, &keep, sizeof(double), hipMemcpyHostToDevice));
             s->capSortN = Nc;
         }
     }
@@ -692,6 +710,8 @@ static void free_device(mdqt_ctx* s) {
     for (void* q : {(void*)s->dKeys, (void*)s->dIon, s->dSortTmp, (void*)s->dRs, (void*)s->dBoxes})
         if (q) (void)hipFree(q);
     s->dKeys = nullptr; s->dIon = nullptr; s->dSortTmp = nullptr; s->dRs = nullptr; s->dBoxes = nullptr;
+    if (s->dTail) (void)hipFree(s->dTail);
+    s->dTail = nullptr;
     s->capSortN = 0;
     if (s->dPeerParts) (void)hipFree((void*)s->dPeerParts);
     s->dSlots = nullptr; s->dFr = nullptr; s->dPeerParts = nullptr;
@@ -834,6 +854,9 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
 }
 
 static double tail_radius(int N, double L, double lDeb, int k, double* bound);
+static double tail_radius_sum(const mdqt_ctx* s, double* bound);
+static bool tail_measured(const mdqt_ctx* s);
+static double skip_radius(const mdqt_ctx* s, double* bound);
 static double far_radius(int N, double L, double lDeb, int k, double* bound);
 static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound);
 extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
@@ -852,10 +875,24 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
     if (!strcmp(n, "force_skip_radius") || !strcmp(n, "force_tail_bound")) {   // the tile-pair skip radius
         double bound;                                  // and its force bound (0: exact, r = L/2)
-        const double r = (s->use_n3b && s->sort_mode == 1) ? tail_radius(s->N, s->L, s->lDeb, s->tail_exp, &bound)
-                                                           : (bound = 0., s->L / 2.);
-        return n[6] == 's' ? r : bound;
+        const double r = (s->use_n3b && s->sort_mode == 1) ? skip_radius(s, &bound) : (bound = 0., s->L / 2.);
+        if (n[6] == 's') return r;
+        if (s->use_n3b && tail_measured(s) && r < s->L / 2.) {   // mode 1: the measured running maximum
+            double m = 0.;                             // (1e-12 relative: the device sum's rounding)
+            if (s->dTail && (hipStreamSynchronize(s->stream) != hipSuccess ||
+                             hipMemcpy(&m, s->dTail + (s->capSortN + 63) / 64, sizeof(double),
+                                       hipMemcpyDeviceToHost) != hipSuccess)) return NAN;
+            return m * (1. + 1e-12);
+        }
+        return bound;
     }
+    if (!strcmp(n, "force_tail_model_bound")) {       // mode 1: the model bound r_t was chosen by
+        double bound;
+        const double r = (s->use_n3b && tail_measured(s)) ? tail_radius_sum(s, &bound) : (bound = 0., 0.);
+        (void)r;
+        return bound;
+    }
+    if (!strcmp(n, "force_tail_mode")) return s->tail_mode;
     if (!strcmp(n, "force_far_radius") || !strcmp(n, "force_far_bound")) {   // the far pair form's radius
         double bound;                                  // and force bound (0: off, r = L/2)
         const double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
@@ -1125,6 +1162,56 @@ static double tail_radius(int N, double L, double lDeb, int k, double* bound) {
     *bound = n1 * tail_g(hi, lDeb);
     return hi;
 }
+// force_tail_mode 1: r_t from a model of the bound the device measures, sum over the skipped tile
+// pairs (I, J) of n_J g(box distance): at density rho = N / L^3 the tiles with box distance in
+// [x, x + dx] hold about rho 4 pi (x + delta)^2 dx ions, delta = two tile widths (64 / rho)^(1/3)
+// bounding the box extents, so B(r) = rho int_r^(L/2) 4 pi (x + delta)^2 g(x) dx (tile pairs >= L/2
+// apart only hold pairs beyond the cutoff); r_t the smallest r with 2 B(r) <= eps (the factor 2 a
+// margin for the model — the kernel's measured sum is what the call reports).  Memoised per context.
+static double tail_model(double r, int N, double L, double lDeb) {
+    const double rho = N / (L * L * L), delta = 2. * cbrt(64. / rho), hi = L / 2.;
+    if (r >= hi) return 0.;
+    const int n = 2000;                             // Simpson on [r, L/2]
+    const double h = (hi - r) / n;
+    auto f = [&](double x) { return 4. * M_PI * (x + delta) * (x + delta) * tail_g(x, lDeb); };
+    double acc = f(r) + f(hi);
+    for (int i = 1; i < n; ++i) acc += (i & 1 ? 4. : 2.) * f(r + i * h);
+    return rho * acc * h / 3.;
+}
+static double tail_radius_sum(const mdqt_ctx* s, double* bound) {
+    const int N = s->N, k = s->tail_exp;
+    const double L = s->L, lDeb = s->lDeb, Rcut = L / 2.;
+    *bound = 0.;
+    if (k <= 0 || N < 2) return Rcut;
+    if (s->tail_key[0] == N && s->tail_key[1] == L && s->tail_key[2] == lDeb && s->tail_key[3] == k) {
+        *bound = s->tail_val[1];
+        return s->tail_val[0];
+    }
+    const double eps = pow(10., -k);
+    double r = Rcut, b = 0.;
+    // only where the a-priori radius is below L/2 (N ~ 1e6): elsewhere the model would skip a sliver
+    // just inside L/2 for nothing, and those sizes keep the exact cutoff
+    double b0;
+    if (tail_radius(N, L, lDeb, k, &b0) < Rcut) {
+        double lo = 0., hi = Rcut;
+        for (int it = 0; it < 60 && hi - lo > 1e-9 * Rcut; ++it) {
+            const double m = 0.5 * (lo + hi);
+            if (m > 0 && 2. * tail_model(m, N, L, lDeb) <= eps) hi = m; else lo = m;
+        }
+        r = hi;
+        b = tail_model(hi, N, L, lDeb);
+    }
+    s->tail_key[0] = N; s->tail_key[1] = L; s->tail_key[2] = lDeb; s->tail_key[3] = k;
+    s->tail_val[0] = r; s->tail_val[1] = b;
+    *bound = b;
+    return r;
+}
+// the context's skip radius: mode 1 (measured bound) on one rank in spatial order, else a priori
+static bool tail_measured(const mdqt_ctx* s) { return s->tail_mode == 1 && s->p.world_size == 1 && s->sort_mode == 1; }
+static double skip_radius(const mdqt_ctx* s, double* bound) {
+    return tail_measured(s) ? tail_radius_sum(s, bound) : tail_radius(s->N, s->L, s->lDeb, s->tail_exp, bound);
+}
+
 // the far radii: the smallest r with (N - 1) g(r) err(r) <= 10^-k, err the relative error of a term
 // at distance r in the form (far: kFarRelErr; very far: (r/lDeb + 3) kRsqRawErr + kExp5RelErr) —
 // L/2 (= never) and bound 0 when k = 0 or that r is >= L/2; bound = (N - 1) g(r) err(r)
@@ -1165,7 +1252,8 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.micGuard = c.micGuard; a.guard = c.guard;
     a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr;
     double bound;
-    a.Rskip = tail_radius(s->N, s->L, s->lDeb, s->tail_exp, &bound);
+    a.Rskip = skip_radius(s, &bound);
+    a.tailb = nullptr;
     a.Rfar = far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound);
     a.Rvfar = far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound);
     a.Rufar = far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound);
@@ -1181,6 +1269,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
         o.tmp = s->dSortTmp; o.tmp_bytes = s->sortTmpBytes; o.Rs = s->dRs; o.boxes = s->dBoxes;
         HIPCHK(launch_spatial_order(o, s->stream));
         a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes;
+        if (tail_measured(s) && a.Rskip < a.Rcut) a.tailb = s->dTail;
     }
     return 0;
 }
@@ -1290,7 +1379,9 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         N3BArgs a;
         if (n3b_args(s, a)) return -1;
         const int W = s->p.world_size;
+        if (a.tailb) HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)a.T * sizeof(double), s->stream));
         HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream));
+        if (a.tailb) HIPCHK(launch_tail_max(a.tailb, a.T, s->dTail + (s->capSortN + 63) / 64, s->stream));
         if (W > 1) {
             if (s->comm) {
                 NCCLCHK(ncclReduceScatter(s->dFr, s->dF, (size_t)3 * s->S, ncclDouble, ncclSum, s->comm, s->stream));
@@ -2455,6 +2546,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     if (!strcmp(name, "force_tail_exp")) {             // error-bounded tail: eps = 10^-value (0: exact)
         if (value < 0 || value > 300) return fail("force_tail_exp must be 0 (exact) .. 300");
         s->tail_exp = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_tail_mode")) {            // 0: a-priori bound, 1: measured (one rank)
+        if (value < 0 || value > 1) return fail("force_tail_mode must be 0 (a priori) or 1 (measured)");
+        s->tail_mode = value;
         return 0;
     }
     if (!strcmp(name, "force_sort")) {                 // Newton-3 blocks: Hilbert order + tile-pair skipping

@@ -412,9 +412,9 @@ void k_pairs_n3b(N3BArgs a) {
     auto sgpr_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
     const float cf32 = sgpr_f((float)(a.invlDeb * kNegLog2e)), invl32 = sgpr_f((float)a.invlDeb),
                 rc2f = sgpr_f((float)a.rc2);
-    auto classify = [&](int Iw, int J) {            // lane-parallel over Iw (staging wave)
+    auto classify = [&](int Iw, int J, double& g2) {   // lane-parallel over Iw (staging wave)
         const double* B = a.boxes;
-        double g2 = 0.;
+        g2 = 0.;
         bool uni = true;
         double n[3];
 #pragma unroll
@@ -439,6 +439,11 @@ void k_pairs_n3b(N3BArgs a) {
     // the three-level blocking fits the 64-VGPR budget of two 16-wave workgroups per CU
     double* fi = irun[q][0];
     fi[l] = 0.; fi[64 + l] = 0.; fi[128 + l] = 0.;
+    // force_tail_mode 1 (a.tailb): the staging lanes' tail bound of their I tiles (I side, over the
+    // whole run) and of the current J tile (J side, summed by thread 0 after the barrier)
+    __shared__ double tbi[BW], tbj[BW];
+    const bool tmeas = !POT && a.tailb != nullptr;
+    if (tmeas && q == 0 && l < BW) tbi[l] = 0.;
     double* ax = accj[q][0];
     double* ay = accj[q][1];
     double* az = accj[q][2];
@@ -459,9 +464,22 @@ void k_pairs_n3b(N3BArgs a) {
                 pj[1][l] = yj; pj[1][l + 64] = yj;
                 pj[2][l] = zj; pj[2][l + 64] = zj;
                 mj[l] = vj ? 1. : 0.; mj[l + 64] = mj[l];
+                if (tmeas && l < BW) tbj[l] = 0.;
                 if (srt && l < BW && P * BW + l < T) {
-                    const double4 t4 = classify(P * BW + l, J);
+                    double g2;
+                    const double4 t4 = classify(P * BW + l, J, g2);
                     tp[l][0] = t4.x; tp[l][1] = t4.y; tp[l][2] = t4.z; tp[l][3] = t4.w;
+                    // a tile pair skipped by the tail radius (boxes >= Rskip apart) with a pair that
+                    // may lie inside L/2: each of its pairs is >= sqrt(g2) apart, so each ion of I
+                    // loses at most n_J g(sqrt(g2)) and each ion of J n_I g(sqrt(g2)); counted once per
+                    // unordered tile pair (block distance 0: J > I only)
+                    const int Iw = P * BW + l;
+                    if (tmeas && t4.w < 0. && g2 < a.Rcut * a.Rcut && (db > 0 || J > Iw)) {
+                        const double d = sqrt(g2);
+                        const double gd = (1. / d + a.invlDeb) * exp(-d / a.lDeb) / d;
+                        tbi[l] += (double)min(64, N - J * 64) * gd;
+                        tbj[l] = (double)min(64, N - Iw * 64) * gd;
+                    }
 #if defined(MDQT_EXPT_CLS)
                     atomicAdd(&g_cls_count[t4.w < 0. ? 0 : 1 + ((int)t4.w & 1)], 1ull);
 #endif
@@ -470,6 +488,11 @@ void k_pairs_n3b(N3BArgs a) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
             __syncthreads();
+            if (tmeas && threadIdx.x == 0) {
+                double sj = 0.;
+                for (int w = 0; w < BW; ++w) sj += tbj[w];
+                if (sj > 0.) atomicAdd(a.tailb + J, sj);
+            }
             const double cls = srt ? uniform_f64(tp[q][3]) : 0.;
             if (vI && (db > 0 || J >= I) && cls >= 0.) {
                 const bool diag = (db == 0 && J == I);
@@ -542,6 +565,17 @@ void k_pairs_n3b(N3BArgs a) {
         double* o = a.slots + (size_t)(a.nd + run) * plane + i;
         o[0] = fi[l]; o[a.Npad] = fi[64 + l]; o[2 * (size_t)a.Npad] = fi[128 + l];
     }
+    if (tmeas && q == 0 && l < BW && P * BW + l < T && tbi[l] > 0.) atomicAdd(a.tailb + P * BW + l, tbi[l]);
+}
+
+// force_tail_mode 1: the largest per-tile tail bound of this force call into the running maximum
+// (positive doubles order as their bit patterns)
+__global__ __launch_bounds__(256) void k_tail_max(const double* __restrict__ tailb, int T, double* out) {
+    double m = 0.;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) m = fmax(m, tailb[t]);
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0 && m > 0.)
+        atomicMax((unsigned long long*)out, (unsigned long long)__double_as_longlong(m));
 }
 
 // canonical per-ion sum of the slots this rank wrote: j-slots db = 0 .. nd-1, then i-slots.
@@ -659,6 +693,11 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
         }
     }
     hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, a, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_tail_max(const double* tailb, int T, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_tail_max, dim3((T + 255) / 256 < 64 ? (T + 255) / 256 : 64), dim3(256), 0, s, tailb, T, out);
     return hipGetLastError();
 }
 

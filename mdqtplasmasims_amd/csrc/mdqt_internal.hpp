@@ -421,6 +421,9 @@ struct N3BArgs {
     double Rskip;       // force tile pairs whose boxes are >= Rskip apart are skipped (use_sort 1):
                         // Rcut exactly (every skipped pair is beyond L/2), or the error-bounded tail
                         // radius r_t < L/2 of mdqt_engine.cpp tail_radius (potentials: always Rcut)
+    double* tailb;      // force_tail_mode 1: per tile, the sum over its tail-skipped tile pairs (boxes
+                        // >= Rskip apart, < L/2) of n_J g(box distance) — the measured bound on what
+                        // each of its ions loses (zeroed before the launch; nullptr: not measured)
 };
 struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]
@@ -436,6 +439,7 @@ struct SortArgs {
 hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s);
 size_t spatial_order_tmp_bytes(int N);
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
+hipError_t launch_tail_max(const double* tailb, int T, double* out, hipStream_t s);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 
 // ---- Monte-Carlo + MD analytics program (mdmc_kernels.hip) ----

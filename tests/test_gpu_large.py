@@ -172,7 +172,8 @@ def test_error_bounded_tail_and_far_form(cfg):
     ru32 = s.const("force_ufar32_radius")             # the f32 ultra-far shell (its bound is in ub)
     assert 0 < fb <= 1e-13 and rf < L / 2 and 0 < vb <= 1e-13 and rf < rv < L / 2
     assert 0 < ub <= 2e-13 and rf < ru < L / 2 and ru <= ru32 <= L / 2   # ub: f64 + f32 shells, 1e-13 each
-    assert (0 < tb <= 1e-12 and rt < L / 2) if cfg == "C4" else (tb == 0 and rt == L / 2)
+    # (C4: the measured bound needs a force call — read after the calls below)
+    assert (rt < L / 2) if cfg == "C4" else (tb == 0 and rt == L / 2)
     out = {}
     for te, fe, ve, ue in ((12, 13, 13, 13), (0, 13, 0, 0), (0, 0, 13, 0), (0, 0, 0, 13), (12, 0, 0, 0),
                            (0, 0, 0, 0)):
@@ -184,6 +185,16 @@ def test_error_bounded_tail_and_far_form(cfg):
         out[te, fe, ve, ue] = s.get_state()["F"]
     assert s.const("force_skip_radius") == L / 2 and s.const("force_far_bound") == 0
     assert s.const("force_vfar_bound") == 0 and s.const("force_ufar_bound") == 0
+    if cfg == "C4":
+        # force_tail_mode 1 (one rank): the bound is what the calls measured — per tile, n_J g(box
+        # distance) summed over its skipped tile pairs — kept as a running maximum over the calls
+        s.set_option("force_tail_exp", 12)
+        assert s.const("force_tail_mode") == 1 and s.const("force_skip_radius") == rt
+        tb = s.const("force_tail_bound")
+        mb = s.const("force_tail_model_bound")
+        print(f"{cfg}: measured tail bound {tb:.3e} (the model chose r_t for {mb:.3e}; a priori (N - 1) g(r_t) "
+              f"{(s.N - 1) * (1 / rt + 1 / s.const('lDeb')) * np.exp(-rt / s.const('lDeb')) / rt:.3e})")
+        assert 0 < tb <= 1e-12 and 0 < mb <= 5e-13
     Fe = out[0, 0, 0, 0]
     scale = 1e-13 * np.abs(Fe).max()
     d = {k: np.abs(v - Fe).max() for k, v in out.items()}

@@ -186,11 +186,33 @@ def cpu_baseline(params, qt, seconds, seed, job):
     threads = cpu_threads()
     rate, n, ratio, N, el = timed(threads, seconds, 400)
     r1, n1, _, _, el1 = timed(1, max(2.0, seconds / 3), 100)
-    return {"value": rate, "unit": "particle-qsteps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} MD steps x {ratio} qsteps of the same workload (N={N}), oracle C "
-                      f"restatement, OpenMP {threads} threads, {el:.1f} s",
-            "single_thread": {"value": r1, "unit": "particle-qsteps/s", "cores": 1,
-                              "sample": f"{n1} MD steps x {ratio} qsteps, 1 thread, {el1:.1f} s"}}
+    out = {"value": rate, "unit": "particle-qsteps/s", "cores": threads, "kind": "port",
+           "sample": f"{n} MD steps x {ratio} qsteps of the same workload (N={N}), oracle C "
+                     f"restatement, OpenMP {threads} threads, {el:.1f} s",
+           "single_thread": {"value": r1, "unit": "particle-qsteps/s", "cores": 1,
+                             "sample": f"{n1} MD steps x {ratio} qsteps, 1 thread, {el1:.1f} s"},
+           "calibration": None}
+    cal = calibration_file()
+    if cal:                                        # the port against the reference itself
+        with open(cal) as f:
+            c = json.load(f)
+        k = c["threads"]["1"]["oracle_over_reference"]
+        out["calibration"] = {
+            "file": os.path.relpath(cal, ROOT), "oracle_over_reference_1_thread": k,
+            "reference_1_thread": c["threads"]["1"]["reference_particle_qsteps_per_s"],
+            "oracle_1_thread_same_container": c["threads"]["1"]["oracle_particle_qsteps_per_s"],
+            "reference_equivalent_on_this_host_1_thread": r1 / k,
+            "note": "the reference SpeedUp's own 1-thread rate (BASELINE.md 2, SURVEY App. B-3) and the oracle's on "
+                    "the same container and workload: the oracle is k x faster, so the reference would run about "
+                    "single_thread / k here"}
+    return out
+
+
+def calibration_file():
+    """the newest committed CPU calibration (profiles/r<round>_cpu_calibration.json, tools/cpu_calibration.py)"""
+    d = os.path.join(ROOT, "profiles")
+    fs = sorted(f for f in os.listdir(d) if f.endswith("_cpu_calibration.json") and f.startswith("r"))
+    return os.path.join(d, fs[-1]) if fs else None
 
 
 def cpu_baseline_large(cfg, seconds=6.0):
@@ -399,19 +421,34 @@ def main():
             # substeps per fused launch: the MD interval split at MAXSUB = 32 (mdqt_internal.hpp)
             launches = -(-ratio // 32)
             nsub_per_launch = ratio / launches
-            bytes_launch = B_Q_PER_ION * N
+            # B_q = 520 B per particle-QSTEP; one fused launch processes N x nsub
+            # particle-qsteps, so its algorithmic bytes are 520 N nsub (the contract's "per-unit figure
+            # x units per launch").  The launch keeps the state in registers across its substeps, so
+            # the bytes it must move (compulsory) are 520 N once — the PMC traffic is measured against
+            # those; and the roof that binds it is neither: FP64 VALU issue at one wave per SIMD
+            # (DESIGN.md §3, §6), reported as binding_roof with F_q = 1.75 kflop per particle-qstep.
+            qsteps_launch = N * nsub_per_launch
+            bytes_launch = B_Q_PER_ION * qsteps_launch
             ach = bytes_launch / s_avg / 1e9
-            flops = F_Q_PER_QSTEP * N * nsub_per_launch
+            compulsory = B_Q_PER_ION * N
+            flops = F_Q_PER_QSTEP * qsteps_launch
             kname = "k_substeps_lanes" if N < 98304 else "k_substeps_r"
             traffic, tsrc = pmc_traffic(kname)
             kinst = tsrc.get("instance")
-            # The fused QT launch is bound by neither roof: one wave per SIMD runs a dependent chain of
-            # ~330 VALU instructions per substep — "latency", with both fractions given.
-            roof = {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            fp64 = flops / s_avg / 1e12
+            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                     "kernel": f"{kinst or kname} (fused {nsub_per_launch:g} x step+qstep)",
                     "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
-                    "fp64_tflops": flops / s_avg / 1e12, "fp64_frac": flops / s_avg / 1e12 / FP64_PEAK_TFS,
+                    "algorithmic_unit": f"{B_Q_PER_ION:g} B per particle-qstep x {qsteps_launch:.0f} particle-qsteps "
+                                        "per launch (SURVEY 8d)",
+                    "compulsory_bytes_per_launch": compulsory,
+                    "compulsory_hbm_frac": compulsory / s_avg / 1e9 / HBM_PEAK_GBS,
+                    "fp64_tflops": fp64, "fp64_frac": fp64 / FP64_PEAK_TFS,
+                    "binding_roof": {"kind": "fp64 VALU issue (one wave per SIMD, dependent chains)",
+                                     "achieved": fp64, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                                     "frac": fp64 / FP64_PEAK_TFS,
+                                     "flop_unit": f"{F_Q_PER_QSTEP:g} flop per particle-qstep (SURVEY 8d)"},
                     "hbm_frac": ach / HBM_PEAK_GBS}
         else:
             pairs = N * (N - 1) / 2.0
@@ -737,6 +774,10 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     sim.init()                                     # collective: Epot0 over all slabs
     t_init = time.perf_counter() - t0
     ratio = int(sim.const("plasmaToQuantumTimestepRatio"))
+    check = world > 1                              # parity against a world-1 run (below)
+    if check:
+        sim.forces()                               # the first call's forces, this rank's slab
+        F0 = sim.get_state()["F"]
     sim.md_steps(1)
     barrier()
     sim.enable_timing(1)
@@ -755,11 +796,44 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     L = sim.const("L")
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
     tmode, tmodel = int(sim.const("force_tail_mode")), sim.const("force_tail_model_bound")
+    fixed, raw = sim.const("force_tail_fixed_tiles"), sim.const("force_tail_raw_bound")
     rf, far = sim.const("force_far_radius"), sim.const("force_far_bound")
     rv, vfar = sim.const("force_vfar_radius"), sim.const("force_vfar_bound")
     ru, ufar = sim.const("force_ufar_radius"), sim.const("force_ufar_bound")
     ru32 = sim.const("force_ufar32_radius")
-    sim.close()
+    tail_eps = 10.0 ** -12                          # force_tail_exp default
+    bound_met = bool(rt >= L / 2 or (tmode == 1 and tail <= tail_eps) or tmode == 0)
+    parity = None
+    if check:
+        # the sharded result against a world-1 context built from the same inputs
+        # (init() is deterministic), run on each rank's own GPU through the same MD steps: every
+        # rank compares its slab — the first call's forces, then R and V after 1 + steps MD steps —
+        # and the maxima over the ranks decide (mdqtplasmasims_amd.sharded.sharded_parity)
+        from mdqtplasmasims_amd.sharded import sharded_parity
+        st = sim.get_state()
+        lo, hi = sim.slab_bounds()
+        sim.close()
+        ref = M.Simulation(device=local, world_size=1, rank=0, seed=12346, job=1, qt_enabled=qt, **params).init()
+        ref.forces()
+        rF0 = ref.get_state()["F"]
+        ref.md_steps(1 + steps)
+        rs = ref.get_state()
+        ref.close()
+
+        def all_max(vals):
+            t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return [float(x) for x in t.tolist()]
+
+        parity = sharded_parity({"F0": F0, "R": st["R"], "V": st["V"]}, {"F0": rF0, "R": rs["R"], "V": rs["V"]},
+                                lo, hi, L, all_max)
+        parity.update(comm_size=comm_size, md_steps_compared=1 + steps,
+                      reference="a world-1 context of the same init() on each rank's GPU; each rank's slab "
+                                "compared, max over ranks")
+        if not parity["ok"]:
+            raise RuntimeError(f"sharded result differs from world 1: {json.dumps(parity)}")
+    else:
+        sim.close()
     unit_steps = ratio if qt else 1
     f_avg = f_ms / max(nf, 1) * 1e-3
     pairs = N * (N - 1) / 2.0
@@ -773,14 +847,17 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force,
-            "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail,
-                           "tail_mode": "measured" if tmode == 1 and world == 1 else "a priori",
-                           "tail_model_bound": tmodel if tmode == 1 and world == 1 else None,
+            "parity": parity if check else {"note": "world 1: this line is the reference the sharded runs are checked against"},
+            "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail, "bound_met": bound_met,
+                           "tail_mode": "measured+enforced" if tmode == 1 else "a priori",
+                           "tail_model_bound": tmodel if tmode == 1 else None,
+                           "tiles_over_eps_fixed": fixed, "largest_tile_sum_before_fix": raw,
                            "far_radius": rf, "far_bound": far, "vfar_radius": rv, "vfar_bound": vfar,
                            "ufar_radius": ru, "ufar_bound": ufar, "ufar32_radius": ru32,
-                           "note": "tile pairs >= skip_radius apart are skipped (tail_mode measured: bound is the largest "
-                                   "per-tile sum over the skipped tile pairs of n_J g(box distance) the force calls met; "
-                                   "a priori: (N - 1) g(skip_radius)), tile pairs >= far_radius / vfar_radius "
+                           "note": "tile pairs >= skip_radius apart are skipped (tail_mode measured+enforced: every "
+                                   "call sums per tile n_J g(box distance) over its skipped tile pairs, tiles over "
+                                   "1e-12 get those pairs added exactly (tiles_over_eps_fixed), bound is the largest "
+                                   "remaining per-tile sum; a priori: (N - 1) g(skip_radius)), tile pairs >= far_radius / vfar_radius "
                                    "apart take the far / very-far / ultra-far pair forms; every ion's force is "
                                    "within bound + far_bound + vfar_bound + ufar_bound of the exact sum to L/2 (mdqt_engine.cpp "
                                    "tail_radius / far_radius_l; 0 = exact). fp64 rates count all N(N-1)/2 pairs "

@@ -118,12 +118,20 @@ struct mdqt_ctx {
     // force changes by more than eps; a no-op where r_t >= L/2 (every BASELINE size but N ~ 1e6)
     int tail_exp = 12;
     // how r_t is bounded (option "force_tail_mode"): 0 a priori, (N - 1) g(r_t) <= eps; 1 (default,
-    // one rank) measured: r_t from the density model's sum over tile pairs (tail_radius_sum), and
-    // every force call sums, per tile, n_J g(box distance) over its skipped tile pairs on the device
-    // (k_pairs_n3b) — the bound the call actually met, kept as a running maximum in dTail[T]
+    // every world size) measured and enforced: r_t from the density model's sum over tile pairs
+    // (tail_radius_sum), every force call sums, per tile, n_J g(box distance) over its skipped tile
+    // pairs on the device (k_pairs_n3b; all-reduced over the ranks), and every tile whose sum
+    // exceeds eps gets the exact sum over those tile pairs added to its rows (k_tail_fix) — so every
+    // ion meets eps whatever the configuration; the host widens r_t when that happened (tail_check)
     int tail_mode = MDQT_TAIL_MODE;
-    double* dTail = nullptr;       // [T + 1]: the per-tile bounds of the current call, then the running max
-    mutable double tail_key[4] = {0, 0, 0, 0}, tail_val[2] = {0, 0};   // tail_radius_sum memo (N, L, lDeb, k)
+    double* dTail = nullptr;       // [T]: the per-tile sums of the current call
+    unsigned long long* dTailSt = nullptr;   // [8]: k_tail_max's running maxima and counters
+    int* dTailList = nullptr;      // [T]: this call's tiles over eps (this rank's)
+    double tail_scale = 1.;        // r_t from 2 tail_scale B(r) <= eps: raised when a call exceeded eps
+    unsigned long long tail_seen = 0;   // tiles over eps the host has reacted to
+    bool tail_pending = false;     // in-process group: the sums wait for the group's (local_reduce)
+    N3BArgs tail_args;             // ... with the call's arguments
+    mutable double tail_key[5] = {0, 0, 0, 0, 0}, tail_val[2] = {0, 0};   // tail_radius_sum memo (N, L, lDeb, k, scale)
     // the far pair form (option "force_far_exp" k: eps = 10^-k, 0 = off): tile pairs whose boxes are
     // >= r_far apart evaluate their pairs within kFarRelErr (rsq1, degree-6 2^f), r_far the smallest
     // radius with (N - 1) g(r_far) kFarRelErr <= eps — so no ion's force moves by more than eps
@@ -205,6 +213,17 @@ struct mdqt_ctx {
 };
 
 static int settle_forces(mdqt_ctx* s);
+static int tail_check(mdqt_ctx* s);
+static double u64_as_double(unsigned long long u) { double d; memcpy(&d, &u, sizeof d); return d; }
+
+// force_tail_mode 1: forget what earlier calls measured (a new state, size or tail option)
+static int tail_reset(mdqt_ctx* s) {
+    s->tail_scale = 1.;
+    s->tail_seen = 0;
+    s->tail_pending = false;
+    if (s->dTailSt) HIPCHK(hipMemsetAsync(s->dTailSt, 0, 8 * sizeof(unsigned long long), s->stream));
+    return 0;
+}
 
 // The substep kernels raise dFlags[0] if a position leaves [-L/8, 9L/8] (an ion moving more than
 // L/8 in half a substep: not a physical run).  Checked at every host synchronisation point;
@@ -227,7 +246,7 @@ static int check_range_flag(mdqt_ctx* s) {
                     "substep); pair range checks are now on, but forces since the last sync used "
                     "the in-box minimum image");
     }
-    return 0;
+    return tail_check(s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -662,15 +681,15 @@ static int ensure_aux(mdqt_ctx* s) {
             HIPCHK(hipMalloc(&s->dSortTmp, s->sortTmpBytes));
             HIPCHK(hipMalloc(&s->dRs, (size_t)3 * Tc * 64 * sizeof(double)));
             HIPCHK(hipMalloc(&s->dBoxes, (size_t)12 * Tc * sizeof(double)));
-            double keep = 0.;                            // the running maximum survives a reallocation
-            if (s->dTail) {
-                HIPCHK(hipMemcpy(&keep, s->dTail + (s->capSortN + 63) / 64, sizeof(double), hipMemcpyDeviceToHost));
-                HIPCHK(hipFree(s->dTail));
-            }
-            HIPCHK(hipMalloc(&s->dTail, (size_t)(Tc + 1) * sizeof(double)));
+            if (s->dTail) HIPCHK(hipFree(s->dTail));
+            if (s->dTailList) HIPCHK(hipFree(s->dTailList));
+            s->dTail = nullptr; s->dTailList = nullptr;
+            HIPCHK(hipMalloc(&s->dTail, (size_t)Tc * sizeof(double)));
             HIPCHK(hipMemset(s->dTail, 0, (size_t)Tc * sizeof(double)));
-            HIPCHK(hipMemcpy(s->dTail + Tc, &keep, sizeof(double), hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&s->dTailList, (size_t)Tc * sizeof(int)));
+            if (!s->dTailSt) HIPCHK(hipMalloc(&s->dTailSt, 8 * sizeof(unsigned long long)));
             s->capSortN = Nc;
+            if (tail_reset(s)) return -1;                // a new size: nothing measured yet
         }
     }
     if (s->use_n3 && s->npairs > 0) {
@@ -711,7 +730,9 @@ static void free_device(mdqt_ctx* s) {
         if (q) (void)hipFree(q);
     s->dKeys = nullptr; s->dIon = nullptr; s->dSortTmp = nullptr; s->dRs = nullptr; s->dBoxes = nullptr;
     if (s->dTail) (void)hipFree(s->dTail);
-    s->dTail = nullptr;
+    if (s->dTailList) (void)hipFree(s->dTailList);
+    if (s->dTailSt) (void)hipFree(s->dTailSt);
+    s->dTail = nullptr; s->dTailList = nullptr; s->dTailSt = nullptr;
     s->capSortN = 0;
     if (s->dPeerParts) (void)hipFree((void*)s->dPeerParts);
     s->dSlots = nullptr; s->dFr = nullptr; s->dPeerParts = nullptr;
@@ -877,15 +898,27 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
         double bound;                                  // and its force bound (0: exact, r = L/2)
         const double r = (s->use_n3b && s->sort_mode == 1) ? skip_radius(s, &bound) : (bound = 0., s->L / 2.);
         if (n[6] == 's') return r;
-        if (s->use_n3b && tail_measured(s) && r < s->L / 2.) {   // mode 1: the measured running maximum
-            double m = 0.;                             // (1e-12 relative: the device sum's rounding)
-            if (s->dTail && (hipStreamSynchronize(s->stream) != hipSuccess ||
-                             hipMemcpy(&m, s->dTail + (s->capSortN + 63) / 64, sizeof(double),
-                                       hipMemcpyDeviceToHost) != hipSuccess)) return NAN;
-            return m * (1. + 1e-12);
+        if (s->use_n3b && tail_measured(s) && r < s->L / 2.) {
+            // mode 1: the running maximum of the per-tile sums each call met after the exact pass
+            // (1e-12 relative: the device sum's rounding); NaN until a force call has measured
+            unsigned long long h[8];
+            if (!s->dTailSt || hipStreamSynchronize(s->stream) != hipSuccess ||
+                hipMemcpy(h, s->dTailSt, sizeof h, hipMemcpyDeviceToHost) != hipSuccess || h[4] == 0) return NAN;
+            return u64_as_double(h[0]) * (1. + 1e-12);
         }
         return bound;
     }
+    // mode 1 diagnostics: the largest per-tile sum the skip radius alone left (before the exact
+    // pass), the tiles that exceeded eps so far, the measured force calls, the model scale
+    if (!strcmp(n, "force_tail_raw_bound") || !strcmp(n, "force_tail_fixed_tiles") ||
+        !strcmp(n, "force_tail_calls")) {
+        unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (s->dTailSt && (hipStreamSynchronize(s->stream) != hipSuccess ||
+                           hipMemcpy(h, s->dTailSt, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)) return NAN;
+        if (n[11] == 'r') return u64_as_double(h[1]) * (1. + 1e-12);
+        return (double)(n[11] == 'f' ? h[2] : h[4]);
+    }
+    if (!strcmp(n, "force_tail_scale")) return s->tail_scale;
     if (!strcmp(n, "force_tail_model_bound")) {       // mode 1: the model bound r_t was chosen by
         double bound;
         const double r = (s->use_n3b && tail_measured(s)) ? tail_radius_sum(s, &bound) : (bound = 0., 0.);
@@ -987,6 +1020,7 @@ extern "C" int mdqt_set_state(mdqt_ctx* s, int N, const double* R, const double*
     if (N != s->N && resize(s, N)) return -1;
     if (ld < (size_t)N) return fail("ld < N");
     if (upload(s, R, V, ld, psi, tPart)) return -1;
+    if (R && tail_reset(s)) return -1;                 // new positions: the tail measurements restart
     s->t = t;
     return 0;
 }
@@ -1104,6 +1138,7 @@ extern "C" int mdqt_init(mdqt_ctx* s) {
     for (int i = 0; i < N; ++i) { R[i] = X[i]; R[(size_t)N + i] = Y[i]; R[(size_t)2 * N + i] = Z[i]; }
     if (resize(s, N)) return -1;
     if (upload(s, R.data(), V.data(), N, psi.data(), tp.data())) return -1;
+    if (tail_reset(s)) return -1;
     if (s->dX48) {                                   // the qstep draws continue this stream
         unsigned long long x = s->x48;
         HIPCHK(hipMemcpy(s->dX48, &x, sizeof x, hipMemcpyHostToDevice));
@@ -1166,8 +1201,11 @@ static double tail_radius(int N, double L, double lDeb, int k, double* bound) {
 // pairs (I, J) of n_J g(box distance): at density rho = N / L^3 the tiles with box distance in
 // [x, x + dx] hold about rho 4 pi (x + delta)^2 dx ions, delta = two tile widths (64 / rho)^(1/3)
 // bounding the box extents, so B(r) = rho int_r^(L/2) 4 pi (x + delta)^2 g(x) dx (tile pairs >= L/2
-// apart only hold pairs beyond the cutoff); r_t the smallest r with 2 B(r) <= eps (the factor 2 a
-// margin for the model — the kernel's measured sum is what the call reports).  Memoised per context.
+// apart only hold pairs beyond the cutoff); r_t the smallest r with 2 s B(r) <= eps (the factor 2 a
+// margin for the model, s = tail_scale: 1, raised by tail_check when a configuration's measured
+// sums exceeded eps), never beyond the a-priori radius (rigorous for any configuration).  The
+// model only picks r_t: the kernel measures every tile's sum and k_tail_fix enforces eps.
+// Memoised per context.
 static double tail_model(double r, int N, double L, double lDeb) {
     const double rho = N / (L * L * L), delta = 2. * cbrt(64. / rho), hi = L / 2.;
     if (r >= hi) return 0.;
@@ -1183,7 +1221,9 @@ static double tail_radius_sum(const mdqt_ctx* s, double* bound) {
     const double L = s->L, lDeb = s->lDeb, Rcut = L / 2.;
     *bound = 0.;
     if (k <= 0 || N < 2) return Rcut;
-    if (s->tail_key[0] == N && s->tail_key[1] == L && s->tail_key[2] == lDeb && s->tail_key[3] == k) {
+    const double sc = s->tail_scale;
+    if (s->tail_key[0] == N && s->tail_key[1] == L && s->tail_key[2] == lDeb && s->tail_key[3] == k &&
+        s->tail_key[4] == sc) {
         *bound = s->tail_val[1];
         return s->tail_val[0];
     }
@@ -1192,24 +1232,91 @@ static double tail_radius_sum(const mdqt_ctx* s, double* bound) {
     // only where the a-priori radius is below L/2 (N ~ 1e6): elsewhere the model would skip a sliver
     // just inside L/2 for nothing, and those sizes keep the exact cutoff
     double b0;
-    if (tail_radius(N, L, lDeb, k, &b0) < Rcut) {
+    const double ra = tail_radius(N, L, lDeb, k, &b0);
+    if (ra < Rcut) {
         double lo = 0., hi = Rcut;
         for (int it = 0; it < 60 && hi - lo > 1e-9 * Rcut; ++it) {
             const double m = 0.5 * (lo + hi);
-            if (m > 0 && 2. * tail_model(m, N, L, lDeb) <= eps) hi = m; else lo = m;
+            if (m > 0 && 2. * sc * tail_model(m, N, L, lDeb) <= eps) hi = m; else lo = m;
         }
         r = hi;
         b = tail_model(hi, N, L, lDeb);
+        if (r > ra) { r = ra; b = b0; }              // the a-priori radius bounds any configuration
     }
-    s->tail_key[0] = N; s->tail_key[1] = L; s->tail_key[2] = lDeb; s->tail_key[3] = k;
+    s->tail_key[0] = N; s->tail_key[1] = L; s->tail_key[2] = lDeb; s->tail_key[3] = k; s->tail_key[4] = sc;
     s->tail_val[0] = r; s->tail_val[1] = b;
     *bound = b;
     return r;
 }
-// the context's skip radius: mode 1 (measured bound) on one rank in spatial order, else a priori
-static bool tail_measured(const mdqt_ctx* s) { return s->tail_mode == 1 && s->p.world_size == 1 && s->sort_mode == 1; }
+// the context's skip radius: mode 1 (measured and enforced) in spatial order at every world size
+// (the per-tile sums are all-reduced, so 1 and W ranks run the same algorithm), else a priori
+static bool tail_measured(const mdqt_ctx* s) { return s->tail_mode == 1 && s->sort_mode == 1; }
 static double skip_radius(const mdqt_ctx* s, double* bound) {
     return tail_measured(s) ? tail_radius_sum(s, bound) : tail_radius(s->N, s->L, s->lDeb, s->tail_exp, bound);
+}
+// force_tail_mode 1 at a host synchronisation point: if tiles exceeded eps since the last check
+// (k_tail_fix summed their skipped tile pairs exactly, so those calls met eps anyway), the density
+// model underestimated this configuration's tail by u = (largest measured sum) / (the model's at
+// r_t): the next calls take r_t for tail_scale = max(2 tail_scale, 2^ceil(log2 u)) — capped at the
+// a-priori radius — and stderr says so.  Every rank sees the same all-reduced sums, so ranks
+// widen alike.
+static int tail_check(mdqt_ctx* s) {
+    if (!s->dTailSt || !s->use_n3b || !tail_measured(s)) return 0;
+    unsigned long long h[8];
+    HIPCHK(hipMemcpyAsync(h, s->dTailSt, sizeof h, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    if (h[2] <= s->tail_seen) return 0;
+    double b0, b1;
+    const double r0 = tail_radius_sum(s, &b0);
+    const double raw = u64_as_double(h[1]);
+    const double u = b0 > 0. ? raw / b0 : INFINITY;
+    // a power of two: the sums' last bits (atomic order, the ranks' partial sums) cannot move it
+    s->tail_scale = std::max(2. * s->tail_scale, std::isfinite(u) && u < 1e300 ? exp2(ceil(log2(u))) : 1e300);
+    const double r1 = tail_radius_sum(s, &b1);
+    fprintf(stderr, "mdqt: force tail over 1e-%d on %llu tile(s) so far (largest per-tile sum %.3e; the model's "
+            "%.3e at r_t = %.4f): corrected by the exact pass; r_t widened to %.4f\n", s->tail_exp,
+            (unsigned long long)h[2], raw, b0, r0, r1);
+    s->tail_seen = h[2];
+    return 0;
+}
+
+// the enforcement after a force call's tail sums are complete: list the tiles over eps, add their
+// skipped pairs exactly (k_tail_fix) to `out` (F, or this rank's dense partial)
+static int tail_enforce(mdqt_ctx* s, const N3BArgs& a, double* out) {
+    const double eps = pow(10., -s->tail_exp);
+    HIPCHK(launch_tail_max(a.tailb, a.T, eps, a.Plo * 16, std::min(a.Phi * 16, a.T), s->dTailSt, s->dTailList, s->stream));
+    HIPCHK(launch_tail_fix(a, s->dTailSt, s->dTailList, out, s->stream));
+    return 0;
+}
+
+// in-process rank group: the ranks' per-tile sums summed in rank order and handed to every rank,
+// which then enforces on its own dense partial — the ncclAllReduce of a real group (mdqt_forces)
+static int local_tail(mdqt_ctx* s) {
+    bool any = false;
+    for (mdqt_ctx* q : s->local) any = any || q->tail_pending;
+    if (!any) return 0;
+    const int T = s->tail_args.T;
+    std::vector<double> sum((size_t)T, 0.), h((size_t)T);
+    for (mdqt_ctx* q : s->local) {
+        if (!q->tail_pending || q->tail_args.T != T) return fail("local group: rank %d has no tail sums", q->p.rank);
+        HIPCHK(hipSetDevice(q->dev));
+        HIPCHK(hipMemcpyAsync(h.data(), q->tail_args.tailb, (size_t)T * sizeof(double), hipMemcpyDeviceToHost, q->stream));
+        HIPCHK(hipStreamSynchronize(q->stream));
+        for (int t = 0; t < T; ++t) sum[t] = sum[t] + h[t];
+    }
+    for (mdqt_ctx* q : s->local) {
+        HIPCHK(hipSetDevice(q->dev));
+        HIPCHK(hipMemcpyAsync(q->tail_args.tailb, sum.data(), (size_t)T * sizeof(double), hipMemcpyHostToDevice, q->stream));
+        if (tail_enforce(q, q->tail_args, q->dFr)) return -1;
+        HIPCHK(hipStreamSynchronize(q->stream));
+        q->tail_pending = false;
+    }
+    for (mdqt_ctx* q : s->local) {                 // every rank reacts here, at the same point
+        HIPCHK(hipSetDevice(q->dev));
+        if (tail_check(q)) return -1;
+    }
+    HIPCHK(hipSetDevice(s->dev));
+    return 0;
 }
 
 // the far radii: the smallest r with (N - 1) g(r) err(r) <= 10^-k, err the relative error of a term
@@ -1291,6 +1398,7 @@ static ForceArgs force_args(mdqt_ctx* s, double* out) {
 // complete: callers step the group in lockstep (all forces before any substeps).
 static int local_reduce(mdqt_ctx* s) {
     if (!s->rs_pending) return 0;
+    if (local_tail(s)) return -1;
     const int W = s->p.world_size;
     std::vector<const double*> h(W, nullptr);
     for (mdqt_ctx* q : s->local) {
@@ -1379,9 +1487,22 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         N3BArgs a;
         if (n3b_args(s, a)) return -1;
         const int W = s->p.world_size;
-        if (a.tailb) HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)a.T * sizeof(double), s->stream));
+        if (a.tailb) {
+            HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)a.T * sizeof(double), s->stream));
+            HIPCHK(hipMemsetAsync(s->dTailSt + 3, 0, sizeof(unsigned long long), s->stream));
+        }
         HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream));
-        if (a.tailb) HIPCHK(launch_tail_max(a.tailb, a.T, s->dTail + (s->capSortN + 63) / 64, s->stream));
+        if (a.tailb) {                  // measured tail: complete the per-tile sums, then enforce eps
+            if (W > 1 && s->comm) {
+                NCCLCHK(ncclAllReduce(a.tailb, a.tailb, (size_t)a.T, ncclDouble, ncclSum, s->comm, s->stream));
+            }
+            if (W == 1 || s->comm) {
+                if (tail_enforce(s, a, W == 1 ? s->dF : s->dFr)) return -1;
+            } else {                    // in-process group: once every rank has its sums (local_reduce)
+                s->tail_pending = true;
+                s->tail_args = a;
+            }
+        }
         if (W > 1) {
             if (s->comm) {
                 NCCLCHK(ncclReduceScatter(s->dFr, s->dF, (size_t)3 * s->S, ncclDouble, ncclSum, s->comm, s->stream));
@@ -2545,11 +2666,13 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     }
     if (!strcmp(name, "force_tail_exp")) {             // error-bounded tail: eps = 10^-value (0: exact)
         if (value < 0 || value > 300) return fail("force_tail_exp must be 0 (exact) .. 300");
+        if (value != s->tail_exp && tail_reset(s)) return -1;
         s->tail_exp = value;
         return 0;
     }
-    if (!strcmp(name, "force_tail_mode")) {            // 0: a-priori bound, 1: measured (one rank)
+    if (!strcmp(name, "force_tail_mode")) {            // 0: a-priori bound, 1: measured and enforced
         if (value < 0 || value > 1) return fail("force_tail_mode must be 0 (a priori) or 1 (measured)");
+        if (value != s->tail_mode && tail_reset(s)) return -1;
         s->tail_mode = value;
         return 0;
     }

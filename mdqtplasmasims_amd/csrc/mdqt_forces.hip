@@ -297,6 +297,8 @@ __device__ __forceinline__ float wave_rol1f(float v) {   // lane l <- lane (l + 
 // each step, wave_rol:1 folded into the f32 add: lane l + 1's sum of the previous step has lane l's
 // current J index) and ends in one ds_add_f64 per component at the group's last index.  Off the
 // diagonal only (a tile's pair with itself is never ultra far).
+// (its separations take xi already shifted by n L: there is no per-pair image form of it)
+static_assert(MDQT_SHIFT_I || !MDQT_UFAR32, "the f32 ultra-far form needs MDQT_SHIFT_I");
 __device__ __forceinline__ void n3b_pair_uf32(int l, double xi, double yi, double zi, const double (*pj)[128],
                                               double* ax, double* ay, double* az, double& fx, double& fy,
                                               double& fz, float cf, float invlf, float rc2f) {
@@ -568,14 +570,117 @@ void k_pairs_n3b(N3BArgs a) {
     if (tmeas && q == 0 && l < BW && P * BW + l < T && tbi[l] > 0.) atomicAdd(a.tailb + P * BW + l, tbi[l]);
 }
 
-// force_tail_mode 1: the largest per-tile tail bound of this force call into the running maximum
-// (positive doubles order as their bit patterns)
-__global__ __launch_bounds__(256) void k_tail_max(const double* __restrict__ tailb, int T, double* out) {
-    double m = 0.;
-    for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) m = fmax(m, tailb[t]);
-    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
-    if ((threadIdx.x & 63) == 0 && m > 0.)
-        atomicMax((unsigned long long*)out, (unsigned long long)__double_as_longlong(m));
+// force_tail_mode 1, after the call's per-tile tail sums are complete (all-reduced over the ranks
+// when sharded): every tile whose sum, with the sum's rounding (x (1 + 1e-12)), exceeds eps is
+// listed for k_tail_fix (this rank's tiles [own_lo, own_hi) only; the count in st[3]); the other
+// tiles' largest sum goes into the running maximum st[0] — the bound every ion met after the fix —
+// and the largest of all into st[1] (what the skip radius alone gave); st[2] counts every tile
+// over eps (the same on every rank: the host widens r_t when it grows), st[4] the measured calls.
+// Positive doubles order as their bit patterns.
+__global__ __launch_bounds__(256) void k_tail_max(const double* __restrict__ tailb, int T, double eps, int own_lo,
+                                                  int own_hi, unsigned long long* st, int* list) {
+    double m = 0., mr = 0.;
+    unsigned long long nf = 0;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) {
+        const double v = tailb[t];
+        mr = fmax(mr, v);
+        if (v * (1. + 1e-12) > eps) {
+            ++nf;
+            if (t >= own_lo && t < own_hi) list[atomicAdd(st + 3, 1ull)] = t;
+        } else {
+            m = fmax(m, v);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        m = fmax(m, __shfl_xor(m, off));
+        mr = fmax(mr, __shfl_xor(mr, off));
+        nf += __shfl_xor(nf, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (m > 0.) atomicMax(st, (unsigned long long)__double_as_longlong(m));
+        if (mr > 0.) atomicMax(st + 1, (unsigned long long)__double_as_longlong(mr));
+        if (nf) atomicAdd(st + 2, nf);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(st + 4, 1ull);
+}
+
+// classify()'s squared minimum-image gap between the boxes of tiles Iw and J — the same operations
+// in the same order, so that k_tail_fix selects exactly the tile pairs the block kernel skipped
+__device__ __forceinline__ double tile_gap2(const double* __restrict__ B, int T, int Iw, int J, double L, double invL) {
+    double g2 = 0.;
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) {
+        double d = B[(size_t)c3 * T + Iw] - B[(size_t)c3 * T + J];
+        d = fma(-__builtin_rint(d * invL), L, d);
+        const double gap = fabs(d) - (B[(size_t)(3 + c3) * T + Iw] + B[(size_t)(3 + c3) * T + J]);
+        g2 = gap > 0. ? fma(gap, gap, g2) : g2;
+    }
+    return g2;
+}
+
+// force_tail_mode 1, enforcement: for every listed tile I (its tail sum over eps) the exact sum of
+// the pairs the skip radius dropped — every J tile whose box gap g satisfies r_t < g < L/2, all
+// 64 x 64 pairs with the per-pair minimum image and the exact cutoff r < L/2 (SpeedUp:213-224) —
+// is added to I's rows of `out` (F, or the rank's dense partial before the reduce-scatter).  Then
+// each of I's ions has every pair inside L/2 (up to the far forms' own bounds).  One workgroup of
+// 4 waves per listed tile (grid-stride over the list), wave q classifying the J tiles q*64 + l +
+// 256 k lane-parallel and walking its ballot; the waves' sums combined in wave order: deterministic.
+// Each ion belongs to one tile, so the read-modify-write of `out` has one writer.  With an empty
+// list (the normal case) every workgroup reads st[3] and returns.
+__global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long long* __restrict__ st,
+                                                  const int* __restrict__ list, double* __restrict__ out) {
+    __shared__ double part[4][3][64];
+    const int n = (int)st[3];
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2, nullptr};
+    const double rs2 = a.Rskip * a.Rskip, rcut2 = a.Rcut * a.Rcut;   // classify()'s rc2 and the tail test
+    const int T = a.T, N = a.N, PS = a.Npad;
+    for (int k = blockIdx.x; k < n; k += gridDim.x) {
+        const int I = __builtin_amdgcn_readfirstlane(list[k]);
+        const int i = I * 64 + l;
+        const bool vi = i < N;
+        const double xi = vi ? a.Rs[i] : 0., yi = vi ? a.Rs[PS + i] : 0., zi = vi ? a.Rs[2 * PS + i] : 0.;
+        double fx = 0., fy = 0., fz = 0.;
+        for (int j0 = q * 64; j0 < T; j0 += 256) {
+            const int Jl = j0 + l;
+            bool in = false;
+            if (Jl < T) {
+                const double g2 = tile_gap2(a.boxes, T, I, Jl, a.L, c.invL);
+                in = g2 > rs2 && g2 < rcut2;
+            }
+            unsigned long long m = __ballot(in);
+            while (m) {
+                const int J = j0 + __builtin_ctzll(m);
+                m &= m - 1;
+                const int j = J * 64 + l;
+                const int nj = min(64, N - J * 64);
+                const double xl = j < N ? a.Rs[j] : 0., yl = j < N ? a.Rs[PS + j] : 0., zl = j < N ? a.Rs[2 * PS + j] : 0.;
+                for (int t = 0; t < nj; ++t) {
+                    auto lane_t = [t](double v) {
+                        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), t),
+                                                __builtin_amdgcn_readlane(__double2loint(v), t));
+                    };
+                    double dx = xi - lane_t(xl), dy = yi - lane_t(yl), dz = zi - lane_t(zl);
+                    mic_r(dx, dy, dz, c);
+                    const double ft = pair_ft<1>(dx, dy, dz, c);   // 0 beyond L/2
+                    fx = fma(dx, ft, fx); fy = fma(dy, ft, fy); fz = fma(dz, ft, fz);
+                }
+            }
+        }
+        part[q][0][l] = fx; part[q][1][l] = fy; part[q][2][l] = fz;
+        __syncthreads();
+        if (q == 0 && vi) {
+            const int ion = a.perm[i];
+            const int w = ion / a.S;
+            double* o = out + (size_t)w * 3 * a.S + (ion - w * a.S);
+#pragma unroll
+            for (int c3 = 0; c3 < 3; ++c3) {
+                const double v = ((part[0][c3][l] + part[1][c3][l]) + part[2][c3][l]) + part[3][c3][l];
+                o[(size_t)c3 * a.S] += v;
+            }
+        }
+        __syncthreads();
+    }
 }
 
 // canonical per-ion sum of the slots this rank wrote: j-slots db = 0 .. nd-1, then i-slots.
@@ -696,8 +801,18 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     return hipGetLastError();
 }
 
-hipError_t launch_tail_max(const double* tailb, int T, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_tail_max, dim3((T + 255) / 256 < 64 ? (T + 255) / 256 : 64), dim3(256), 0, s, tailb, T, out);
+hipError_t launch_tail_max(const double* tailb, int T, double eps, int own_lo, int own_hi, unsigned long long* st,
+                           int* list, hipStream_t s) {
+    if (T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tail_max, dim3((T + 255) / 256 < 64 ? (T + 255) / 256 : 64), dim3(256), 0, s, tailb, T, eps,
+                       own_lo, own_hi, st, list);
+    return hipGetLastError();
+}
+
+hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const int* list, double* out,
+                           hipStream_t s) {
+    if (a.T <= 0 || !a.Rs || !a.perm || !a.boxes) return hipErrorInvalidValue;   // spatial order only
+    hipLaunchKernelGGL(k_tail_fix, dim3(a.T < 512 ? a.T : 512), dim3(256), 0, s, a, st, list, out);
     return hipGetLastError();
 }
 

@@ -439,7 +439,14 @@ struct SortArgs {
 hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s);
 size_t spatial_order_tmp_bytes(int N);
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
-hipError_t launch_tail_max(const double* tailb, int T, double* out, hipStream_t s);
+// force_tail_mode 1 (mdqt_forces.hip): the per-tile tail sums against eps — st[0] running max of the
+// tiles within eps, st[1] of all, st[2] tiles over eps (cumulative), st[3] this call's list length
+// (this rank's tiles [own_lo, own_hi)), st[4] measured calls — and the exact pass over the listed
+// tiles' skipped tile pairs, added to `out` ([world][3][S], by ion)
+hipError_t launch_tail_max(const double* tailb, int T, double eps, int own_lo, int own_hi, unsigned long long* st,
+                           int* list, hipStream_t s);
+hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const int* list, double* out,
+                           hipStream_t s);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 
 // ---- Monte-Carlo + MD analytics program (mdmc_kernels.hip) ----

@@ -59,6 +59,34 @@ def check_partition(N: int, rank: int, world: int):
     return lo, hi, S
 
 
+PARITY_TOL = 1e-12
+
+
+def sharded_parity(mine: dict, ref: dict, lo: int, hi: int, L: float, all_max, tol: float = PARITY_TOL) -> dict:
+    """A sharded run checked against a world-1 run of the same inputs (bench.py's sharded lines;
+    SURVEY §8(e), reference scale-out exampleSlurmFile.slurm:3,16).
+
+    mine / ref: "F0" (forces after the first forces() call), "R", "V" (after the same MD steps) as
+    [3][N] arrays — of `mine` only this rank's slab [lo, hi) is read (a rank's copies of the other
+    slabs are stale between all-gathers).  all_max(list of floats) -> their element-wise maximum over
+    the ranks (torch.distributed all_reduce MAX: RCCL on the GPU box, gloo in the CPU test).
+    Relative errors: forces by max|F|, positions by L, velocities by max|V| — every rank's slab, so
+    one bad rank fails the check on all of them.  ok: max_rel_err <= tol (NaN fails)."""
+    import numpy as np
+    loc = []
+    for k in ("F0", "R", "V"):
+        a, b = np.asarray(mine[k])[:, lo:hi], np.asarray(ref[k])[:, lo:hi]
+        if hi > lo:
+            d = np.abs(a - b)
+            loc += [float(d.max()) if np.all(np.isfinite(d)) else float("inf"), float(np.abs(b).max())]
+        else:
+            loc += [0.0, 0.0]
+    dF, sF, dR, _, dV, sV = all_max(loc)
+    rel = {"F0": dF / sF if sF > 0 else dF, "R": dR / L, "V": dV / sV if sV > 0 else dV}
+    m = max(rel.values())
+    return {"max_rel_err": m, "rel_err": rel, "tol": tol, "ok": bool(m <= tol)}
+
+
 def create(params: dict, rank: int, world: int, local_rank: int) -> Simulation:
     """one rank's context with its RCCL communicator (collective over the world)."""
     sim = Simulation(world_size=world, rank=rank, device=local_rank, **params)

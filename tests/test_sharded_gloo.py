@@ -55,6 +55,7 @@ def _worker(rank, world, port, q):
         L, lDeb = o.const("L"), o.const("lDeb")
         ratio = int(o.const("plasmaToQuantumTimestepRatio"))
         lo, hi, S = slab(N, world, rank)
+        F0 = None
         for _ in range(3):
             st = o.get_state()
             buf = torch.zeros(world, 3, S, dtype=torch.float64)
@@ -63,12 +64,28 @@ def _worker(rank, world, port, q):
             R = np.concatenate([buf[w].numpy() for w in range(world)], axis=1)[:, :N]
             o.set_state(R, st["V"], st["psi"], st["tPart"], st["t"])
             F = O.forces_rows(R, lo, hi, L, lDeb)
+            F0 = F if F0 is None else F0
             o.set_forces(F)
             o.substeps(ratio)
         st = o.get_state()
         ref = O.OracleSim(**kw).init()
+        rF0 = O.forces_raw(ref.get_state()["R"], L, lDeb)
         ref.md_steps(3)
         rs = ref.get_state()
+        # 4. bench.py's sharded parity check (sharded.sharded_parity): each rank's slab against the
+        # world-1 run, maxima over the ranks by all_reduce MAX; then rank 1's slab perturbed by 1e-9
+        # of max|V| — every rank, rank 0 included, must see the failure
+        def all_max(vals):
+            t = torch.tensor(vals, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return t.tolist()
+        mine = {"F0": F0, "R": st["R"], "V": st["V"]}
+        refd = {"F0": rF0, "R": rs["R"], "V": rs["V"]}
+        out["parity"] = sharded.sharded_parity(mine, refd, lo, hi, L, all_max)
+        bad = dict(mine, V=st["V"].copy())
+        if rank == 1:
+            bad["V"][1, lo] += 1e-9 * np.abs(rs["V"]).max()
+        out["parity_bad"] = sharded.sharded_parity(bad, refd, lo, hi, L, all_max)
         out["bitwise"] = all(np.array_equal(st[k][..., lo:hi] if k in ("R", "V") else st[k][lo:hi],
                                             rs[k][..., lo:hi] if k in ("R", "V") else rs[k][lo:hi])
                              for k in ("R", "V", "psi", "tPart"))
@@ -119,3 +136,14 @@ def test_sharded_protocol_partition_invariant(results):
     for out in results.values():
         assert out["bitwise"]
         assert out["t"][0] == out["t"][1]
+
+
+def test_sharded_parity_check(results):
+    """bench.py's check of a sharded line against world 1: passes on the partition-invariant run
+    (first forces, then R and V after 3 MD steps: bit for bit, so 0), and a 1e-9 error confined
+    to rank 1's slab fails the check on both ranks"""
+    for out in results.values():
+        p, b = out["parity"], out["parity_bad"]
+        assert p["ok"] and p["max_rel_err"] <= 1e-15, p
+        assert not b["ok"] and 5e-10 < b["rel_err"]["V"] < 2e-9, b
+        assert b["rel_err"]["F0"] == p["rel_err"]["F0"] and b["rel_err"]["R"] == p["rel_err"]["R"]

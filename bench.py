@@ -756,6 +756,65 @@ def end_to_end_line(local, cfg, md_steps):
             "value": b["N"] * dq / el, "unit": "particle-qsteps/s"}
 
 
+N3B_KERNEL = "void mdqt::k_pairs_n3b<1, false, false>(mdqt::N3BArgs)"   # the large-N dominant kernel
+
+
+def latest_large_pmc(cfg):
+    """the newest committed PMC summary of a large line (profiles/r<round><letter>_<cfg>_pmc.json)"""
+    d = os.path.join(ROOT, "profiles")
+    fs = sorted(f for f in os.listdir(d) if f.endswith(f"_{cfg}_pmc.json") and f.startswith("r"))
+    return os.path.join(d, fs[-1]) if fs else None
+
+
+def large_roofline(cfg, census, f_avg, N, world):
+    """Roofline of a large line's dominant kernel, k_pairs_n3b.  FP64 VALU is the
+    roof (30 flop per distinct pair, ~0 B per pair after staging).  Two rates:
+    algorithmic — all N(N-1)/2 pairs, what 8(d) defines — and on the pairs the kernel actually
+    evaluates (the census: skipped tile pairs excluded, lane-steps of the evaluated ones, every tier).
+    With a PMC summary of the same config measured on this tree's kernel sources (world 1): VALU /
+    SALU / LDS instructions per evaluated pair, the VALU issue-slot fraction (VALU x 4 cycles over
+    1,024 SIMDs x the kernel's cycles GRBM_GUI_ACTIVE / 8), and the kernel's own duration from the
+    kernel trace of the same command."""
+    tot = N * (N - 1) / 2.0
+    ev = sum(v[0] for k, v in census.items() if not k.startswith("skip"))
+    peak = FP64_PEAK_TFS
+    roof = {"bound": "fp64", "kernel": N3B_KERNEL, "unit": "TFLOP/s", "peak": peak,
+            "achieved": W_F_PER_PAIR * tot / f_avg / 1e12, "frac": W_F_PER_PAIR * tot / f_avg / 1e12 / peak,
+            "fp64_frac_algorithmic": W_F_PER_PAIR * tot / f_avg / 1e12 / peak,
+            "fp64_frac_evaluated": W_F_PER_PAIR * ev / f_avg / 1e12 / peak,
+            "evaluated_lane_steps": ev, "evaluated_per_pair": ev / tot,
+            "time": "force() HIP events: spatial sort + block kernel + slot reduction (+ tail pass)",
+            "tiers": {k: {"lane_steps": v[0], "ion_pairs": v[1], "pairs_frac": v[1] / tot} for k, v in census.items()},
+            "traffic": None, "pmc": None}
+    path = latest_large_pmc(cfg)
+    if world != 1 or not path:
+        return roof
+    with open(path) as f:
+        d = json.load(f)
+    meta = d.get("_meta", {})
+    p = {"file": os.path.relpath(path, ROOT), "measured_src_hash": meta.get("src_hash"),
+         "src_hash": kernel_source_hash(), "workload": meta.get("workload")}
+    e = d.get(N3B_KERNEL)
+    if meta.get("src_hash") != p["src_hash"] or not e:
+        roof["pmc"] = dict(p, status="stale: measured on other kernel sources" if e else "kernel not in the summary")
+        return roof
+    w = ev / 64.0                                   # wave-level pair steps
+    cyc = e.get("GRBM_GUI_ACTIVE", 0) / 8.0          # the kernel's cycles (summed over the 8 XCDs)
+    p.update(status="ok", dispatches=e.get("dispatches"),
+             valu_per_evaluated_pair=e["SQ_INSTS_VALU"] / w, salu_per_evaluated_pair=e.get("SQ_INSTS_SALU", 0) / w,
+             lds_per_evaluated_pair=e.get("SQ_INSTS_LDS", 0) / w,
+             valu_issue_frac=e["SQ_INSTS_VALU"] * 4.0 / (1024.0 * cyc) if cyc else None)
+    if e.get("duration_us"):
+        ks = e["duration_us"] * 1e-6
+        p.update(kernel_us=e["duration_us"], clock_ghz=cyc / ks / 1e9 if cyc else None,
+                 fp64_frac_algorithmic_kernel=W_F_PER_PAIR * tot / ks / 1e12 / peak,
+                 fp64_frac_evaluated_kernel=W_F_PER_PAIR * ev / ks / 1e12 / peak)
+    if "FETCH_SIZE" in e and "WRITE_SIZE" in e:    # kB; FETCH x 2 per MI355X_MICROARCH.md (gfx950)
+        roof["traffic"] = (2.0 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
+    roof["pmc"] = p
+    return roof
+
+
 def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     """C5 (or C3/C4) as ONE system whose ions are sharded over the world: strong scaling."""
     import torch
@@ -774,7 +833,9 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     sim.init()                                     # collective: Epot0 over all slabs
     t_init = time.perf_counter() - t0
     ratio = int(sim.const("plasmaToQuantumTimestepRatio"))
-    check = world > 1                              # parity against a world-1 run (below)
+    # parity against a world-1 run (below); MDQT_BENCH_PARITY=1 runs the same check at world 1 (the
+    # code path of the check on a one-GPU box: the comparison is then world 1 against itself)
+    check = world > 1 or os.environ.get("MDQT_BENCH_PARITY") == "1"
     if check:
         sim.forces()                               # the first call's forces, this rank's slab
         F0 = sim.get_state()["F"]
@@ -803,6 +864,15 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     ru32 = sim.const("force_ufar32_radius")
     tail_eps = 10.0 ** -12                          # force_tail_exp default
     bound_met = bool(rt >= L / 2 or (tmode == 1 and tail <= tail_eps) or tmode == 0)
+    census = None                                  # the block kernel's work by tile-pair class
+    if int(sim.const("force_scheme")) == 3 and int(sim.const("force_sort")) == 1:
+        census = sim.force_census()                # (this rank's block pairs: summed over the ranks)
+        if world > 1:
+            keys = list(census)
+            t = torch.tensor([x for k in keys for x in census[k]], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            v = t.tolist()
+            census = {k: (v[2 * i], v[2 * i + 1]) for i, k in enumerate(keys)}
     parity = None
     if check:
         # the sharded result against a world-1 context built from the same inputs
@@ -822,7 +892,8 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
 
         def all_max(vals):
             t = torch.tensor(vals, dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if world > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return [float(x) for x in t.tolist()]
 
         parity = sharded_parity({"F0": F0, "R": st["R"], "V": st["V"]}, {"F0": rF0, "R": rs["R"], "V": rs["V"]},
@@ -847,6 +918,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force,
+            "roofline": large_roofline(cfg, census, f_avg, N, world) if census and f_avg else None,
             "parity": parity if check else {"note": "world 1: this line is the reference the sharded runs are checked against"},
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail, "bound_met": bound_met,
                            "tail_mode": "measured+enforced" if tmode == 1 else "a priori",

@@ -139,6 +139,15 @@ int         mdqt_potentials_raw(int N, double L, double lDeb, const double* R, s
                                 int nseg, int device, int variant);
 
 /* ---- diagnostics / output ---- */
+/* Work census of the Newton-3 block force kernel (N > 65,536, spatial order; this rank's block
+ * pairs) for the current positions — the tile pairs of forces() by the path they take: out[0..12)
+ * lane-steps (64 per step of a wave: 16 steps per evaluated sub-tile group, 4,096 per skipped tile
+ * pair, 2,560 on a diagonal tile), out[12..24) distinct ion pairs; classes 0 skipped beyond L/2,
+ * 1 skipped by the tail radius, 2 ragged last tile, 3 exact per-pair image, 4 exact uniform image,
+ * 5 far per-pair, 6 far uniform, 7 very far per-pair, 8 very far uniform, 9 ultra far (f64)
+ * uniform, 10 ultra far in f32, 11 skipped sub-tile groups of evaluated tile pairs.  n >= 24.  Not
+ * part of the reference's seam: the benchmark's roofline bookkeeping (VALU per evaluated pair). */
+int         mdqt_force_census(mdqt_ctx* c, double* out, int n);
 int         mdqt_epotential(mdqt_ctx* c, double* Epot);      /* Epotential(), SpeedUp:244-281   */
 /* observables of output(), SpeedUp:917-1032: out7 = t, EkinX, EkinY, EkinZ, Epot,
  * Etot-Epot0, <vx>; Pvel [3][2001] (may be NULL); pops [N][3] = S,P,D (may be NULL). */
@@ -180,20 +189,39 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     (the two differ by a few ulp per pair; both meet the 1e-13 force gate)
  *   "force_scheme":   0 = auto, 1 = owner-computes rows, 2 = Newton-3 tile pairs (one GPU),
  *                     3 = Newton-3 block pairs (auto above 65,536 ions; sharded: reduce-scatter)
- *   "force_sort":     block pairs only: 1 = Hilbert-curve order with exact skipping of tile
- *                     pairs >= L/2 apart (default), 2 = the same order, nothing skipped (bit-
- *                     identical to 1), 0 = storage order
+ *   "force_sort":     block pairs only: 1 = Hilbert-curve order with skipping of tile pairs whose
+ *                     boxes are >= the skip radius apart (default), 2 = the same order, nothing
+ *                     skipped (bit-identical to 1 where the skip radius is L/2 — every BASELINE size
+ *                     but N ~ 1e6, where 1 also skips the error-bounded tail), 0 = storage order
  *   "force_tail_exp": block pairs in spatial order: tile pairs whose boxes are >= r_t apart are
- *                     skipped, r_t the smallest radius with (N - 1) g(r_t) <= 10^-k (g(r) one
- *                     pair's |F| at distance r, SpeedUp:224): every ion's force within 10^-k of
- *                     the exact sum to L/2; k = 12 default, 0 = exact (r_t = L/2); a no-op where
- *                     r_t >= L/2 (every BASELINE size but N ~ 1e6).  mdqt_get_const
- *                     "force_skip_radius" / "force_tail_bound" report r_t and (N - 1) g(r_t)
+ *                     skipped with every ion's force kept within eps = 10^-k of the exact sum to
+ *                     L/2 (g(r) = one pair's |F| at distance r, SpeedUp:224); k = 12 default, 0 =
+ *                     exact (r_t = L/2); a no-op where the a-priori radius below is >= L/2 (every
+ *                     BASELINE size but N ~ 1e6).  "force_skip_radius" reports r_t
+ *   "force_tail_mode": how r_t is bounded.  1 (default, every world size) = measured and
+ *                     enforced: r_t from a density model of the per-tile sums (<= the a-priori
+ *                     radius); every force call sums, per tile, n_J g(box distance) over its
+ *                     skipped tile pairs (all-reduced over the ranks), and every tile whose sum
+ *                     exceeds eps gets those pairs added exactly (an exact pass over its skipped
+ *                     tile pairs), so eps holds for any configuration; when that happened the next
+ *                     host sync widens r_t (stderr says so).  "force_tail_bound" = the largest
+ *                     per-tile sum the calls met (NaN before a measured call), "force_tail_raw_bound"
+ *                     the largest before the exact pass, "force_tail_fixed_tiles" the tiles over
+ *                     eps so far, "force_tail_model_bound" the model's sum at r_t.  0 = a priori:
+ *                     r_t the smallest radius with (N - 1) g(r_t) <= eps, "force_tail_bound" that
  *   "force_far_exp":  block pairs in spatial order: tile pairs >= r_far apart evaluate their pairs
  *                     within 3e-9 relative (rsq + one Newton step, degree-6 2^f), r_far the
  *                     smallest radius with (N - 1) g(r_far) 3e-9 <= 10^-k: every ion's force
  *                     within 10^-k more; k = 13 default, 0 = off.  "force_far_radius" /
  *                     "force_far_bound" report r_far and the bound
+ *   "force_vfar_exp": the very-far form beyond r_vfar (raw v_rsq_f64, degree-5 2^f; its error
+ *                     (r/lDeb + 3) 2^-23 + 1.1e-7 relative): (N - 1) g(r) err(r) <= 10^-k; k = 13
+ *                     default, 0 = off.  "force_vfar_radius" / "force_vfar_bound"
+ *   "force_ufar_exp": the ultra-far forms: beyond r_ufar the raw rsq and 2^t by v_exp_f32, and
+ *                     beyond r_ufar32 (uniform-image tile pairs, only while the cutoff's own term
+ *                     (N - 1) g(L/2 (1 - 2^-20)) stays inside the budget) the pair terms in f32;
+ *                     each shell's bound <= 10^-k; k = 13 default, 0 = off.  "force_ufar_radius",
+ *                     "force_ufar32_radius", "force_ufar_bound" (both shells)
  *   "qt_enabled":     1 = qstep() runs in the substeps, 0 = skipped (t still advances): the
  *                     pumping programs' pump window (randomFrozenStartTag408Linear.cpp main)
  *   "qt_math":        0 = the reference's exact operations, 1 = FMA-contracted with a refined

@@ -124,7 +124,7 @@ struct mdqt_ctx {
     // exceeds eps gets the exact sum over those tile pairs added to its rows (k_tail_fix) — so every
     // ion meets eps whatever the configuration; the host widens r_t when that happened (tail_check)
     int tail_mode = MDQT_TAIL_MODE;
-    double* dTail = nullptr;       // [T]: the per-tile sums of the current call
+    double* dTail = nullptr;       // [4T]: the per-sub-tile sums of the current call
     unsigned long long* dTailSt = nullptr;   // [8]: k_tail_max's running maxima and counters
     int* dTailList = nullptr;      // [T]: this call's tiles over eps (this rank's)
     double tail_scale = 1.;        // r_t from 2 tail_scale B(r) <= eps: raised when a call exceeded eps
@@ -149,6 +149,7 @@ struct mdqt_ctx {
     size_t sortTmpBytes = 0;
     double* dRs = nullptr;         // [3][Npad] positions in sorted order
     double* dBoxes = nullptr;      // [12][T] tile boxes, raw coordinate bounds
+    double* dSubBoxes = nullptr;   // [6][4T] the 16-ion sub-tiles' boxes (the block kernel's sub-tile groups)
     int capSortN = 0;
     // overlapped MD step (option "overlap", OFF by default — measured slower): the
     // QT launch of step k runs on its own stream beside step k's force launch and waits on the
@@ -669,9 +670,11 @@ static int ensure_aux(mdqt_ctx* s) {
         if (s->p.world_size > 1 && !s->dFr)
             HIPCHK(hipMalloc(&s->dFr, (size_t)s->capS * 3 * s->p.world_size * sizeof(double)));
         if (s->sort_mode && s->N > s->capSortN) {
-            for (void* q : {(void*)s->dKeys, (void*)s->dIon, s->dSortTmp, (void*)s->dRs, (void*)s->dBoxes})
+            for (void* q : {(void*)s->dKeys, (void*)s->dIon, s->dSortTmp, (void*)s->dRs, (void*)s->dBoxes,
+                            (void*)s->dSubBoxes})
                 if (q) HIPCHK(hipFree(q));
             s->dKeys = nullptr; s->dIon = nullptr; s->dSortTmp = nullptr; s->dRs = nullptr; s->dBoxes = nullptr;
+            s->dSubBoxes = nullptr;
             const int Nc = s->N;
             const int Tc = (Nc + 63) / 64;
             HIPCHK(hipMalloc(&s->dKeys, (size_t)2 * Nc * sizeof(uint32_t)));
@@ -681,11 +684,12 @@ static int ensure_aux(mdqt_ctx* s) {
             HIPCHK(hipMalloc(&s->dSortTmp, s->sortTmpBytes));
             HIPCHK(hipMalloc(&s->dRs, (size_t)3 * Tc * 64 * sizeof(double)));
             HIPCHK(hipMalloc(&s->dBoxes, (size_t)12 * Tc * sizeof(double)));
+            HIPCHK(hipMalloc(&s->dSubBoxes, (size_t)6 * 4 * Tc * sizeof(double)));
             if (s->dTail) HIPCHK(hipFree(s->dTail));
             if (s->dTailList) HIPCHK(hipFree(s->dTailList));
             s->dTail = nullptr; s->dTailList = nullptr;
-            HIPCHK(hipMalloc(&s->dTail, (size_t)Tc * sizeof(double)));
-            HIPCHK(hipMemset(s->dTail, 0, (size_t)Tc * sizeof(double)));
+            HIPCHK(hipMalloc(&s->dTail, (size_t)4 * Tc * sizeof(double)));
+            HIPCHK(hipMemset(s->dTail, 0, (size_t)4 * Tc * sizeof(double)));
             HIPCHK(hipMalloc(&s->dTailList, (size_t)Tc * sizeof(int)));
             if (!s->dTailSt) HIPCHK(hipMalloc(&s->dTailSt, 8 * sizeof(unsigned long long)));
             s->capSortN = Nc;
@@ -726,9 +730,10 @@ static void free_device(mdqt_ctx* s) {
     s->capPairs = 0;
     if (s->dSlots) (void)hipFree(s->dSlots);
     if (s->dFr) (void)hipFree(s->dFr);
-    for (void* q : {(void*)s->dKeys, (void*)s->dIon, s->dSortTmp, (void*)s->dRs, (void*)s->dBoxes})
+    for (void* q : {(void*)s->dKeys, (void*)s->dIon, s->dSortTmp, (void*)s->dRs, (void*)s->dBoxes, (void*)s->dSubBoxes})
         if (q) (void)hipFree(q);
     s->dKeys = nullptr; s->dIon = nullptr; s->dSortTmp = nullptr; s->dRs = nullptr; s->dBoxes = nullptr;
+    s->dSubBoxes = nullptr;
     if (s->dTail) (void)hipFree(s->dTail);
     if (s->dTailList) (void)hipFree(s->dTailList);
     if (s->dTailSt) (void)hipFree(s->dTailSt);
@@ -1197,17 +1202,17 @@ static double tail_radius(int N, double L, double lDeb, int k, double* bound) {
     *bound = n1 * tail_g(hi, lDeb);
     return hi;
 }
-// force_tail_mode 1: r_t from a model of the bound the device measures, sum over the skipped tile
-// pairs (I, J) of n_J g(box distance): at density rho = N / L^3 the tiles with box distance in
-// [x, x + dx] hold about rho 4 pi (x + delta)^2 dx ions, delta = two tile widths (64 / rho)^(1/3)
-// bounding the box extents, so B(r) = rho int_r^(L/2) 4 pi (x + delta)^2 g(x) dx (tile pairs >= L/2
-// apart only hold pairs beyond the cutoff); r_t the smallest r with 2 s B(r) <= eps (the factor 2 a
+// force_tail_mode 1: r_t from a model of the bound the device measures, per 16-ion sub-tile a sum over
+// the dropped sub-blocks (a, b) of n_b g(sub-box gap): at density rho = N / L^3 the sub-tiles with box
+// gap in [x, x + dx] hold about rho 4 pi (x + delta)^2 dx ions, delta = two sub-tile widths
+// (16 / rho)^(1/3) bounding the box extents, so B(r) = rho int_r^(L/2) 4 pi (x + delta)^2 g(x) dx
+// (beyond L/2 only pairs beyond the cutoff); r_t the smallest r with 2 s B(r) <= eps (the factor 2 a
 // margin for the model, s = tail_scale: 1, raised by tail_check when a configuration's measured
 // sums exceeded eps), never beyond the a-priori radius (rigorous for any configuration).  The
 // model only picks r_t: the kernel measures every tile's sum and k_tail_fix enforces eps.
 // Memoised per context.
 static double tail_model(double r, int N, double L, double lDeb) {
-    const double rho = N / (L * L * L), delta = 2. * cbrt(64. / rho), hi = L / 2.;
+    const double rho = N / (L * L * L), delta = 2. * cbrt(16. / rho), hi = L / 2.;
     if (r >= hi) return 0.;
     const int n = 2000;                             // Simpson on [r, L/2]
     const double h = (hi - r) / n;
@@ -1284,7 +1289,7 @@ static int tail_check(mdqt_ctx* s) {
 // skipped pairs exactly (k_tail_fix) to `out` (F, or this rank's dense partial)
 static int tail_enforce(mdqt_ctx* s, const N3BArgs& a, double* out) {
     const double eps = pow(10., -s->tail_exp);
-    HIPCHK(launch_tail_max(a.tailb, a.T, eps, a.Plo * 16, std::min(a.Phi * 16, a.T), s->dTailSt, s->dTailList, s->stream));
+    HIPCHK(launch_tail_max(a.tailb, a.T, eps, s->dTailSt, s->dTailList, s->stream));
     HIPCHK(launch_tail_fix(a, s->dTailSt, s->dTailList, out, s->stream));
     return 0;
 }
@@ -1295,18 +1300,18 @@ static int local_tail(mdqt_ctx* s) {
     bool any = false;
     for (mdqt_ctx* q : s->local) any = any || q->tail_pending;
     if (!any) return 0;
-    const int T = s->tail_args.T;
-    std::vector<double> sum((size_t)T, 0.), h((size_t)T);
+    const int T = s->tail_args.T, T4 = 4 * T;                 // per-sub-tile sums
+    std::vector<double> sum((size_t)T4, 0.), h((size_t)T4);
     for (mdqt_ctx* q : s->local) {
         if (!q->tail_pending || q->tail_args.T != T) return fail("local group: rank %d has no tail sums", q->p.rank);
         HIPCHK(hipSetDevice(q->dev));
-        HIPCHK(hipMemcpyAsync(h.data(), q->tail_args.tailb, (size_t)T * sizeof(double), hipMemcpyDeviceToHost, q->stream));
+        HIPCHK(hipMemcpyAsync(h.data(), q->tail_args.tailb, (size_t)T4 * sizeof(double), hipMemcpyDeviceToHost, q->stream));
         HIPCHK(hipStreamSynchronize(q->stream));
-        for (int t = 0; t < T; ++t) sum[t] = sum[t] + h[t];
+        for (int t = 0; t < T4; ++t) sum[t] = sum[t] + h[t];
     }
     for (mdqt_ctx* q : s->local) {
         HIPCHK(hipSetDevice(q->dev));
-        HIPCHK(hipMemcpyAsync(q->tail_args.tailb, sum.data(), (size_t)T * sizeof(double), hipMemcpyHostToDevice, q->stream));
+        HIPCHK(hipMemcpyAsync(q->tail_args.tailb, sum.data(), (size_t)T4 * sizeof(double), hipMemcpyHostToDevice, q->stream));
         if (tail_enforce(q, q->tail_args, q->dFr)) return -1;
         HIPCHK(hipStreamSynchronize(q->stream));
         q->tail_pending = false;
@@ -1357,7 +1362,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.Rall = s->dR; a.slots = s->dSlots; a.S = s->S;
     a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
     a.micGuard = c.micGuard; a.guard = c.guard;
-    a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr;
+    a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr; a.subboxes = nullptr;
     double bound;
     a.Rskip = skip_radius(s, &bound);
     a.tailb = nullptr;
@@ -1374,8 +1379,9 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
         o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
         o.keys = s->dKeys; o.keys2 = s->dKeys + s->N; o.ion = s->dIon; o.perm = s->dIon + s->N;
         o.tmp = s->dSortTmp; o.tmp_bytes = s->sortTmpBytes; o.Rs = s->dRs; o.boxes = s->dBoxes;
+        o.subboxes = s->dSubBoxes;
         HIPCHK(launch_spatial_order(o, s->stream));
-        a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes;
+        a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes; a.subboxes = s->dSubBoxes;
         if (tail_measured(s) && a.Rskip < a.Rcut) a.tailb = s->dTail;
     }
     return 0;
@@ -1456,6 +1462,28 @@ static int take_events(mdqt_ctx* s, int k, hipEvent_t* e0, hipEvent_t* e1) {
     return 0;
 }
 
+// the block kernel's work by tile-pair class for the current positions (k_n3b_census): out[0, 12)
+// lane-steps, out[12, 24) distinct ion pairs — this rank's block pairs (diagnostic, outside any
+// timed region: it runs the spatial order itself)
+extern "C" int mdqt_force_census(mdqt_ctx* s, double* out, int n) {
+    if (!s || !out) return fail("mdqt_force_census: NULL argument");
+    if (n < 2 * kCensus) return fail("mdqt_force_census: need %d doubles", 2 * kCensus);
+    if (!s->use_n3b || !s->sort_mode) return fail("mdqt_force_census: Newton-3 blocks in spatial order only");
+    HIPCHK(hipSetDevice(s->dev));
+    N3BArgs a;
+    if (n3b_args(s, a)) return -1;
+    unsigned long long* d = nullptr;
+    unsigned long long h[2 * kCensus];
+    HIPCHK(hipMalloc(&d, sizeof h));
+    hipError_t e = launch_n3b_census(a, d, s->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail("mdqt_force_census: %s", hipGetErrorString(e));
+    for (int k = 0; k < 2 * kCensus; ++k) out[k] = (double)h[k];
+    return 0;
+}
+
 extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:192-236
     if (!s) return fail("NULL context");
     if (s->nloc == 0) return 0;
@@ -1488,13 +1516,13 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         if (n3b_args(s, a)) return -1;
         const int W = s->p.world_size;
         if (a.tailb) {
-            HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)a.T * sizeof(double), s->stream));
+            HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)4 * a.T * sizeof(double), s->stream));
             HIPCHK(hipMemsetAsync(s->dTailSt + 3, 0, sizeof(unsigned long long), s->stream));
         }
         HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream));
         if (a.tailb) {                  // measured tail: complete the per-tile sums, then enforce eps
             if (W > 1 && s->comm) {
-                NCCLCHK(ncclAllReduce(a.tailb, a.tailb, (size_t)a.T, ncclDouble, ncclSum, s->comm, s->stream));
+                NCCLCHK(ncclAllReduce(a.tailb, a.tailb, (size_t)4 * a.T, ncclDouble, ncclSum, s->comm, s->stream));
             }
             if (W == 1 || s->comm) {
                 if (tail_enforce(s, a, W == 1 ? s->dF : s->dFr)) return -1;

@@ -191,25 +191,26 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
     return Rall + (size_t)w * 3 * S + (g - w * S);
 }
 
-// steps whose j-side terms are combined in registers before one LDS atomic (block kernel; 1 = every
-// step its own ds_add_f64)
-#ifndef MDQT_N3B_JCOMB
-#define MDQT_N3B_JCOMB 1
-#endif
-constexpr int kJComb = MDQT_N3B_JCOMB;
-static_assert(kJComb == 1 || kJComb == 2 || kJComb == 4 || kJComb == 8 || kJComb == 16, "j-side step groups");
-__device__ __forceinline__ double wave_rol1(double v) {   // lane l <- lane (l + 1) mod 64
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x134, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x134, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
+// Sub-tile groups (round 4).  The J tile sits in LDS by 16-ion sub-tiles, each twice over: J ion
+// 16 b + m at LDS index 32 b + m and 32 b + 16 + m (n3b_lds).  Lane l = 16 a + m (I sub-tile a) runs a
+// tile pair as four groups of 16 steps: group d pairs I sub-tile a with J sub-tile (a + d) & 3 — a
+// cyclic diagonal of the 4 x 4 sub-block matrix — and at step t lane l meets J ion
+// 16 ((a + d) & 3) + ((m + t) & 15) at LDS index 32 ((a + d) & 3) + m + t (immediate offsets t).  A
+// group covers its four sub-blocks once, and at every step the 64 lanes meet 64 distinct J ions (the
+// j-side ds_add_f64 stays conflict-free).  Group d runs iff bit d of `groups` (wave-uniform): a group
+// whose four sub-blocks all have sub-tile boxes farther apart than the skip radius is skipped — the
+// pairs of a tile pair that straddles the cutoff sphere (or the tail radius) by less than a whole
+// tile pair (tools/subtile_cull_model.py).  The diagonal tile (I = J): group 0 with
+// t = 1..8 (t = 8 for m < 8 only: each pair inside a sub-tile once), group 1, and group 2 for a < 2
+// (the sub-tile pairs (0, 2), (1, 3) once); group 3 would repeat group 1's pairs.
+__device__ __forceinline__ int n3b_lds(int l) { return 32 * (l >> 4) + (l & 15); }   // J ion l's first copy
 
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
           bool POT = false, int FAR = 0>
-__device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi, double zi, double mi,
-                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
-                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
-                                         const double* nsh = nullptr) {
+__device__ __forceinline__ void n3b_pair(bool diag, unsigned groups, int l, double xi, double yi, double zi,
+                                         double mi, const double (*pj)[128], const double* mj, double* ax,
+                                         double* ay, double* az, double& fx, double& fy, double& fz,
+                                         const PairC& c, const double* nsh = nullptr) {
     // every 16 steps the LDS arrays are re-based at the lane's index (an opaque register), so the
     // 16 unrolled steps address them with immediate offsets t, 128 + t, 256 + t: without it the
     // compiler's strength reduction moved the base past the arrays and spent a v_add_u32 per
@@ -220,121 +221,59 @@ __device__ __forceinline__ void n3b_pair(bool diag, int l, double xi, double yi,
     const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);                    \
     const double* mjb = mj + b_;                                                           \
     double *axb = ax + b_, *ayb = ay + b_, *azb = az + b_
-    if constexpr (kJComb > 1) {
-        // j side combined over kJComb consecutive steps before one ds_add_f64 per component: at
-        // step t lane l's pair is with J index l + t, at step t + 1 lane l + 1's is too, so the
-        // running sum rotated one lane down (wave_rol:1, lane l reads lane l + 1) plus this step's
-        // term is the sum for lane l's current J index; lane 63 receives lane 0's sum, whose index
-        // differs by 64 — the same J ion (the tile sits in LDS twice, the halves summed at the end)
-        auto group = [&](auto&& pjb, const double* mjb, double* axb, double* ayb, double* azb, int t, double m,
-                         double& jx, double& jy, double& jz) {
-            double px, py, pz;
-            n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, m, xi, yi, zi, mi, pjb, mjb, fx, fy, fz, c, nsh,
-                                                                   px, py, pz);
-            if (t % kJComb == 0) {
-                jx = px; jy = py; jz = pz;
-            } else {
-                jx = wave_rol1(jx) + px;
-                if constexpr (!POT) { jy = wave_rol1(jy) + py; jz = wave_rol1(jz) + pz; }
-            }
-            if (t % kJComb == kJComb - 1) {
-                __hip_atomic_fetch_add(&axb[t], jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                if constexpr (!POT) {
-                    __hip_atomic_fetch_add(&ayb[t], jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    __hip_atomic_fetch_add(&azb[t], jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                }
-            }
-        };
-        if (!diag) {
-            for (int t0 = 0; t0 < 64; t0 += 16) {
-                N3B_REBASE(l + t0);
-                double jx = 0., jy = 0., jz = 0.;
-#pragma unroll
-                for (int t = 0; t < 16; ++t) group(pjb, mjb, axb, ayb, azb, t, 1., jx, jy, jz);
-            }
-        } else {
-            for (int t0 = 1; t0 < 33; t0 += 16) {
-                N3B_REBASE(l + t0);
-                double jx = 0., jy = 0., jz = 0.;
-#pragma unroll
-                for (int t = 0; t < 16; ++t)
-                    group(pjb, mjb, axb, ayb, azb, t, (t0 + t == 32 && l >= 32) ? 0. : 1., jx, jy, jz);
-            }
-        }
-    } else if (!diag) {
-        for (int t0 = 0; t0 < 64; t0 += 16) {
-            N3B_REBASE(l + t0);
+    const int a = l >> 4, m = l & 15;
+    if (!diag) {
+        for (int d = 0; d < 4; ++d) {
+            if (!((groups >> d) & 1u)) continue;    // wave-uniform
+            N3B_REBASE(32 * ((a + d) & 3) + m);
 #pragma unroll
             for (int t = 0; t < 16; ++t)
                 n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, 1., xi, yi, zi, mi, pjb, mjb, axb, ayb, azb,
                                                                       fx, fy, fz, c, nsh);
         }
     } else {
-        for (int t0 = 1; t0 < 33; t0 += 16) {
-            N3B_REBASE(l + t0);
+        {
+            N3B_REBASE(32 * a + m + 1);
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const double m = (t0 + t == 32 && l >= 32) ? 0. : 1.;   // lane distance 32: once
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, m, xi, yi, zi, mi, pjb, mjb, axb, ayb, azb,
+            for (int t = 0; t < 8; ++t)            // sub-tile distance 8: once (m < 8)
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, (t == 7 && m >= 8) ? 0. : 1., xi, yi, zi, mi,
+                                                                      pjb, mjb, axb, ayb, azb, fx, fy, fz, c, nsh);
+        }
+        for (int d = 1; d < 3; ++d) {
+            N3B_REBASE(32 * ((a + d) & 3) + m);
+            const double w = (d == 2 && a >= 2) ? 0. : 1.;
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, w, xi, yi, zi, mi, pjb, mjb, axb, ayb, azb,
                                                                       fx, fy, fz, c, nsh);
-            }
         }
     }
 #undef N3B_REBASE
 }
 
-#ifndef MDQT_UFAR32_PK
-#define MDQT_UFAR32_PK 0   // packed f32 (v_pk_*): measured slower at N = 1M (329.6-330.5 vs 325.6-327.2 ms, A/B)
-#endif
-__device__ __forceinline__ float wave_rol1f(float v) {   // lane l <- lane (l + 1) mod 64
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xF, 0xF, false));
+__device__ __forceinline__ float row_rol1f(float v) {   // lane 16 a + m <- lane 16 a + ((m + 1) & 15)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x12F, 0xF, 0xF, false));   // row_ror:15
 }
 
 // An ultra-far tile pair (boxes >= r_ufar32 apart) with a uniform image, pair terms in f32
 // (MDQT_UFAR32; error analysis and bound in mdqt_internal.hpp kUfar32A/B): dx = fl32(xi - n L - xj)
-// from the f64 separation, v_rsq_f32, 2^t by v_exp_f32, the cutoff on the f32 r^2 (t = -inf).  Per 16-step group the i side is summed in f32 registers and then added to the
-// f64 partial, and the j side runs as MDQT_N3B_JCOMB does (the running sum rotated one lane down
-// each step, wave_rol:1 folded into the f32 add: lane l + 1's sum of the previous step has lane l's
-// current J index) and ends in one ds_add_f64 per component at the group's last index.  Off the
-// diagonal only (a tile's pair with itself is never ultra far).
-// (its separations take xi already shifted by n L: there is no per-pair image form of it)
+// from the f64 separation, v_rsq_f32, 2^t by v_exp_f32, the cutoff on the f32 r^2 (t = -inf).  Per
+// 16-step group the i side is summed in f32 registers and then added to the f64 partial; the j side
+// is a running sum rotated one lane down inside the lane's row of 16 each step (row_ror:15 folded
+// into the f32 add: lane m + 1's sum of the previous step is for lane m's current J ion) and ends in
+// one ds_add_f64 per component at the group's last index.  Off the diagonal only (a tile's pair with
+// itself is never ultra far); its separations take xi already shifted by n L.
 static_assert(MDQT_SHIFT_I || !MDQT_UFAR32, "the f32 ultra-far form needs MDQT_SHIFT_I");
-__device__ __forceinline__ void n3b_pair_uf32(int l, double xi, double yi, double zi, const double (*pj)[128],
-                                              double* ax, double* ay, double* az, double& fx, double& fy,
-                                              double& fz, float cf, float invlf, float rc2f) {
-    for (int t0 = 0; t0 < 64; t0 += 16) {
-        int b_ = l + t0;
+__device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, double xi, double yi, double zi,
+                                              const double (*pj)[128], double* ax, double* ay, double* az,
+                                              double& fx, double& fy, double& fz, float cf, float invlf, float rc2f) {
+    const int a = l >> 4, m = l & 15;
+    for (int d = 0; d < 4; ++d) {
+        if (!((groups >> d) & 1u)) continue;        // wave-uniform
+        int b_ = 32 * ((a + d) & 3) + m;
         asm volatile("" : "+v"(b_));                // immediate LDS offsets (N3B_REBASE)
         const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);
         float ix = 0.f, iy = 0.f, iz = 0.f, jx = 0.f, jy = 0.f, jz = 0.f;
-#if MDQT_UFAR32_PK
-        // two steps per iteration in packed f32 (v_pk_mul/add/fma_f32: two lanes' worth per
-        // instruction); the i side in two interleaved sums, combined at the group's end
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 ix2 = {0.f, 0.f}, iy2 = {0.f, 0.f}, iz2 = {0.f, 0.f};
-        const f2 cf2 = {cf, cf}, il2 = {invlf, invlf};
-#pragma unroll
-        for (int t = 0; t < 16; t += 2) {
-            const f2 dx = {(float)(xi - pjb[0][t]), (float)(xi - pjb[0][t + 1])};
-            const f2 dy = {(float)(yi - pjb[1][t]), (float)(yi - pjb[1][t + 1])};
-            const f2 dz = {(float)(zi - pjb[2][t]), (float)(zi - pjb[2][t + 1])};
-            const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
-            const f2 ri = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
-            const f2 tt = (r2 * ri) * cf2;
-            const f2 e = {__builtin_amdgcn_exp2f(r2.x < rc2f ? tt.x : -INFINITY),
-                          __builtin_amdgcn_exp2f(r2.y < rc2f ? tt.y : -INFINITY)};
-            const f2 ft = ((ri + il2) * e) * (ri * ri);
-            const f2 px = dx * ft, py = dy * ft, pz = dz * ft;
-            ix2 += px; iy2 += py; iz2 += pz;
-            if (t == 0) {
-                jx = px.x; jy = py.x; jz = pz.x;
-            } else {
-                jx = wave_rol1f(jx) + px.x; jy = wave_rol1f(jy) + py.x; jz = wave_rol1f(jz) + pz.x;
-            }
-            jx = wave_rol1f(jx) + px.y; jy = wave_rol1f(jy) + py.y; jz = wave_rol1f(jz) + pz.y;
-        }
-        ix = ix2.x + ix2.y; iy = iy2.x + iy2.y; iz = iz2.x + iz2.y;
-#else
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const float dx = (float)(xi - pjb[0][t]), dy = (float)(yi - pjb[1][t]), dz = (float)(zi - pjb[2][t]);
@@ -348,16 +287,92 @@ __device__ __forceinline__ void n3b_pair_uf32(int l, double xi, double yi, doubl
                 jx = px; jy = py; jz = pz;
             } else {
                 ix += px; iy += py; iz += pz;
-                jx = wave_rol1f(jx) + px; jy = wave_rol1f(jy) + py; jz = wave_rol1f(jz) + pz;
+                jx = row_rol1f(jx) + px; jy = row_rol1f(jy) + py; jz = row_rol1f(jz) + pz;
             }
         }
-#endif
         __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         fx += (double)ix; fy += (double)iy; fz += (double)iz;
     }
 }
+
+// The class of tile pair (Iw, J) in spatial order (SpeedUp:222 keeps a pair only below r = L/2):
+// returns the minimum-image multiples n_x, n_y, n_z of a uniform image and the class — skip when the
+// boxes are farther apart than sqrt(r.rc2) (use_sort 1): -1 beyond L/2 (no pair inside the cutoff),
+// -2 inside L/2 (the error-bounded tail: its pairs count in the tail sums) — else bit 0 = uniform
+// image (FAST: the fast variant) + 2 x the far level (1 far, 2 very far, 3 ultra far, 4 ultra far in
+// f32); g2 = the squared box gap.  Shared by k_pairs_n3b (the staging wave's lanes) and k_n3b_census.
+struct N3BRadii { double rc2, rf2, rv2, ru2, ru32; };
+// the squared radii of the classes: skip below the cutoff only for the forces (error-bounded tail,
+// mdqt_engine.cpp tail_radius); the far forms are the fast force variant's
+template <int VARIANT, bool POT>
+__device__ __forceinline__ N3BRadii n3b_radii(const N3BArgs& a) {
+    N3BRadii r;
+    r.rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
+    r.rf2 = (POT || VARIANT != 1 || !(a.Rfar < a.Rcut)) ? INFINITY : a.Rfar * a.Rfar;
+    r.rv2 = (POT || VARIANT != 1 || !(a.Rvfar < a.Rcut)) ? INFINITY : a.Rvfar * a.Rvfar;
+    r.ru2 = (POT || VARIANT != 1 || !(a.Rufar < a.Rcut)) ? INFINITY : a.Rufar * a.Rufar;
+    r.ru32 = (POT || VARIANT != 1 || !MDQT_UFAR32 || !(a.Rufar32 < a.Rcut)) ? INFINITY : a.Rufar32 * a.Rufar32;
+    return r;
+}
+template <bool FAST>
+__device__ __forceinline__ double4 n3b_classify(const N3BArgs& a, double invL, const N3BRadii& r, int Iw, int J,
+                                                double& g2) {
+    const double* B = a.boxes;
+    const int T = a.T;
+    g2 = 0.;
+    bool uni = true;
+    double n[3];
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) {
+        double d = B[(size_t)c3 * T + Iw] - B[(size_t)c3 * T + J];
+        d = fma(-__builtin_rint(d * invL), a.L, d);
+        const double gap = fabs(d) - (B[(size_t)(3 + c3) * T + Iw] + B[(size_t)(3 + c3) * T + J]);
+        g2 = gap > 0. ? fma(gap, gap, g2) : g2;
+        const double lo = B[(size_t)(6 + c3) * T + Iw] - B[(size_t)(9 + c3) * T + J];
+        const double hi = B[(size_t)(9 + c3) * T + Iw] - B[(size_t)(6 + c3) * T + J];
+        const double nlo = __builtin_rint(lo * invL), nhi = __builtin_rint(hi * invL);
+        uni = uni && (nlo == nhi);
+        n[c3] = nlo;
+    }
+    const double cls = (a.use_sort == 1 && g2 > r.rc2) ? (g2 < a.Rcut * a.Rcut ? -2. : -1.)
+                                                        : ((FAST && uni) ? 1. : 0.) +
+                                                              (g2 > r.ru32 ? 8. : g2 > r.ru2 ? 6. : g2 > r.rv2 ? 4. :
+                                                               g2 > r.rf2 ? 2. : 0.);
+    return make_double4(n[0], n[1], n[2], cls);
+}
+
+// the squared minimum-image gap between the boxes of 16-ion sub-tiles s and u ([6][T4] layout)
+__device__ __forceinline__ double sub_gap2(const double* __restrict__ SB, int T4, int s, int u, double L,
+                                           double invL) {
+    double g2 = 0.;
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) {
+        double d = SB[(size_t)c3 * T4 + s] - SB[(size_t)c3 * T4 + u];
+        d = fma(-__builtin_rint(d * invL), L, d);
+        const double gap = fabs(d) - (SB[(size_t)(3 + c3) * T4 + s] + SB[(size_t)(3 + c3) * T4 + u]);
+        g2 = gap > 0. ? fma(gap, gap, g2) : g2;
+    }
+    return g2;
+}
+// the group mask of an off-diagonal tile pair from its 16 sub-block activities (bit 4 a + b: sub-tiles
+// (a, b) closer than the skip radius): bit d = any sub-block (a, (a + d) & 3) active
+__host__ __device__ __forceinline__ unsigned sub_groups_of(unsigned act16) {
+    unsigned g = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) g |= ((act16 >> (4 * a + ((a + d) & 3))) & 1u) << d;
+    return g;
+}
+// one pair's |F| bound at distance d >= the box gap (SpeedUp:224 times r): the tail sums' g
+__device__ __forceinline__ double tail_gd(double g2, double invlDeb) {
+    const double d = sqrt(g2);
+    return (1. / d + invlDeb) * exp(-d * invlDeb) / d;
+}
+// real ions of 16-ion sub-tile s (0 for the padding of the ragged last tile)
+__device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0, min(16, N - 16 * s)); }
 
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
 template <int VARIANT, bool GUARD, bool POT = false>
@@ -392,60 +407,38 @@ void k_pairs_n3b(N3BArgs a) {
     }
     // Tile-pair classes in spatial order (SpeedUp:222 keeps a pair only below r = L/2), decided
     // for all BW waves' tile pairs (I, J) by the staging wave's lanes 0..BW-1 into tp[q]:
-    //  * skip (force_sort 1): boxes >= L/2 apart in the minimum image — no pair inside the
-    //    cutoff, the tile pair adds exact zeros;
+    //  * skip (force_sort 1): boxes beyond the skip radius in the minimum image — at L/2 no pair
+    //    inside the cutoff (exact zeros), inside L/2 the error-bounded tail (tail sums below);
     //  * uniform image: every pair's raw separation fl(xi - xj) lies in [fl(lo_I - hi_J),
     //    fl(hi_I - lo_J)] (rounding is monotone), and so does rint(fl(dx / L)) between the rints
     //    of the two ends; equal ends = one minimum-image multiple per axis for every pair, bit for
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
-    // class: -1 skip; otherwise bit 0 = uniform image, + 2 x the far level (1 far pair form, 2 very
-    // far, 3 ultra far, 4 ultra far in f32; forces only): 0 .. 9
+    // class: -1 / -2 skip; otherwise bit 0 = uniform image, + 2 x the far level (1 far pair form, 2
+    // very far, 3 ultra far, 4 ultra far in f32; forces only): 0 .. 9.  Then every wave takes the
+    // sub-tile groups of its own tile pair (16 sub-block gaps, one per lane).
     __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class
-    // skip below the cutoff only for the forces (error-bounded tail, mdqt_engine.cpp tail_radius)
-    const double rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
-    const double rf2 = (POT || VARIANT != 1 || !(a.Rfar < a.Rcut)) ? INFINITY : a.Rfar * a.Rfar;
-    const double rv2 = (POT || VARIANT != 1 || !(a.Rvfar < a.Rcut)) ? INFINITY : a.Rvfar * a.Rvfar;
-    const double ru2 = (POT || VARIANT != 1 || !(a.Rufar < a.Rcut)) ? INFINITY : a.Rufar * a.Rufar;
-    const double ru32 = (POT || VARIANT != 1 || !MDQT_UFAR32 || !(a.Rufar32 < a.Rcut)) ? INFINITY
-                                                                                      : a.Rufar32 * a.Rufar32;
+    const N3BRadii rad = n3b_radii<VARIANT, POT>(a);
     // the f32 form's constants as wave-uniform SGPR values (in VGPRs they were spilled and reloaded
     // inside the pair loop at the kernel's 64-VGPR budget)
     auto sgpr_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
     const float cf32 = sgpr_f((float)(a.invlDeb * kNegLog2e)), invl32 = sgpr_f((float)a.invlDeb),
                 rc2f = sgpr_f((float)a.rc2);
-    auto classify = [&](int Iw, int J, double& g2) {   // lane-parallel over Iw (staging wave)
-        const double* B = a.boxes;
-        g2 = 0.;
-        bool uni = true;
-        double n[3];
-#pragma unroll
-        for (int c3 = 0; c3 < 3; ++c3) {
-            double d = B[(size_t)c3 * T + Iw] - B[(size_t)c3 * T + J];
-            d = fma(-__builtin_rint(d * c.invL), a.L, d);
-            const double gap = fabs(d) - (B[(size_t)(3 + c3) * T + Iw] + B[(size_t)(3 + c3) * T + J]);
-            g2 = gap > 0. ? fma(gap, gap, g2) : g2;
-            const double lo = B[(size_t)(6 + c3) * T + Iw] - B[(size_t)(9 + c3) * T + J];
-            const double hi = B[(size_t)(9 + c3) * T + Iw] - B[(size_t)(6 + c3) * T + J];
-            const double nlo = __builtin_rint(lo * c.invL), nhi = __builtin_rint(hi * c.invL);
-            uni = uni && (nlo == nhi);
-            n[c3] = nlo;
-        }
-        const double cls = (a.use_sort == 1 && g2 > rc2) ? -1.
-                                                          : ((VARIANT == 1 && uni) ? 1. : 0.) +
-                                                                (g2 > ru32 ? 8. : g2 > ru2 ? 6. : g2 > rv2 ? 4. :
-                                                                 g2 > rf2 ? 2. : 0.);
-        return make_double4(n[0], n[1], n[2], cls);
-    };
     // the run's i accumulator lives in LDS (read and written once per block distance) so that
     // the three-level blocking fits the 64-VGPR budget of two 16-wave workgroups per CU
     double* fi = irun[q][0];
     fi[l] = 0.; fi[64 + l] = 0.; fi[128 + l] = 0.;
-    // force_tail_mode 1 (a.tailb): the staging lanes' tail bound of their I tiles (I side, over the
-    // whole run) and of the current J tile (J side, summed by thread 0 after the barrier)
-    __shared__ double tbi[BW], tbj[BW];
+    // force_tail_mode 1 (a.tailb, per 16-ion sub-tile): every pair the call drops inside L/2 — in a
+    // tile pair skipped by the tail radius, or in a skipped sub-tile group — is at least its sub-block
+    // gap apart, so each ion of I sub-tile a loses at most sum_b n_b g(gap_ab) and each ion of J
+    // sub-tile b sum_a n_a g(gap_ab); counted once per unordered tile pair.  The I side is kept per
+    // wave over the run (tbi[q]), the J side summed over the waves in LDS per J tile (tbj) and added
+    // to the global sums by thread 0 after the tile's work.
+    __shared__ double tbi[BW][4], tbj[4];
     const bool tmeas = !POT && a.tailb != nullptr;
-    if (tmeas && q == 0 && l < BW) tbi[l] = 0.;
+    if (tmeas && l < 4) tbi[q][l] = 0.;
+    if (tmeas && threadIdx.x < 4) tbj[threadIdx.x] = 0.;
+    const int T4 = 4 * T;
     double* ax = accj[q][0];
     double* ay = accj[q][1];
     double* az = accj[q][2];
@@ -457,31 +450,20 @@ void k_pairs_n3b(N3BArgs a) {
         for (int b = 0; b < BW; ++b) {
             const int J = Q * BW + b;
             if (J >= T) break;
-            if (q == 0) {                           // stage J (twice over)
+            if (q == 0) {                           // stage J (by sub-tiles, twice over)
                 const int j = J * 64 + l;
                 const bool vj = j < N;
                 const double* p = tile_ptr(J) + l;
                 const double xj = vj ? p[0] : pad, yj = vj ? p[PS] : pad, zj = vj ? p[2 * PS] : pad;
-                pj[0][l] = xj; pj[0][l + 64] = xj;
-                pj[1][l] = yj; pj[1][l + 64] = yj;
-                pj[2][l] = zj; pj[2][l + 64] = zj;
-                mj[l] = vj ? 1. : 0.; mj[l + 64] = mj[l];
-                if (tmeas && l < BW) tbj[l] = 0.;
+                const int li = n3b_lds(l);
+                pj[0][li] = xj; pj[0][li + 16] = xj;
+                pj[1][li] = yj; pj[1][li + 16] = yj;
+                pj[2][li] = zj; pj[2][li + 16] = zj;
+                mj[li] = vj ? 1. : 0.; mj[li + 16] = mj[li];
                 if (srt && l < BW && P * BW + l < T) {
                     double g2;
-                    const double4 t4 = classify(P * BW + l, J, g2);
+                    const double4 t4 = n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2);
                     tp[l][0] = t4.x; tp[l][1] = t4.y; tp[l][2] = t4.z; tp[l][3] = t4.w;
-                    // a tile pair skipped by the tail radius (boxes >= Rskip apart) with a pair that
-                    // may lie inside L/2: each of its pairs is >= sqrt(g2) apart, so each ion of I
-                    // loses at most n_J g(sqrt(g2)) and each ion of J n_I g(sqrt(g2)); counted once per
-                    // unordered tile pair (block distance 0: J > I only)
-                    const int Iw = P * BW + l;
-                    if (tmeas && t4.w < 0. && g2 < a.Rcut * a.Rcut && (db > 0 || J > Iw)) {
-                        const double d = sqrt(g2);
-                        const double gd = (1. / d + a.invlDeb) * exp(-d / a.lDeb) / d;
-                        tbi[l] += (double)min(64, N - J * 64) * gd;
-                        tbj[l] = (double)min(64, N - Iw * 64) * gd;
-                    }
 #if defined(MDQT_EXPT_CLS)
                     atomicAdd(&g_cls_count[t4.w < 0. ? 0 : 1 + ((int)t4.w & 1)], 1ull);
 #endif
@@ -490,25 +472,42 @@ void k_pairs_n3b(N3BArgs a) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
             __syncthreads();
-            if (tmeas && threadIdx.x == 0) {
-                double sj = 0.;
-                for (int w = 0; w < BW; ++w) sj += tbj[w];
-                if (sj > 0.) atomicAdd(a.tailb + J, sj);
-            }
             const double cls = srt ? uniform_f64(tp[q][3]) : 0.;
-            if (vI && (db > 0 || J >= I) && cls >= 0.) {
-                const bool diag = (db == 0 && J == I);
+            const bool mine = vI && (db > 0 || J >= I);
+            const bool diag = (db == 0 && J == I);
+            unsigned groups = 0xFu;
+            if (a.use_sort == 1 && mine && !diag && (cls >= 0. || (tmeas && cls == -2.))) {   // (2: nothing skipped)
+                // the tile pair's 16 sub-blocks, lane l < 16: (a, b) = (l >> 2, l & 3)
+                const int sa = l >> 2, sb = l & 3;
+                const double sg = l < 16 ? sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, c.invL) : INFINITY;
+                const unsigned act = (unsigned)__ballot(l < 16 && sg <= rad.rc2);
+                groups = __builtin_amdgcn_readfirstlane(sub_groups_of(act));
+                if (tmeas && (db > 0 || J > I)) {          // once per unordered tile pair
+                    const bool evald = cls >= 0. && ((groups >> ((sb - sa) & 3)) & 1u);
+                    double gi = 0., gj = 0.;
+                    if (l < 16 && !evald && sg < a.Rcut * a.Rcut) {
+                        const double gd = tail_gd(sg, a.invlDeb);
+                        gi = sub_count(N, 4 * J + sb) * gd;     // for I sub-tile sa
+                        gj = sub_count(N, 4 * I + sa) * gd;     // for J sub-tile sb
+                    }
+                    gi += __shfl_xor(gi, 1); gi += __shfl_xor(gi, 2);       // over b: lanes 4 sa .. 4 sa + 3
+                    gj += __shfl_xor(gj, 4); gj += __shfl_xor(gj, 8);       // over a: lanes sb, sb + 4, ..
+                    if (l < 16 && sb == 0 && gi > 0.) tbi[q][sa] += gi;
+                    if (l < 4 && gj > 0.) atomicAdd(&tbj[l], gj);
+                }
+            }
+            if (mine && cls >= 0. && groups) {
                 const int ci = (int)cls;            // bit 0 uniform image, bits 1-3 far level
                 const int fl = ci >> 1;
-                // blocked i accumulation: the tile pair's 64 steps into a fresh sum, those into the
+                // blocked i accumulation: the tile pair's steps into a fresh sum, those into the
                 // block distance's sum, those into the run's (a run is ~1e5 pair terms at N = 1e6;
                 // in spatial order they arrive in coherent groups, and one serial chain would
                 // carry their rounding: momentum |sum F| / mean |F| 1.8e-8 -> 1e-10 at C4)
                 double tx = 0., ty = 0., tz = 0.;
                 constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
                 if (ragN && (I == T - 1 || J == T - 1))
-                    n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty,
-                                                                    tz, c);
+                    n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                    az, tx, ty, tz, c);
                 else if (VARIANT == 1 && (ci & 1)) {       // uniform image
                     const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
                     // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
@@ -518,46 +517,51 @@ void k_pairs_n3b(N3BArgs a) {
                     if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
                         if (fl == 4) {              // ultra far in f32
 #if !defined(MDQT_EXPT_UFAR_SKIP)                   // (diagnostic build: skip them, wrong results)
-                            n3b_pair_uf32(l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
+                            n3b_pair_uf32(groups, l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
 #endif
                         }
                         else if (fl == 3)           // ultra far tile pair
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
-                                                                               az, tx, ty, tz, c, nsh);
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(diag, groups, l, sx, sy, sz, mi, pj, mj,
+                                                                               ax, ay, az, tx, ty, tz, c, nsh);
                         else if (fl == 2)           // very far tile pair
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
-                                                                               az, tx, ty, tz, c, nsh);
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(diag, groups, l, sx, sy, sz, mi, pj, mj,
+                                                                               ax, ay, az, tx, ty, tz, c, nsh);
                         else if (fl == 1)           // far tile pair: the far pair form
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 1>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
-                                                                               az, tx, ty, tz, c, nsh);
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 1>(diag, groups, l, sx, sy, sz, mi, pj, mj,
+                                                                               ax, ay, az, tx, ty, tz, c, nsh);
                         else
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(diag, l, sx, sy, sz, mi, pj, mj, ax, ay,
-                                                                            az, tx, ty, tz, c, nsh);
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(diag, groups, l, sx, sy, sz, mi, pj, mj, ax,
+                                                                            ay, az, tx, ty, tz, c, nsh);
                     } else {
-                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, l, sx, sy, sz, mi, pj, mj, ax,
-                                                                                ay, az, tx, ty, tz, c, nsh);
+                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, groups, l, sx, sy, sz, mi, pj, mj,
+                                                                                ax, ay, az, tx, ty, tz, c, nsh);
                     }
                 } else if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
                     if (fl >= 2)                    // (ultra far with a per-pair image: rare, very-far form)
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay,
-                                                                            az, tx, ty, tz, c);
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                            ay, az, tx, ty, tz, c);
                     else if (fl == 1)
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay,
-                                                                            az, tx, ty, tz, c);
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                            ay, az, tx, ty, tz, c);
                     else
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az,
-                                                                         tx, ty, tz, c);
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                         az, tx, ty, tz, c);
                 } else
-                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx,
-                                                                     ty, tz, c);
+                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay, az,
+                                                                     tx, ty, tz, c);
                 bx += tx; by += ty; bz += tz;
             }
             __syncthreads();
             if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db
+                const int li = n3b_lds(l);
                 double v = 0.;
 #pragma unroll
-                for (int w = 0; w < BW; ++w) v = v + (accj[w][q][l] + accj[w][q][l + 64]);
+                for (int w = 0; w < BW; ++w) v = v + (accj[w][q][li] + accj[w][q][li + 16]);
                 a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? v : -v;
+            }
+            if (tmeas && threadIdx.x < 4) {         // J's sub-tile sums of this J step -> global
+                if (tbj[threadIdx.x] > 0.) atomicAdd(a.tailb + 4 * J + threadIdx.x, tbj[threadIdx.x]);
+                tbj[threadIdx.x] = 0.;
             }
             __syncthreads();
         }
@@ -567,26 +571,26 @@ void k_pairs_n3b(N3BArgs a) {
         double* o = a.slots + (size_t)(a.nd + run) * plane + i;
         o[0] = fi[l]; o[a.Npad] = fi[64 + l]; o[2 * (size_t)a.Npad] = fi[128 + l];
     }
-    if (tmeas && q == 0 && l < BW && P * BW + l < T && tbi[l] > 0.) atomicAdd(a.tailb + P * BW + l, tbi[l]);
+    if (tmeas && vI && l < 4 && tbi[q][l] > 0.) atomicAdd(a.tailb + 4 * I + l, tbi[q][l]);
 }
 
-// force_tail_mode 1, after the call's per-tile tail sums are complete (all-reduced over the ranks
-// when sharded): every tile whose sum, with the sum's rounding (x (1 + 1e-12)), exceeds eps is
-// listed for k_tail_fix (this rank's tiles [own_lo, own_hi) only; the count in st[3]); the other
-// tiles' largest sum goes into the running maximum st[0] — the bound every ion met after the fix —
-// and the largest of all into st[1] (what the skip radius alone gave); st[2] counts every tile
-// over eps (the same on every rank: the host widens r_t when it grows), st[4] the measured calls.
-// Positive doubles order as their bit patterns.
-__global__ __launch_bounds__(256) void k_tail_max(const double* __restrict__ tailb, int T, double eps, int own_lo,
-                                                  int own_hi, unsigned long long* st, int* list) {
+// force_tail_mode 1, after the call's per-sub-tile tail sums are complete (all-reduced over the
+// ranks when sharded): every tile with a sub-tile sum that, with the sum's rounding (x (1 + 1e-12)),
+// exceeds eps is listed for k_tail_fix (st[3] the list length; the same list on every rank); the
+// other sums' largest goes into the running maximum st[0] — the bound every ion met after the fix —
+// and the largest of all into st[1] (what the skip radius alone gave); st[2] counts the tiles over
+// eps (the host widens r_t when it grows), st[4] the measured calls.  Positive doubles order as
+// their bit patterns.
+__global__ __launch_bounds__(256) void k_tail_max(const double* __restrict__ tailb, int T, double eps,
+                                                  unsigned long long* st, int* list) {
     double m = 0., mr = 0.;
     unsigned long long nf = 0;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) {
-        const double v = tailb[t];
+        const double v = fmax(fmax(tailb[4 * t], tailb[4 * t + 1]), fmax(tailb[4 * t + 2], tailb[4 * t + 3]));
         mr = fmax(mr, v);
         if (v * (1. + 1e-12) > eps) {
             ++nf;
-            if (t >= own_lo && t < own_hi) list[atomicAdd(st + 3, 1ull)] = t;
+            list[atomicAdd(st + 3, 1ull)] = t;
         } else {
             m = fmax(m, v);
         }
@@ -604,49 +608,40 @@ __global__ __launch_bounds__(256) void k_tail_max(const double* __restrict__ tai
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(st + 4, 1ull);
 }
 
-// classify()'s squared minimum-image gap between the boxes of tiles Iw and J — the same operations
-// in the same order, so that k_tail_fix selects exactly the tile pairs the block kernel skipped
-__device__ __forceinline__ double tile_gap2(const double* __restrict__ B, int T, int Iw, int J, double L, double invL) {
-    double g2 = 0.;
-#pragma unroll
-    for (int c3 = 0; c3 < 3; ++c3) {
-        double d = B[(size_t)c3 * T + Iw] - B[(size_t)c3 * T + J];
-        d = fma(-__builtin_rint(d * invL), L, d);
-        const double gap = fabs(d) - (B[(size_t)(3 + c3) * T + Iw] + B[(size_t)(3 + c3) * T + J]);
-        g2 = gap > 0. ? fma(gap, gap, g2) : g2;
-    }
-    return g2;
-}
-
-// force_tail_mode 1, enforcement: for every listed tile I (its tail sum over eps) the exact sum of
-// the pairs the skip radius dropped — every J tile whose box gap g satisfies r_t < g < L/2, all
-// 64 x 64 pairs with the per-pair minimum image and the exact cutoff r < L/2 (SpeedUp:213-224) —
-// is added to I's rows of `out` (F, or the rank's dense partial before the reduce-scatter).  Then
-// each of I's ions has every pair inside L/2 (up to the far forms' own bounds).  One workgroup of
-// 4 waves per listed tile (grid-stride over the list), wave q classifying the J tiles q*64 + l +
-// 256 k lane-parallel and walking its ballot; the waves' sums combined in wave order: deterministic.
-// Each ion belongs to one tile, so the read-modify-write of `out` has one writer.  With an empty
-// list (the normal case) every workgroup reads st[3] and returns.
+// force_tail_mode 1, enforcement: every listed tile's ions get their force recomputed exactly —
+// all pairs inside L/2 (SpeedUp:213-224: per-pair minimum image, the exact cutoff, the fast pair
+// form's values), over every J tile whose box is within L/2 of the tile's box — and the result
+// REPLACES their rows of `out`: on the rank that owns the tile's block (F, or its dense partial
+// before the reduce-scatter; the other ranks write 0 there, so the sum over the ranks is the exact
+// force).  Replacing (not adding the dropped pairs) holds whatever the block kernel skipped: whole
+// tile pairs, sub-tile groups, far forms.  One workgroup of 4 waves per listed tile (grid-stride
+// over the list), wave q classifying the J tiles q*64 + l + 256 k lane-parallel and walking its
+// ballot; the waves' sums combined in wave order: deterministic.  Each ion belongs to one tile, so
+// `out` has one writer per ion.  With an empty list (the normal case) every workgroup reads st[3]
+// and returns.
 __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long long* __restrict__ st,
                                                   const int* __restrict__ list, double* __restrict__ out) {
     __shared__ double part[4][3][64];
     const int n = (int)st[3];
     const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
     const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2, nullptr};
-    const double rs2 = a.Rskip * a.Rskip, rcut2 = a.Rcut * a.Rcut;   // classify()'s rc2 and the tail test
+    const double rcut2 = a.Rcut * a.Rcut;
+    const N3BRadii none = {rcut2, INFINITY, INFINITY, INFINITY, INFINITY};
     const int T = a.T, N = a.N, PS = a.Npad;
     for (int k = blockIdx.x; k < n; k += gridDim.x) {
         const int I = __builtin_amdgcn_readfirstlane(list[k]);
+        const bool own = I / BW >= a.Plo && I / BW < a.Phi;
         const int i = I * 64 + l;
         const bool vi = i < N;
         const double xi = vi ? a.Rs[i] : 0., yi = vi ? a.Rs[PS + i] : 0., zi = vi ? a.Rs[2 * PS + i] : 0.;
         double fx = 0., fy = 0., fz = 0.;
-        for (int j0 = q * 64; j0 < T; j0 += 256) {
+        for (int j0 = q * 64; own && j0 < T; j0 += 256) {
             const int Jl = j0 + l;
             bool in = false;
             if (Jl < T) {
-                const double g2 = tile_gap2(a.boxes, T, I, Jl, a.L, c.invL);
-                in = g2 > rs2 && g2 < rcut2;
+                double g2;
+                (void)n3b_classify<false>(a, c.invL, none, I, Jl, g2);
+                in = g2 < rcut2;
             }
             unsigned long long m = __ballot(in);
             while (m) {
@@ -662,7 +657,7 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
                     };
                     double dx = xi - lane_t(xl), dy = yi - lane_t(yl), dz = zi - lane_t(zl);
                     mic_r(dx, dy, dz, c);
-                    const double ft = pair_ft<1>(dx, dy, dz, c);   // 0 beyond L/2
+                    const double ft = pair_ft<1>(dx, dy, dz, c);   // 0 beyond L/2 and for i = j
                     fx = fma(dx, ft, fx); fy = fma(dy, ft, fy); fz = fma(dz, ft, fz);
                 }
             }
@@ -674,13 +669,76 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
             const int w = ion / a.S;
             double* o = out + (size_t)w * 3 * a.S + (ion - w * a.S);
 #pragma unroll
-            for (int c3 = 0; c3 < 3; ++c3) {
-                const double v = ((part[0][c3][l] + part[1][c3][l]) + part[2][c3][l]) + part[3][c3][l];
-                o[(size_t)c3 * a.S] += v;
-            }
+            for (int c3 = 0; c3 < 3; ++c3)
+                o[(size_t)c3 * a.S] = ((part[0][c3][l] + part[1][c3][l]) + part[2][c3][l]) + part[3][c3][l];
         }
         __syncthreads();
     }
+}
+
+// Census of the block kernel's work (diagnostic; bench.py's large lines): k_pairs_n3b's loop over
+// this rank's block pairs without the pair terms — every tile pair classified by n3b_classify and
+// its sub-tile groups by the same sub-block gaps, counted by the path the kernel takes, as
+// lane-steps (its work: 64 per step of a wave, 16 steps per sub-tile group; 40 steps on a diagonal
+// tile) in out[0, kCensus) and as distinct ion pairs in out[kCensus, 2 kCensus).  Classes:
+// 0 skipped (boxes beyond L/2), 1 skipped by the tail radius, 2 ragged last tile (exact, per-pair
+// image), 3 exact per-pair image, 4 exact uniform image, 5 far per-pair, 6 far uniform, 7 very far
+// per-pair (ultra far with a per-pair image included), 8 very far uniform, 9 ultra far uniform (f64),
+// 10 ultra far uniform in f32, 11 skipped sub-tile groups of evaluated tile pairs.  One workgroup
+// per (block P, block distance db); thread (b, q) takes tile pair (16 P + q, 16 Q + b) as the
+// kernel's wave q at J-step b does.
+__global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long h[2 * kCensus];
+    const int t = threadIdx.x;
+    if (t < 2 * kCensus) h[t] = 0;
+    __syncthreads();
+    const int P = a.Plo + (int)blockIdx.x / a.nd, db = (int)blockIdx.x % a.nd;
+    const int q = t & (BW - 1), b = t / BW;
+    const int Q = (P + db) % a.NB;
+    const int I = P * BW + q, J = Q * BW + b;
+    const bool half = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;   // the other half covers it
+    if (!half && I < a.T && J < a.T && (db > 0 || J >= I)) {
+        const N3BRadii rad = n3b_radii<1, false>(a);
+        double g2;
+        const double4 t4 = n3b_classify<true>(a, 1. / a.L, rad, I, J, g2);
+        const bool diag = db == 0 && J == I;
+        const double nI = (double)min(64, a.N - I * 64), nJ = (double)min(64, a.N - J * 64);
+        int k;
+        if (t4.w < 0.) {
+            k = t4.w == -2. ? 1 : 0;
+        } else if ((a.N & 63) && (I == a.T - 1 || J == a.T - 1)) {
+            k = 2;
+        } else {
+            const int ci = (int)t4.w, fl = ci >> 1;
+            if (ci & 1) k = fl == 4 ? 10 : fl == 3 ? 9 : fl == 2 ? 8 : fl == 1 ? 6 : 4;
+            else k = fl >= 2 ? 7 : fl == 1 ? 5 : 3;
+        }
+        if (diag) {
+            atomicAdd(&h[k], 2560ull);
+            atomicAdd(&h[kCensus + k], (unsigned long long)(nI * (nI - 1) / 2));
+        } else if (k < 2) {
+            atomicAdd(&h[k], 4096ull);
+            atomicAdd(&h[kCensus + k], (unsigned long long)(nI * nJ));
+        } else {
+            const int T4 = 4 * a.T;
+            unsigned act = 0;
+            double np[4] = {0., 0., 0., 0.};       // ion pairs per group
+            for (int sa = 0; sa < 4; ++sa)
+                for (int sb = 0; sb < 4; ++sb) {
+                    if (sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, 1. / a.L) <= rad.rc2) act |= 1u << (4 * sa + sb);
+                    np[(sb - sa) & 3] += sub_count(a.N, 4 * I + sa) * sub_count(a.N, 4 * J + sb);
+                }
+            const unsigned g = a.use_sort == 1 ? sub_groups_of(act) : 0xFu;   // (2: nothing skipped)
+            double on = 0., off = 0.;
+            for (int d = 0; d < 4; ++d) ((g >> d) & 1u ? on : off) += np[d];
+            atomicAdd(&h[k], 1024ull * (unsigned)__builtin_popcount(g));
+            atomicAdd(&h[kCensus + k], (unsigned long long)on);
+            atomicAdd(&h[11], 1024ull * (unsigned)(4 - __builtin_popcount(g)));
+            atomicAdd(&h[kCensus + 11], (unsigned long long)off);
+        }
+    }
+    __syncthreads();
+    if (t < 2 * kCensus && h[t]) atomicAdd(out + t, h[t]);
 }
 
 // canonical per-ion sum of the slots this rank wrote: j-slots db = 0 .. nd-1, then i-slots.
@@ -801,11 +859,10 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     return hipGetLastError();
 }
 
-hipError_t launch_tail_max(const double* tailb, int T, double eps, int own_lo, int own_hi, unsigned long long* st,
-                           int* list, hipStream_t s) {
+hipError_t launch_tail_max(const double* tailb, int T, double eps, unsigned long long* st, int* list, hipStream_t s) {
     if (T <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_tail_max, dim3((T + 255) / 256 < 64 ? (T + 255) / 256 : 64), dim3(256), 0, s, tailb, T, eps,
-                       own_lo, own_hi, st, list);
+                       st, list);
     return hipGetLastError();
 }
 
@@ -813,6 +870,14 @@ hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const
                            hipStream_t s) {
     if (a.T <= 0 || !a.Rs || !a.perm || !a.boxes) return hipErrorInvalidValue;   // spatial order only
     hipLaunchKernelGGL(k_tail_fix, dim3(a.T < 512 ? a.T : 512), dim3(256), 0, s, a, st, list, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s) {
+    if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // the classes need the boxes
+    const int nblk = (a.Phi - a.Plo) * a.nd;
+    if (hipMemsetAsync(out, 0, 2 * kCensus * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
+    if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(256), 0, s, a, out);
     return hipGetLastError();
 }
 

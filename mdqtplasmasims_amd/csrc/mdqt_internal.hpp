@@ -421,9 +421,11 @@ struct N3BArgs {
     double Rskip;       // force tile pairs whose boxes are >= Rskip apart are skipped (use_sort 1):
                         // Rcut exactly (every skipped pair is beyond L/2), or the error-bounded tail
                         // radius r_t < L/2 of mdqt_engine.cpp tail_radius (potentials: always Rcut)
-    double* tailb;      // force_tail_mode 1: per tile, the sum over its tail-skipped tile pairs (boxes
-                        // >= Rskip apart, < L/2) of n_J g(box distance) — the measured bound on what
-                        // each of its ions loses (zeroed before the launch; nullptr: not measured)
+    double* tailb;      // force_tail_mode 1: per 16-ion sub-tile [4T], the sum over the pairs the call
+                        // drops inside L/2 (tail-skipped tile pairs, skipped sub-tile groups) of
+                        // n_b g(sub-block gap) — the measured bound on what each of its ions loses
+                        // (zeroed before the launch; nullptr: not measured)
+    const double* subboxes;   // [6][4T]: the 16-ion sub-tiles' centers and half extents (use_sort)
 };
 struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]
@@ -435,18 +437,21 @@ struct SortArgs {
     size_t tmp_bytes;
     double* Rs;              // out [3][Npad]
     double* boxes;           // out [12][T]
+    double* subboxes;        // out [6][4T]: the 16-ion sub-tiles' centers and half extents (or null)
 };
 hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s);
 size_t spatial_order_tmp_bytes(int N);
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
-// force_tail_mode 1 (mdqt_forces.hip): the per-tile tail sums against eps — st[0] running max of the
-// tiles within eps, st[1] of all, st[2] tiles over eps (cumulative), st[3] this call's list length
-// (this rank's tiles [own_lo, own_hi)), st[4] measured calls — and the exact pass over the listed
-// tiles' skipped tile pairs, added to `out` ([world][3][S], by ion)
-hipError_t launch_tail_max(const double* tailb, int T, double eps, int own_lo, int own_hi, unsigned long long* st,
-                           int* list, hipStream_t s);
+// force_tail_mode 1 (mdqt_forces.hip): the per-sub-tile tail sums [4T] against eps — st[0] running
+// max of the tiles within eps, st[1] of all, st[2] tiles over eps (cumulative), st[3] this call's
+// list length, st[4] measured calls — and the exact recomputation of the listed tiles' forces,
+// written into `out` ([world][3][S], by ion) on the rank that owns the tile (0 on the others)
+hipError_t launch_tail_max(const double* tailb, int T, double eps, unsigned long long* st, int* list, hipStream_t s);
 hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const int* list, double* out,
                            hipStream_t s);
+// census of k_pairs_n3b's work by tile-pair class (mdqt_forces.hip k_n3b_census): out[2 kCensus]
+constexpr int kCensus = 12;
+hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 
 // ---- Monte-Carlo + MD analytics program (mdmc_kernels.hip) ----
@@ -557,12 +562,14 @@ inline void launch_timed(F kernel, dim3 grid, dim3 block, hipStream_t s, hipEven
 // through `instance`): tests check which instance a configuration's production launch takes.
 enum QTKernel : int {
     QTK_NONE = 0,
-    QTK_LANES_IM_EDZ = 1,      // k_substeps_lanes_im<true, true>: model 0 FAST + IM01 + EDZ (C2 production)
+    QTK_LANES_IM_EDZ = 1,      // k_substeps_lanes_im<true, true, true>: model 0 FAST + IM01 + EDZ, no
+                               // renormalisation (the C2 production launch)
     QTK_LANES_IM = 2,          // k_substeps_lanes_im<true, false>
     QTK_LANES_R_FAST = 3,      // k_substeps_lanes_r<true, true>
     QTK_LANES_R = 4,           // k_substeps_lanes_r<true, false>
     QTK_LANES_R_PUMP_FAST = 5, // k_substeps_lanes_r<false, true>
     QTK_LANES_R_PUMP = 6,      // k_substeps_lanes_r<false, false>
+    QTK_LANES_IM_EDZ_RN = 7,   // k_substeps_lanes_im<true, true, false>: the same with reNormalizewvFns on
     QTK_THREAD_R = 10,         // k_substeps_r<model>: 10 + model
     QTK_MD_STEP = 20,          // k_md_step (one launch per MD step)
     QTK_EXACT_LANES = 30,      // k_substeps_lanes<fast>: 30 + qt_math

@@ -922,7 +922,7 @@ hipError_t launch_substeps_r(const SubstepArgs& a, const FastTab* tab, int mode,
                     inst = QTK_LANES_IM_EDZ;
                 } else if (a.expdet_zero && MDQT_EDZ) {
                     launch_timed(k_substeps_lanes_im<true, true>, gl, bl, s, ev0, ev1, a, tab + 1);
-                    inst = QTK_LANES_IM_EDZ;
+                    inst = QTK_LANES_IM_EDZ_RN;
                 } else {
                     launch_timed(k_substeps_lanes_im<true, false>, gl, bl, s, ev0, ev1, a, tab + 1);
                     inst = QTK_LANES_IM;

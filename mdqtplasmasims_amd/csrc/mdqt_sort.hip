@@ -12,7 +12,8 @@
 //                    sorts the same gathered positions gets the same order
 //   k_gather_sorted  positions in sorted order, [3][Npad]
 //   k_tile_boxes     per 64-ion tile: a reference ion, the minimum-image offsets of the others
-//                    from it, their min / max per axis -> center and half extents
+//                    from it, their min / max per axis -> center and half extents; the same per
+//                    16-ion sub-tile
 // Skipped pairs would have added exact zeros, so the forces are bit-identical with and without
 // the skipping for a given order (tests/test_gpu_large.py checks it).
 #include "mdqt_internal.hpp"
@@ -85,9 +86,10 @@ __global__ __launch_bounds__(256) void k_gather_sorted(const double* __restrict_
 
 // one wave per tile; boxes[c][T] = center, boxes[3 + c][T] = half extent (+ a rounding margin),
 // boxes[6 + c][T] / boxes[9 + c][T] = min / max of the raw coordinates (exact; for the tile pair's
-// uniform minimum image in k_pairs_n3b)
+// uniform minimum image in k_pairs_n3b); sub (if not null) [6][4T]: center and half extent of the
+// tile's four 16-ion sub-tiles (k_pairs_n3b's sub-tile groups and tail sums)
 __global__ __launch_bounds__(256) void k_tile_boxes(const double* __restrict__ Rs, int N, int Npad, int T, double L,
-                                                    double* __restrict__ boxes) {
+                                                    double* __restrict__ boxes, double* __restrict__ sub) {
     const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int l = threadIdx.x & 63;
     if (tile >= T) return;                                 // wave-uniform
@@ -115,6 +117,22 @@ __global__ __launch_bounds__(256) void k_tile_boxes(const double* __restrict__ R
             boxes[(size_t)(6 + c) * T + tile] = rl;
             boxes[(size_t)(9 + c) * T + tile] = rh;
         }
+        if (sub) {                                         // the four 16-ion sub-tiles' boxes, the same
+            const double sref = X[tile * 64 + (l & 48)];   // way from each sub-tile's first ion
+            double e = v ? X[j] - sref : 0.;
+            e = fma(-__builtin_rint(e * invL), L, e);
+            double slo = e, shi = e;
+#pragma unroll
+            for (int m = 8; m >= 1; m >>= 1) {
+                slo = fmin(slo, __shfl_xor(slo, m));
+                shi = fmax(shi, __shfl_xor(shi, m));
+            }
+            if ((l & 15) == 0) {
+                const int st = 4 * tile + (l >> 4);
+                sub[(size_t)c * 4 * T + st] = sref + 0.5 * (slo + shi);
+                sub[(size_t)(3 + c) * 4 * T + st] = 0.5 * (shi - slo) * (1. + 1e-12) + 1e-12 * L;
+            }
+        }
     }
 }
 
@@ -128,7 +146,8 @@ hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gather_sorted, dim3((a.Npad + 255) / 256), dim3(256), 0, s, a.Rall, a.N, a.S, a.Npad,
                        a.perm, a.Rs);
     const int T = a.Npad / 64;
-    hipLaunchKernelGGL(k_tile_boxes, dim3((T + 3) / 4), dim3(256), 0, s, a.Rs, a.N, a.Npad, T, a.L, a.boxes);
+    hipLaunchKernelGGL(k_tile_boxes, dim3((T + 3) / 4), dim3(256), 0, s, a.Rs, a.N, a.Npad, T, a.L, a.boxes,
+                       a.subboxes);
     return hipGetLastError();
 }
 

@@ -330,6 +330,17 @@ class Simulation:
         else:
             check(lib().mdqt_enable_timing_at(self.h, int(period), int(kinds), int(offset)))
 
+    CENSUS_CLASSES = ("skip_cut", "skip_tail", "ragged", "exact_image", "exact_uniform", "far_image",
+                      "far_uniform", "vfar_image", "vfar_uniform", "ufar_uniform", "ufar32_uniform", "skip_sub")
+
+    def force_census(self):
+        """the Newton-3 block kernel's work by tile-pair class for the current positions (this rank's
+        block pairs): {class: (lane_steps, ion_pairs)} (include/mdqt.h mdqt_force_census)"""
+        n = len(self.CENSUS_CLASSES)
+        out = (C.c_double * (2 * n))()
+        check(lib().mdqt_force_census(self.h, out, 2 * n), "force_census")
+        return {k: (out[i], out[n + i]) for i, k in enumerate(self.CENSUS_CLASSES)}
+
     def kernel_time_totals(self):
         """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""
         a = C.c_double(); b = C.c_double(); na = C.c_int(); nb = C.c_int()

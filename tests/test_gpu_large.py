@@ -134,6 +134,32 @@ def test_large_config_forces_and_interval(cfg, orc):
 
 
 @pytest.mark.gpu
+def test_force_census_covers_every_pair():
+    """mdqt_force_census (the bench's per-tier pair counts): every distinct ion pair of the system is
+    in exactly one tile pair of one class — the classes' ion pairs sum to N(N-1)/2 — at C3 (no tail
+    skipping: r_t = L/2) and in a world-2 group (the ranks' censuses add up)"""
+    import mdqtplasmasims_amd as M
+    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C3"]).init()
+    N = s.N
+    c = s.force_census()
+    pairs = sum(v[1] for v in c.values())
+    work = sum(v[0] for k, v in c.items() if not k.startswith("skip"))
+    print(f"C3 census: " + ", ".join(f"{k} {v[1] / (N * (N - 1) / 2):.3f}" for k, v in c.items())
+          + f"; evaluated lane-steps / (N(N-1)/2) = {work / (N * (N - 1) / 2):.3f}")
+    assert pairs == N * (N - 1) // 2
+    assert c["skip_tail"] == (0, 0) and c["skip_cut"][1] > 0 and c["ufar32_uniform"] == (0, 0)
+    st = s.get_state()
+    s.close()
+    tot = 0
+    for r in range(2):
+        x = M.Simulation(seed=SEED, job=1, rng_mode=1, world_size=2, rank=r, **CONFIGS["C3"])
+        x.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+        tot += sum(v[1] for v in x.force_census().values())
+        x.close()
+    assert tot == N * (N - 1) // 2
+
+
+@pytest.mark.gpu
 def test_spatial_order_tile_skipping_is_exact(orc):
     """Newton-3 blocks in Hilbert order (mdqt_sort.hip): skipping tile pairs whose boxes are >= L/2
     apart changes nothing (they add exact zeros) — bit for bit against the same order without

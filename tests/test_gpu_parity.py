@@ -265,14 +265,16 @@ def test_md_steps_short_horizon(eng, orc, qt, qt_math):
         assert np.array_equal(a["tPart"] == 0, b["tPart"] == 0)
 
 
-QTK_LANES_IM_EDZ = 1         # mdqt_internal.hpp QTKernel: k_substeps_lanes_im<true, true>
+QTK_LANES_IM_EDZ = 1         # mdqt_internal.hpp QTKernel: k_substeps_lanes_im<true, true, true> (no renorm)
+QTK_LANES_IM_EDZ_RN = 7      # the same instance with reNormalizewvFns on
 
 
 def test_c2_headline_qt_instance_matches_oracle(eng, orc):
     """BASELINE configs[1] (C2) exactly as bench.py runs it — N0 = 3500, seed 12346, job 1,
     Philox (rng_mode 1), every option at its default — against the oracle over 3 MD steps with
     quantum jumps.  The production launch must be the one the headline number times:
-    k_substeps_lanes_im<true, true> (FAST + IM01 + EDZ) summing all 56 Newton-3 tile slots in its
+    k_substeps_lanes_im<true, true, true> (FAST + IM01 + EDZ, no renormalisation: the reference's
+    reNormalizewvFns = false) summing all 56 Newton-3 tile slots in its
     lane-distributed prologue (lane k: slots k, k + 16, k + 32, k + 48 — all 16 lanes busy only
     at >= 49 slots), so a slot-sum bug shared with the thread-per-ion kernel cannot hide behind
     a self-comparison.  SpeedUp:438-717 (qstep), :1369-1377 (the MD step's cadence)."""
@@ -447,6 +449,8 @@ def test_lane_and_thread_qt_kernels_bit_identical(eng, N0, extra, qt_math):
         s.set_option("substep_kernel", mode)
         s.set_option("qt_math", qt_math)
         s.md_steps(3)
+        if mode == 2 and qt_math == 2 and extra.get("reNormalizewvFns"):
+            assert s.const("qt_kernel") == QTK_LANES_IM_EDZ_RN     # not the production (no-renorm) code
         sims.append(s.get_state())
     a, b = sims
     jumped = (a["tPart"] < 3 * 0.002).sum()

@@ -2,9 +2,12 @@
 """Per-kernel averages of rocprofv3 --pmc counters (one rocpd database per pass).
 
     python tools/pmc_summary.py gpurun_out/pmc_fetch/run_results.db gpurun_out/pmc_write/run_results.db ...
+        [--factors FETCH WRITE] [--trace gpurun_out/trace/run_results.db] [--tag NAME]
 
 Counter values are summed over the rows of one dispatch (per-SE / per-XCD instances), then
 averaged over the dispatches of each kernel.  Prints JSON {kernel: {counter: mean, "dispatches": n}}.
+With --trace (a --kernel-trace database of the same command, un-profiled counters) each kernel also
+gets its average dispatch duration "duration_us"; --tag records what workload the passes ran.
 """
 import collections
 import json
@@ -34,6 +37,15 @@ def main(args):
         k = dbs.index("--factors")
         meta["fetch_factor"], meta["write_factor"] = float(dbs[k + 1]), float(dbs[k + 2])
         dbs = dbs[:k] + dbs[k + 3:]
+    trace = None
+    if "--trace" in dbs:
+        k = dbs.index("--trace")
+        trace = dbs[k + 1]
+        dbs = dbs[:k] + dbs[k + 2:]
+    if "--tag" in dbs:
+        k = dbs.index("--tag")
+        meta["workload"] = dbs[k + 1]
+        dbs = dbs[:k] + dbs[k + 2:]
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for db in dbs:
         for (k, d, n), v in load(db).items():
@@ -42,6 +54,12 @@ def main(args):
     for k, cs in agg.items():
         out[k] = {n: sum(v) / len(v) for n, v in cs.items()}
         out[k]["dispatches"] = max(len(v) for v in cs.values())
+    if trace:
+        c = sqlite3.connect(trace)
+        for name, calls, avg in c.execute("select name, total_calls, average from top_kernels"):
+            if name in out:
+                out[name]["duration_us"] = avg                  # top_kernels: microseconds (tools/prof_summary.py)
+                out[name]["trace_dispatches"] = calls
     print(json.dumps(out, indent=1, sort_keys=True))
 
 

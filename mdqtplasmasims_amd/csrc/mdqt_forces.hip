@@ -205,50 +205,54 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
 // (the sub-tile pairs (0, 2), (1, 3) once); group 3 would repeat group 1's pairs.
 __device__ __forceinline__ int n3b_lds(int l) { return 32 * (l >> 4) + (l & 15); }   // J ion l's first copy
 
-template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
-          bool POT = false, int FAR = 0>
-__device__ __forceinline__ void n3b_pair(bool diag, unsigned groups, int l, double xi, double yi, double zi,
-                                         double mi, const double (*pj)[128], const double* mj, double* ax,
-                                         double* ay, double* az, double& fx, double& fy, double& fz,
-                                         const PairC& c, const double* nsh = nullptr) {
-    // every 16 steps the LDS arrays are re-based at the lane's index (an opaque register), so the
-    // 16 unrolled steps address them with immediate offsets t, 128 + t, 256 + t: without it the
-    // compiler's strength reduction moved the base past the arrays and spent a v_add_u32 per
-    // ds_add_f64 (3.5 VALU per pair, ~8 % of the block kernel's instructions)
+// every 16 steps the LDS arrays are re-based at the lane's index (an opaque register), so the 16
+// unrolled steps address them with immediate offsets t, 128 + t, 256 + t: without it the compiler's
+// strength reduction moved the base past the arrays and spent a v_add_u32 per ds_add_f64 (3.5 VALU
+// per pair, ~8 % of the block kernel's instructions)
 #define N3B_REBASE(b0)                                                                     \
     int b_ = (b0);                                                                         \
     asm volatile("" : "+v"(b_));                                                           \
     const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);                    \
     const double* mjb = mj + b_;                                                           \
     double *axb = ax + b_, *ayb = ay + b_, *azb = az + b_
+
+// one sub-tile group: 16 rotation steps from LDS index b0 (the lane's first J ion) with weight w
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
+          bool POT = false, int FAR = 0, int NSTEP = 16>
+__device__ __forceinline__ void n3b_group(int b0, double w, double xi, double yi, double zi, double mi,
+                                          const double (*pj)[128], const double* mj, double* ax, double* ay,
+                                          double* az, double& fx, double& fy, double& fz, const PairC& c,
+                                          const double* nsh, double w_last = 1.) {
+    N3B_REBASE(b0);
+#pragma unroll
+    for (int t = 0; t < NSTEP; ++t)
+        n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, t == NSTEP - 1 ? w * w_last : w, xi, yi, zi, mi, pjb,
+                                                              mjb, axb, ayb, azb, fx, fy, fz, c, nsh);
+}
+
+// a whole tile pair in one pair form: the groups of `groups` (off the diagonal) or the diagonal
+// tile's three groups
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
+          bool POT = false, int FAR = 0>
+__device__ __forceinline__ void n3b_pair(bool diag, unsigned groups, int l, double xi, double yi, double zi,
+                                         double mi, const double (*pj)[128], const double* mj, double* ax,
+                                         double* ay, double* az, double& fx, double& fy, double& fz,
+                                         const PairC& c, const double* nsh = nullptr) {
     const int a = l >> 4, m = l & 15;
     if (!diag) {
         for (int d = 0; d < 4; ++d) {
             if (!((groups >> d) & 1u)) continue;    // wave-uniform
-            N3B_REBASE(32 * ((a + d) & 3) + m);
-#pragma unroll
-            for (int t = 0; t < 16; ++t)
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, 1., xi, yi, zi, mi, pjb, mjb, axb, ayb, azb,
-                                                                      fx, fy, fz, c, nsh);
+            n3b_group<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(32 * ((a + d) & 3) + m, 1., xi, yi, zi, mi, pj, mj,
+                                                                    ax, ay, az, fx, fy, fz, c, nsh);
         }
     } else {
-        {
-            N3B_REBASE(32 * a + m + 1);
-#pragma unroll
-            for (int t = 0; t < 8; ++t)            // sub-tile distance 8: once (m < 8)
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, (t == 7 && m >= 8) ? 0. : 1., xi, yi, zi, mi,
-                                                                      pjb, mjb, axb, ayb, azb, fx, fy, fz, c, nsh);
-        }
-        for (int d = 1; d < 3; ++d) {
-            N3B_REBASE(32 * ((a + d) & 3) + m);
-            const double w = (d == 2 && a >= 2) ? 0. : 1.;
-#pragma unroll
-            for (int t = 0; t < 16; ++t)
-                n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, w, xi, yi, zi, mi, pjb, mjb, axb, ayb, azb,
-                                                                      fx, fy, fz, c, nsh);
-        }
+        // sub-tile distance 1..8 inside each sub-tile, the 8th once (m < 8)
+        n3b_group<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, 8>(32 * a + m + 1, 1., xi, yi, zi, mi, pj, mj, ax, ay, az,
+                                                                   fx, fy, fz, c, nsh, m >= 8 ? 0. : 1.);
+        for (int d = 1; d < 3; ++d)
+            n3b_group<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(32 * ((a + d) & 3) + m, (d == 2 && a >= 2) ? 0. : 1.,
+                                                                    xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c, nsh);
     }
-#undef N3B_REBASE
 }
 
 __device__ __forceinline__ float row_rol1f(float v) {   // lane 16 a + m <- lane 16 a + ((m + 1) & 15)
@@ -264,36 +268,46 @@ __device__ __forceinline__ float row_rol1f(float v) {   // lane 16 a + m <- lane
 // one ds_add_f64 per component at the group's last index.  Off the diagonal only (a tile's pair with
 // itself is never ultra far); its separations take xi already shifted by n L.
 static_assert(MDQT_SHIFT_I || !MDQT_UFAR32, "the f32 ultra-far form needs MDQT_SHIFT_I");
+__device__ __forceinline__ void n3b_group_uf32(int b0, double xi, double yi, double zi, const double (*pj)[128],
+                                               double* ax, double* ay, double* az, double& fx, double& fy, double& fz,
+                                               float cf, float invlf, float rc2f) {
+    int b_ = b0;
+    asm volatile("" : "+v"(b_));                    // immediate LDS offsets (N3B_REBASE)
+    const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);
+    float ix = 0.f, iy = 0.f, iz = 0.f, jx = 0.f, jy = 0.f, jz = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const float dx = (float)(xi - pjb[0][t]), dy = (float)(yi - pjb[1][t]), dz = (float)(zi - pjb[2][t]);
+        const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+        const float ri = __builtin_amdgcn_rsqf(r2);
+        const float e = __builtin_amdgcn_exp2f(r2 < rc2f ? (r2 * ri) * cf : -INFINITY);
+        const float ft = ((ri + invlf) * e) * (ri * ri);
+        const float px = dx * ft, py = dy * ft, pz = dz * ft;
+        if (t == 0) {
+            ix = px; iy = py; iz = pz;
+            jx = px; jy = py; jz = pz;
+        } else {
+            ix += px; iy += py; iz += pz;
+            jx = row_rol1f(jx) + px; jy = row_rol1f(jy) + py; jz = row_rol1f(jz) + pz;
+        }
+        // each step's i and j sums formed in their step: without it the compiler sank the 45 DPP adds
+        // and the i-side adds after the last step and spilled the pending terms (64-VGPR budget)
+        asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
+    }
+    __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    fx += (double)ix; fy += (double)iy; fz += (double)iz;
+}
+
+// the f32 ultra-far form over the groups of `groups` (off the diagonal)
 __device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, double xi, double yi, double zi,
                                               const double (*pj)[128], double* ax, double* ay, double* az,
                                               double& fx, double& fy, double& fz, float cf, float invlf, float rc2f) {
     const int a = l >> 4, m = l & 15;
     for (int d = 0; d < 4; ++d) {
         if (!((groups >> d) & 1u)) continue;        // wave-uniform
-        int b_ = 32 * ((a + d) & 3) + m;
-        asm volatile("" : "+v"(b_));                // immediate LDS offsets (N3B_REBASE)
-        const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);
-        float ix = 0.f, iy = 0.f, iz = 0.f, jx = 0.f, jy = 0.f, jz = 0.f;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const float dx = (float)(xi - pjb[0][t]), dy = (float)(yi - pjb[1][t]), dz = (float)(zi - pjb[2][t]);
-            const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-            const float ri = __builtin_amdgcn_rsqf(r2);
-            const float e = __builtin_amdgcn_exp2f(r2 < rc2f ? (r2 * ri) * cf : -INFINITY);
-            const float ft = ((ri + invlf) * e) * (ri * ri);
-            const float px = dx * ft, py = dy * ft, pz = dz * ft;
-            if (t == 0) {
-                ix = px; iy = py; iz = pz;
-                jx = px; jy = py; jz = pz;
-            } else {
-                ix += px; iy += py; iz += pz;
-                jx = row_rol1f(jx) + px; jy = row_rol1f(jy) + py; jz = row_rol1f(jz) + pz;
-            }
-        }
-        __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        fx += (double)ix; fy += (double)iy; fz += (double)iz;
+        n3b_group_uf32(32 * ((a + d) & 3) + m, xi, yi, zi, pj, ax, ay, az, fx, fy, fz, cf, invlf, rc2f);
     }
 }
 
@@ -355,6 +369,28 @@ __device__ __forceinline__ double sub_gap2(const double* __restrict__ SB, int T4
         g2 = gap > 0. ? fma(gap, gap, g2) : g2;
     }
     return g2;
+}
+// the sub-blocks (a, (a + d) & 3) of sub-tile group d as bits 4 a + b
+constexpr unsigned kGroupBits[4] = {0x8421u, 0x1842u, 0x2184u, 0x4218u};
+// each group's far level from the sub-blocks beyond r_far / r_vfar / r_ufar / r_ufar32 (bit 4 a + b):
+// the highest level all four of its sub-blocks reach, 4 bits per group
+__host__ __device__ __forceinline__ unsigned sub_group_levels(unsigned mf, unsigned mv, unsigned mu, unsigned m32) {
+    unsigned lv = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const unsigned g = kGroupBits[d];
+        const unsigned x = (m32 & g) == g ? 4u : (mu & g) == g ? 3u : (mv & g) == g ? 2u : (mf & g) == g ? 1u : 0u;
+        lv |= x << (4 * d);
+    }
+    return lv;
+}
+// the groups of `groups` whose far level (4 bits each in lv) is x
+__host__ __device__ __forceinline__ unsigned group_mask_at(unsigned groups, unsigned lv, unsigned x) {
+    unsigned g = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+        if (((groups >> d) & 1u) && ((lv >> (4 * d)) & 15u) == x) g |= 1u << d;
+    return g;
 }
 // the group mask of an off-diagonal tile pair from its 16 sub-block activities (bit 4 a + b: sub-tiles
 // (a, b) closer than the skip radius): bit d = any sub-block (a, (a + d) & 3) active
@@ -475,36 +511,45 @@ void k_pairs_n3b(N3BArgs a) {
             const double cls = srt ? uniform_f64(tp[q][3]) : 0.;
             const bool mine = vI && (db > 0 || J >= I);
             const bool diag = (db == 0 && J == I);
-            unsigned groups = 0xFu;
-            if (a.use_sort == 1 && mine && !diag && (cls >= 0. || (tmeas && cls == -2.))) {   // (2: nothing skipped)
+            // sub-tile groups of this wave's tile pair: which run (bit d of `groups`) and in which pair
+            // form (4 bits per group in `lv`: the far level all four of its sub-blocks allow — their
+            // sub-box gaps, not the tile pair's; each form's bound needs every pair of the group that
+            // far apart, which the sub-boxes guarantee)
+            constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
+            constexpr bool FARF = VARIANT == 1 && !POT && !GUARD && CUT;   // the error-bounded pair forms
+            unsigned groups = 0xFu, lv = 0u;
+            if (srt && mine && !diag && (cls >= 0. || (tmeas && cls == -2.))) {
                 // the tile pair's 16 sub-blocks, lane l < 16: (a, b) = (l >> 2, l & 3)
                 const int sa = l >> 2, sb = l & 3;
-                const double sg = l < 16 ? sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, c.invL) : INFINITY;
-                const unsigned act = (unsigned)__ballot(l < 16 && sg <= rad.rc2);
-                groups = __builtin_amdgcn_readfirstlane(sub_groups_of(act));
+                const bool lg = l < 16;
+                const double sg = lg ? sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, c.invL) : INFINITY;
+                if (a.use_sort == 1)                // (force_sort 2: nothing skipped)
+                    groups = __builtin_amdgcn_readfirstlane(sub_groups_of((unsigned)__ballot(lg && sg <= rad.rc2)));
+                if constexpr (FARF)
+                    lv = __builtin_amdgcn_readfirstlane(sub_group_levels(
+                        (unsigned)__ballot(lg && sg > rad.rf2), (unsigned)__ballot(lg && sg > rad.rv2),
+                        (unsigned)__ballot(lg && sg > rad.ru2), (unsigned)__ballot(lg && sg > rad.ru32)));
                 if (tmeas && (db > 0 || J > I)) {          // once per unordered tile pair
                     const bool evald = cls >= 0. && ((groups >> ((sb - sa) & 3)) & 1u);
                     double gi = 0., gj = 0.;
-                    if (l < 16 && !evald && sg < a.Rcut * a.Rcut) {
+                    if (lg && !evald && sg < a.Rcut * a.Rcut) {
                         const double gd = tail_gd(sg, a.invlDeb);
                         gi = sub_count(N, 4 * J + sb) * gd;     // for I sub-tile sa
                         gj = sub_count(N, 4 * I + sa) * gd;     // for J sub-tile sb
                     }
                     gi += __shfl_xor(gi, 1); gi += __shfl_xor(gi, 2);       // over b: lanes 4 sa .. 4 sa + 3
                     gj += __shfl_xor(gj, 4); gj += __shfl_xor(gj, 8);       // over a: lanes sb, sb + 4, ..
-                    if (l < 16 && sb == 0 && gi > 0.) tbi[q][sa] += gi;
+                    if (lg && sb == 0 && gi > 0.) tbi[q][sa] += gi;
                     if (l < 4 && gj > 0.) atomicAdd(&tbj[l], gj);
                 }
             }
             if (mine && cls >= 0. && groups) {
-                const int ci = (int)cls;            // bit 0 uniform image, bits 1-3 far level
-                const int fl = ci >> 1;
+                const int ci = (int)cls;            // bit 0 uniform image (the tile pair's)
                 // blocked i accumulation: the tile pair's steps into a fresh sum, those into the
                 // block distance's sum, those into the run's (a run is ~1e5 pair terms at N = 1e6;
                 // in spatial order they arrive in coherent groups, and one serial chain would
                 // carry their rounding: momentum |sum F| / mean |F| 1.8e-8 -> 1e-10 at C4)
                 double tx = 0., ty = 0., tz = 0.;
-                constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
                 if (ragN && (I == T - 1 || J == T - 1))
                     n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                     az, tx, ty, tz, c);
@@ -514,38 +559,45 @@ void k_pairs_n3b(N3BArgs a) {
                     const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
                     const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
                     const double sz = MDQT_SHIFT_I ? fma(-nsh[2], a.L, zi) : zi;
-                    if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                        if (fl == 4) {              // ultra far in f32
-#if !defined(MDQT_EXPT_UFAR_SKIP)                   // (diagnostic build: skip them, wrong results)
-                            n3b_pair_uf32(groups, l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
+                    if constexpr (FARF) {
+                        if (diag) {                 // (a tile with itself: the exact form)
+                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(true, groups, l, sx, sy, sz, mi, pj, mj, ax, ay,
+                                                                            az, tx, ty, tz, c, nsh);
+                        } else {                    // each form over the groups at its level
+                            const unsigned g4 = group_mask_at(groups, lv, 4), g3 = group_mask_at(groups, lv, 3),
+                                           g2 = group_mask_at(groups, lv, 2), g1 = group_mask_at(groups, lv, 1),
+                                           g0 = group_mask_at(groups, lv, 0);
+                            if (g3) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(false, g3, l, sx, sy, sz, mi, pj, mj,
+                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
+                            if (g2) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(false, g2, l, sx, sy, sz, mi, pj, mj,
+                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
+                            if (g1) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 1>(false, g1, l, sx, sy, sz, mi, pj, mj,
+                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
+                            if (g0) n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(false, g0, l, sx, sy, sz, mi, pj, mj, ax,
+                                                                                    ay, az, tx, ty, tz, c, nsh);
+#if !defined(MDQT_EXPT_UFAR_SKIP)                   // last: nothing after it keeps sx, nsh live (diagnostic build: skip it, wrong results)
+                            if (g4) n3b_pair_uf32(g4, l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
 #endif
                         }
-                        else if (fl == 3)           // ultra far tile pair
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(diag, groups, l, sx, sy, sz, mi, pj, mj,
-                                                                               ax, ay, az, tx, ty, tz, c, nsh);
-                        else if (fl == 2)           // very far tile pair
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(diag, groups, l, sx, sy, sz, mi, pj, mj,
-                                                                               ax, ay, az, tx, ty, tz, c, nsh);
-                        else if (fl == 1)           // far tile pair: the far pair form
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 1>(diag, groups, l, sx, sy, sz, mi, pj, mj,
-                                                                               ax, ay, az, tx, ty, tz, c, nsh);
-                        else
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(diag, groups, l, sx, sy, sz, mi, pj, mj, ax,
-                                                                            ay, az, tx, ty, tz, c, nsh);
                     } else {
                         n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, groups, l, sx, sy, sz, mi, pj, mj,
                                                                                 ax, ay, az, tx, ty, tz, c, nsh);
                     }
-                } else if constexpr (VARIANT == 1 && !POT && !GUARD && CUT) {
-                    if (fl >= 2)                    // (ultra far with a per-pair image: rare, very-far form)
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax,
-                                                                            ay, az, tx, ty, tz, c);
-                    else if (fl == 1)
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax,
-                                                                            ay, az, tx, ty, tz, c);
-                    else
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                } else if constexpr (FARF) {       // per-pair image
+                    if (diag) {
+                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(true, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                          az, tx, ty, tz, c);
+                    } else {                        // (ultra far with a per-pair image: rare, very-far form)
+                        const unsigned g2 = group_mask_at(groups, lv, 2) | group_mask_at(groups, lv, 3) |
+                                            group_mask_at(groups, lv, 4),
+                                       g1 = group_mask_at(groups, lv, 1), g0 = group_mask_at(groups, lv, 0);
+                        if (g2) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                                    ay, az, tx, ty, tz, c);
+                        if (g1) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(false, g1, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                                    ay, az, tx, ty, tz, c);
+                        if (g0) n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(false, g0, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                                 az, tx, ty, tz, c);
+                    }
                 } else
                     n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay, az,
                                                                      tx, ty, tz, c);
@@ -703,38 +755,44 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
         const double4 t4 = n3b_classify<true>(a, 1. / a.L, rad, I, J, g2);
         const bool diag = db == 0 && J == I;
         const double nI = (double)min(64, a.N - I * 64), nJ = (double)min(64, a.N - J * 64);
-        int k;
+        const bool rag = (a.N & 63) && (I == a.T - 1 || J == a.T - 1);
+        const bool uni = ((int)t4.w & 1) != 0;
+        // the class of a group at far level gl (the kernel's dispatch)
+        auto cls_of = [&](unsigned gl) {
+            if (rag) return 2;
+            if (uni) return gl == 4 ? 10 : gl == 3 ? 9 : gl == 2 ? 8 : gl == 1 ? 6 : 4;
+            return gl >= 2 ? 7 : gl == 1 ? 5 : 3;
+        };
         if (t4.w < 0.) {
-            k = t4.w == -2. ? 1 : 0;
-        } else if ((a.N & 63) && (I == a.T - 1 || J == a.T - 1)) {
-            k = 2;
-        } else {
-            const int ci = (int)t4.w, fl = ci >> 1;
-            if (ci & 1) k = fl == 4 ? 10 : fl == 3 ? 9 : fl == 2 ? 8 : fl == 1 ? 6 : 4;
-            else k = fl >= 2 ? 7 : fl == 1 ? 5 : 3;
-        }
-        if (diag) {
-            atomicAdd(&h[k], 2560ull);
-            atomicAdd(&h[kCensus + k], (unsigned long long)(nI * (nI - 1) / 2));
-        } else if (k < 2) {
+            const int k = t4.w == -2. ? 1 : 0;
             atomicAdd(&h[k], 4096ull);
             atomicAdd(&h[kCensus + k], (unsigned long long)(nI * nJ));
+        } else if (diag) {
+            const int k = cls_of(0);
+            atomicAdd(&h[k], 2560ull);
+            atomicAdd(&h[kCensus + k], (unsigned long long)(nI * (nI - 1) / 2));
         } else {
             const int T4 = 4 * a.T;
-            unsigned act = 0;
+            unsigned act = 0, mf = 0, mv = 0, mu = 0, m32 = 0;
             double np[4] = {0., 0., 0., 0.};       // ion pairs per group
             for (int sa = 0; sa < 4; ++sa)
                 for (int sb = 0; sb < 4; ++sb) {
-                    if (sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, 1. / a.L) <= rad.rc2) act |= 1u << (4 * sa + sb);
+                    const double sg = sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, 1. / a.L);
+                    const unsigned bit = 1u << (4 * sa + sb);
+                    if (sg <= rad.rc2) act |= bit;
+                    if (sg > rad.rf2) mf |= bit;
+                    if (sg > rad.rv2) mv |= bit;
+                    if (sg > rad.ru2) mu |= bit;
+                    if (sg > rad.ru32) m32 |= bit;
                     np[(sb - sa) & 3] += sub_count(a.N, 4 * I + sa) * sub_count(a.N, 4 * J + sb);
                 }
             const unsigned g = a.use_sort == 1 ? sub_groups_of(act) : 0xFu;   // (2: nothing skipped)
-            double on = 0., off = 0.;
-            for (int d = 0; d < 4; ++d) ((g >> d) & 1u ? on : off) += np[d];
-            atomicAdd(&h[k], 1024ull * (unsigned)__builtin_popcount(g));
-            atomicAdd(&h[kCensus + k], (unsigned long long)on);
-            atomicAdd(&h[11], 1024ull * (unsigned)(4 - __builtin_popcount(g)));
-            atomicAdd(&h[kCensus + 11], (unsigned long long)off);
+            const unsigned lv = sub_group_levels(mf, mv, mu, m32);
+            for (int d = 0; d < 4; ++d) {
+                const int k = (g >> d) & 1u ? cls_of((lv >> (4 * d)) & 15u) : 11;
+                atomicAdd(&h[k], 1024ull);
+                atomicAdd(&h[kCensus + k], (unsigned long long)np[d]);
+            }
         }
     }
     __syncthreads();

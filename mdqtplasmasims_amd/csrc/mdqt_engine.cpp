@@ -150,6 +150,8 @@ struct mdqt_ctx {
     double* dRs = nullptr;         // [3][Npad] positions in sorted order
     double* dBoxes = nullptr;      // [12][T] tile boxes, raw coordinate bounds
     double* dSubBoxes = nullptr;   // [6][4T] the 16-ion sub-tiles' boxes (the block kernel's sub-tile groups)
+    uint2* dPlan = nullptr;        // [(Phi - Plo) nd][256] the block kernel's tile-pair words (k_n3b_plan)
+    size_t capPlan = 0;
     int capSortN = 0;
     // overlapped MD step (option "overlap", OFF by default — measured slower): the
     // QT launch of step k runs on its own stream beside step k's force launch and waits on the
@@ -739,6 +741,8 @@ static void free_device(mdqt_ctx* s) {
     if (s->dTailSt) (void)hipFree(s->dTailSt);
     s->dTail = nullptr; s->dTailList = nullptr; s->dTailSt = nullptr;
     s->capSortN = 0;
+    if (s->dPlan) (void)hipFree(s->dPlan);
+    s->dPlan = nullptr; s->capPlan = 0;
     if (s->dPeerParts) (void)hipFree((void*)s->dPeerParts);
     s->dSlots = nullptr; s->dFr = nullptr; s->dPeerParts = nullptr;
     s->capSlots = 0;
@@ -1366,7 +1370,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.Rall = s->dR; a.slots = s->dSlots; a.S = s->S;
     a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
     a.micGuard = c.micGuard; a.guard = c.guard;
-    a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr; a.subboxes = nullptr;
+    a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr; a.subboxes = nullptr; a.plan = nullptr;
     double bound;
     a.Rskip = skip_radius(s, &bound);
     a.tailb = nullptr;
@@ -1387,6 +1391,14 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
         HIPCHK(launch_spatial_order(o, s->stream));
         a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes; a.subboxes = s->dSubBoxes;
         if (tail_measured(s) && a.Rskip < a.Rcut) a.tailb = s->dTail;
+        const size_t need = (size_t)std::max(a.Phi - a.Plo, 0) * a.nd * 256;   // the plan (k_n3b_plan)
+        if (need > s->capPlan) {
+            if (s->dPlan) HIPCHK(hipFree(s->dPlan));
+            s->dPlan = nullptr;
+            HIPCHK(hipMalloc((void**)&s->dPlan, need * sizeof(uint2)));
+            s->capPlan = need;
+        }
+        a.plan = s->dPlan;
     }
     return 0;
 }

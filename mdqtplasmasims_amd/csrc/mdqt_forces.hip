@@ -384,14 +384,8 @@ __host__ __device__ __forceinline__ unsigned sub_group_levels(unsigned mf, unsig
     }
     return lv;
 }
-// the groups of `groups` whose far level (4 bits each in lv) is x
-__host__ __device__ __forceinline__ unsigned group_mask_at(unsigned groups, unsigned lv, unsigned x) {
-    unsigned g = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-        if (((groups >> d) & 1u) && ((lv >> (4 * d)) & 15u) == x) g |= 1u << d;
-    return g;
-}
+// the groups of a staging word (n3b_stage_groups) that run in the pair form of far level x
+__device__ __forceinline__ unsigned level_groups(unsigned word, int x) { return (word >> (4 + 4 * x)) & 15u; }
 // the group mask of an off-diagonal tile pair from its 16 sub-block activities (bit 4 a + b: sub-tiles
 // (a, b) closer than the skip radius): bit d = any sub-block (a, (a + d) & 3) active
 __host__ __device__ __forceinline__ unsigned sub_groups_of(unsigned act16) {
@@ -402,13 +396,31 @@ __host__ __device__ __forceinline__ unsigned sub_groups_of(unsigned act16) {
         for (int a = 0; a < 4; ++a) g |= ((act16 >> (4 * a + ((a + d) & 3))) & 1u) << d;
     return g;
 }
-// one pair's |F| bound at distance d >= the box gap (SpeedUp:224 times r): the tail sums' g
-__device__ __forceinline__ double tail_gd(double g2, double invlDeb) {
-    const double d = sqrt(g2);
-    return (1. / d + invlDeb) * exp(-d * invlDeb) / d;
+// one pair's |F| bound at distance >= the gap d (g2 = d^2 > 0): g(d) = (1/d + 1/lDeb) e^(-d/lDeb) / d
+// (SpeedUp:224 times r), the tail sums' term, as an upper bound in a few f32 operations: v_rsq_f32
+// and v_exp_f32 (each within 2^-22 relative, tests/test_gpu_large.py), d^2 and the exponent's
+// constant rounded to f32 (e^(-d/lDeb) within (d/lDeb) 2^-23 relative), the result x (1 + 2^-12):
+// an upper bound while d/lDeb < 1000; beyond f32's range e^(-d/lDeb) flushes to 0 (< 1e-44)
+__device__ __forceinline__ double tail_g(double g2, float invl, float cf) {
+    const float s = (float)g2;
+    const float ri = __builtin_amdgcn_rsqf(s);
+    const float e = __builtin_amdgcn_exp2f((s * ri) * cf);
+    return (double)(((ri + invl) * e) * ri) * (1. + 0x1p-12);
+}
+// a tile pair's class and uniform-image multiples in one LDS word: bits 0-3 class + 2, 4-11 / 12-19 /
+// 20-27 n_x, n_y, n_z (signed); a uniform image with a multiple beyond +-127 (positions that far
+// outside the box) is taken per pair instead
+__device__ __forceinline__ int n3b_pack_class(double4 t4) {
+    int cls = (int)t4.w;
+    const bool uni = cls >= 0 && (cls & 1);
+    if (uni && !(fabs(t4.x) <= 127. && fabs(t4.y) <= 127. && fabs(t4.z) <= 127.)) cls -= 1;
+    const bool u2 = cls >= 0 && (cls & 1);
+    const int nx = u2 ? (int)t4.x : 0, ny = u2 ? (int)t4.y : 0, nz = u2 ? (int)t4.z : 0;
+    return (cls + 2) | ((nx & 255) << 4) | ((ny & 255) << 12) | ((nz & 255) << 20);
 }
 // real ions of 16-ion sub-tile s (0 for the padding of the ragged last tile)
 __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0, min(16, N - 16 * s)); }
+
 
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
 template <int VARIANT, bool GUARD, bool POT = false>
@@ -442,7 +454,7 @@ void k_pairs_n3b(N3BArgs a) {
         xi = p[0]; yi = p[PS]; zi = p[2 * PS]; mi = 1.;
     }
     // Tile-pair classes in spatial order (SpeedUp:222 keeps a pair only below r = L/2), decided
-    // for all BW waves' tile pairs (I, J) by the staging wave's lanes 0..BW-1 into tp[q]:
+    // for all BW waves' tile pairs (I, J) by the staging wave's lanes 0..BW-1:
     //  * skip (force_sort 1): boxes beyond the skip radius in the minimum image — at L/2 no pair
     //    inside the cutoff (exact zeros), inside L/2 the error-bounded tail (tail sums below);
     //  * uniform image: every pair's raw separation fl(xi - xj) lies in [fl(lo_I - hi_J),
@@ -451,9 +463,14 @@ void k_pairs_n3b(N3BArgs a) {
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
     // class: -1 / -2 skip; otherwise bit 0 = uniform image, + 2 x the far level (1 far pair form, 2
-    // very far, 3 ultra far, 4 ultra far in f32; forces only): 0 .. 9.  Then every wave takes the
-    // sub-tile groups of its own tile pair (16 sub-block gaps, one per lane).
-    __shared__ double tp[BW][4];                    // n_x, n_y, n_z, class
+    // very far, 3 ultra far, 4 ultra far in f32; forces only): 0 .. 9 (n3b_pack_class: tpw[q]).
+    // The forces take them, with the sub-tile groups (tg[q]), from the call's plan (k_n3b_plan: one
+    // 8-byte word per tile pair, loaded by lanes 0..15); without a plan (potentials, unsorted order)
+    // the staging lanes classify the tile pairs themselves and every group runs in the exact form.
+    __shared__ int tpw[BW];                         // class and uniform-image multiples
+    __shared__ unsigned tg[BW];                     // sub-tile groups by pair form (k_n3b_plan)
+    constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
+    constexpr bool FARF = VARIANT == 1 && !POT && !GUARD && CUT;   // the error-bounded pair forms
     const N3BRadii rad = n3b_radii<VARIANT, POT>(a);
     // the f32 form's constants as wave-uniform SGPR values (in VGPRs they were spilled and reloaded
     // inside the pair loop at the kernel's 64-VGPR budget)
@@ -464,17 +481,7 @@ void k_pairs_n3b(N3BArgs a) {
     // the three-level blocking fits the 64-VGPR budget of two 16-wave workgroups per CU
     double* fi = irun[q][0];
     fi[l] = 0.; fi[64 + l] = 0.; fi[128 + l] = 0.;
-    // force_tail_mode 1 (a.tailb, per 16-ion sub-tile): every pair the call drops inside L/2 — in a
-    // tile pair skipped by the tail radius, or in a skipped sub-tile group — is at least its sub-block
-    // gap apart, so each ion of I sub-tile a loses at most sum_b n_b g(gap_ab) and each ion of J
-    // sub-tile b sum_a n_a g(gap_ab); counted once per unordered tile pair.  The I side is kept per
-    // wave over the run (tbi[q]), the J side summed over the waves in LDS per J tile (tbj) and added
-    // to the global sums by thread 0 after the tile's work.
-    __shared__ double tbi[BW][4], tbj[4];
-    const bool tmeas = !POT && a.tailb != nullptr;
-    if (tmeas && l < 4) tbi[q][l] = 0.;
-    if (tmeas && threadIdx.x < 4) tbj[threadIdx.x] = 0.;
-    const int T4 = 4 * T;
+    const uint2* plan = POT ? nullptr : a.plan;
     double* ax = accj[q][0];
     double* ay = accj[q][1];
     double* az = accj[q][2];
@@ -496,55 +503,34 @@ void k_pairs_n3b(N3BArgs a) {
                 pj[1][li] = yj; pj[1][li + 16] = yj;
                 pj[2][li] = zj; pj[2][li + 16] = zj;
                 mj[li] = vj ? 1. : 0.; mj[li + 16] = mj[li];
-                if (srt && l < BW && P * BW + l < T) {
-                    double g2;
-                    const double4 t4 = n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2);
-                    tp[l][0] = t4.x; tp[l][1] = t4.y; tp[l][2] = t4.z; tp[l][3] = t4.w;
-#if defined(MDQT_EXPT_CLS)
-                    atomicAdd(&g_cls_count[t4.w < 0. ? 0 : 1 + ((int)t4.w & 1)], 1ull);
-#endif
+                if (l < BW) {
+                    if (plan) {                     // (P, db, b): 16 words, one per wave
+                        const uint2 w = plan[((size_t)(P - a.Plo) * a.nd + db) * (BW * BW) + b * BW + l];
+                        tpw[l] = (int)w.x;
+                        tg[l] = w.y;
+                    } else {
+                        int w = 2;                  // class 0 (unsorted: every tile pair, per-pair image)
+                        if (srt && P * BW + l < T) {
+                            double g2;
+                            w = n3b_pack_class(n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2));
+                        }
+                        tpw[l] = w;
+                        tg[l] = 0xFFu;
+                    }
                 }
             }
 #pragma unroll
             for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
             __syncthreads();
-            const double cls = srt ? uniform_f64(tp[q][3]) : 0.;
+            const int tw = __builtin_amdgcn_readfirstlane(tpw[q]);
+            const int cls = (tw & 15) - 2;
             const bool mine = vI && (db > 0 || J >= I);
             const bool diag = (db == 0 && J == I);
-            // sub-tile groups of this wave's tile pair: which run (bit d of `groups`) and in which pair
-            // form (4 bits per group in `lv`: the far level all four of its sub-blocks allow — their
-            // sub-box gaps, not the tile pair's; each form's bound needs every pair of the group that
-            // far apart, which the sub-boxes guarantee)
-            constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
-            constexpr bool FARF = VARIANT == 1 && !POT && !GUARD && CUT;   // the error-bounded pair forms
-            unsigned groups = 0xFu, lv = 0u;
-            if (srt && mine && !diag && (cls >= 0. || (tmeas && cls == -2.))) {
-                // the tile pair's 16 sub-blocks, lane l < 16: (a, b) = (l >> 2, l & 3)
-                const int sa = l >> 2, sb = l & 3;
-                const bool lg = l < 16;
-                const double sg = lg ? sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, c.invL) : INFINITY;
-                if (a.use_sort == 1)                // (force_sort 2: nothing skipped)
-                    groups = __builtin_amdgcn_readfirstlane(sub_groups_of((unsigned)__ballot(lg && sg <= rad.rc2)));
-                if constexpr (FARF)
-                    lv = __builtin_amdgcn_readfirstlane(sub_group_levels(
-                        (unsigned)__ballot(lg && sg > rad.rf2), (unsigned)__ballot(lg && sg > rad.rv2),
-                        (unsigned)__ballot(lg && sg > rad.ru2), (unsigned)__ballot(lg && sg > rad.ru32)));
-                if (tmeas && (db > 0 || J > I)) {          // once per unordered tile pair
-                    const bool evald = cls >= 0. && ((groups >> ((sb - sa) & 3)) & 1u);
-                    double gi = 0., gj = 0.;
-                    if (lg && !evald && sg < a.Rcut * a.Rcut) {
-                        const double gd = tail_gd(sg, a.invlDeb);
-                        gi = sub_count(N, 4 * J + sb) * gd;     // for I sub-tile sa
-                        gj = sub_count(N, 4 * I + sa) * gd;     // for J sub-tile sb
-                    }
-                    gi += __shfl_xor(gi, 1); gi += __shfl_xor(gi, 2);       // over b: lanes 4 sa .. 4 sa + 3
-                    gj += __shfl_xor(gj, 4); gj += __shfl_xor(gj, 8);       // over a: lanes sb, sb + 4, ..
-                    if (lg && sb == 0 && gi > 0.) tbi[q][sa] += gi;
-                    if (l < 4 && gj > 0.) atomicAdd(&tbj[l], gj);
-                }
-            }
-            if (mine && cls >= 0. && groups) {
-                const int ci = (int)cls;            // bit 0 uniform image (the tile pair's)
+            // this wave's sub-tile groups, by pair form (k_n3b_plan)
+            const unsigned word = __builtin_amdgcn_readfirstlane(tg[q]);
+            const unsigned groups = word & 15u;
+            if (mine && cls >= 0 && groups) {
+                const int ci = cls;                 // bit 0 uniform image (the tile pair's)
                 // blocked i accumulation: the tile pair's steps into a fresh sum, those into the
                 // block distance's sum, those into the run's (a run is ~1e5 pair terms at N = 1e6;
                 // in spatial order they arrive in coherent groups, and one serial chain would
@@ -554,7 +540,7 @@ void k_pairs_n3b(N3BArgs a) {
                     n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                     az, tx, ty, tz, c);
                 else if (VARIANT == 1 && (ci & 1)) {       // uniform image
-                    const double nsh[3] = {uniform_f64(tp[q][0]), uniform_f64(tp[q][1]), uniform_f64(tp[q][2])};
+                    const double nsh[3] = {(double)((tw << 20) >> 24), (double)((tw << 12) >> 24), (double)((tw << 4) >> 24)};
                     // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
                     const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
                     const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
@@ -564,9 +550,9 @@ void k_pairs_n3b(N3BArgs a) {
                             n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(true, groups, l, sx, sy, sz, mi, pj, mj, ax, ay,
                                                                             az, tx, ty, tz, c, nsh);
                         } else {                    // each form over the groups at its level
-                            const unsigned g4 = group_mask_at(groups, lv, 4), g3 = group_mask_at(groups, lv, 3),
-                                           g2 = group_mask_at(groups, lv, 2), g1 = group_mask_at(groups, lv, 1),
-                                           g0 = group_mask_at(groups, lv, 0);
+                            const unsigned g4 = level_groups(word, 4), g3 = level_groups(word, 3),
+                                           g2 = level_groups(word, 2), g1 = level_groups(word, 1),
+                                           g0 = level_groups(word, 0);
                             if (g3) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(false, g3, l, sx, sy, sz, mi, pj, mj,
                                                                                        ax, ay, az, tx, ty, tz, c, nsh);
                             if (g2) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(false, g2, l, sx, sy, sz, mi, pj, mj,
@@ -588,9 +574,8 @@ void k_pairs_n3b(N3BArgs a) {
                         n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(true, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                          az, tx, ty, tz, c);
                     } else {                        // (ultra far with a per-pair image: rare, very-far form)
-                        const unsigned g2 = group_mask_at(groups, lv, 2) | group_mask_at(groups, lv, 3) |
-                                            group_mask_at(groups, lv, 4),
-                                       g1 = group_mask_at(groups, lv, 1), g0 = group_mask_at(groups, lv, 0);
+                        const unsigned g2 = level_groups(word, 2) | level_groups(word, 3) | level_groups(word, 4),
+                                       g1 = level_groups(word, 1), g0 = level_groups(word, 0);
                         if (g2) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax,
                                                                                     ay, az, tx, ty, tz, c);
                         if (g1) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(false, g1, l, xi, yi, zi, mi, pj, mj, ax,
@@ -611,10 +596,6 @@ void k_pairs_n3b(N3BArgs a) {
                 for (int w = 0; w < BW; ++w) v = v + (accj[w][q][li] + accj[w][q][li + 16]);
                 a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? v : -v;
             }
-            if (tmeas && threadIdx.x < 4) {         // J's sub-tile sums of this J step -> global
-                if (tbj[threadIdx.x] > 0.) atomicAdd(a.tailb + 4 * J + threadIdx.x, tbj[threadIdx.x]);
-                tbj[threadIdx.x] = 0.;
-            }
             __syncthreads();
         }
         fi[l] += bx; fi[64 + l] += by; fi[128 + l] += bz;   // one wave's own LDS words: in order
@@ -623,7 +604,6 @@ void k_pairs_n3b(N3BArgs a) {
         double* o = a.slots + (size_t)(a.nd + run) * plane + i;
         o[0] = fi[l]; o[a.Npad] = fi[64 + l]; o[2 * (size_t)a.Npad] = fi[128 + l];
     }
-    if (tmeas && vI && l < 4 && tbi[q][l] > 0.) atomicAdd(a.tailb + 4 * I + l, tbi[q][l]);
 }
 
 // force_tail_mode 1, after the call's per-sub-tile tail sums are complete (all-reduced over the
@@ -686,7 +666,14 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
         const int i = I * 64 + l;
         const bool vi = i < N;
         const double xi = vi ? a.Rs[i] : 0., yi = vi ? a.Rs[PS + i] : 0., zi = vi ? a.Rs[2 * PS + i] : 0.;
-        double fx = 0., fy = 0., fz = 0.;
+        // per J tile a 64-term partial, added with its rounding error kept (Neumaier): the exact
+        // pass's sum is accurate to a few ulp of |F| rather than carrying ~1e5 rounded additions
+        double fx = 0., fy = 0., fz = 0., ex = 0., ey = 0., ez = 0.;
+        auto nadd = [](double& s, double& e, double v) {
+            const double t = s + v;
+            e += fabs(s) >= fabs(v) ? (s - t) + v : (v - t) + s;
+            s = t;
+        };
         for (int j0 = q * 64; own && j0 < T; j0 += 256) {
             const int Jl = j0 + l;
             bool in = false;
@@ -702,6 +689,7 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
                 const int j = J * 64 + l;
                 const int nj = min(64, N - J * 64);
                 const double xl = j < N ? a.Rs[j] : 0., yl = j < N ? a.Rs[PS + j] : 0., zl = j < N ? a.Rs[2 * PS + j] : 0.;
+                double px = 0., py = 0., pz = 0.;
                 for (int t = 0; t < nj; ++t) {
                     auto lane_t = [t](double v) {
                         return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), t),
@@ -710,11 +698,12 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
                     double dx = xi - lane_t(xl), dy = yi - lane_t(yl), dz = zi - lane_t(zl);
                     mic_r(dx, dy, dz, c);
                     const double ft = pair_ft<1>(dx, dy, dz, c);   // 0 beyond L/2 and for i = j
-                    fx = fma(dx, ft, fx); fy = fma(dy, ft, fy); fz = fma(dz, ft, fz);
+                    px = fma(dx, ft, px); py = fma(dy, ft, py); pz = fma(dz, ft, pz);
                 }
+                nadd(fx, ex, px); nadd(fy, ey, py); nadd(fz, ez, pz);
             }
         }
-        part[q][0][l] = fx; part[q][1][l] = fy; part[q][2][l] = fz;
+        part[q][0][l] = fx + ex; part[q][1][l] = fy + ey; part[q][2][l] = fz + ez;
         __syncthreads();
         if (q == 0 && vi) {
             const int ion = a.perm[i];
@@ -797,6 +786,90 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
     }
     __syncthreads();
     if (t < 2 * kCensus && h[t]) atomicAdd(out + t, h[t]);
+}
+
+// The block kernel's plan (force calls in spatial order): every tile pair of this rank's block pairs
+// classified once per call, before k_pairs_n3b, so that its staging lanes read one 8-byte word per
+// tile pair instead of classifying — work the block kernel's other 15 waves waited out at every J
+// step's barrier (the sub-tile classification there cost C5 +8 %).  plan[((P - Plo) nd
+// + db) 256 + 16 b + q] is tile pair (16 P + q, 16 Q + b), Q = P + db mod NB: .x its class and
+// uniform-image multiples (n3b_pack_class), .y its sub-tile groups by pair form:
+//  * group d = the sub-blocks (a, (a + d) & 3) of the tile pair's 4 x 4 (16-ion sub-tiles; the block
+//    kernel's lane 16 a + m runs them as its d-th 16-step group); its gap is the least of their four
+//    sub-box gaps.  It runs iff that gap is within the skip radius (force_sort 1; 2 runs all), in the
+//    pair form the gap allows (the far level every pair of the group reaches: each form's error
+//    bound needs every pair that far apart, which the sub-boxes guarantee).  .y = groups | (the
+//    groups of far level x) << (4 + 4 x), x = 0..4; 0xFF (all groups, exact form) where unused.
+//  * tail sums (force_tail_mode 1, a.tailb): every pair the call drops inside L/2 — in a tile pair
+//    the tail radius skips (class -2) or in a skipped group — is at least its sub-block gap apart, so
+//    each ion of I sub-tile a loses at most sum_b n_b g(gap_ab) and each ion of J sub-tile b at most
+//    sum_a n_a g(gap_ab); counted once per unordered tile pair, summed per sub-tile in LDS over the
+//    workgroup and added to tailb (128 atomics per workgroup).
+// One workgroup per (P, db), thread (b, q) — the census's decomposition.
+template <int VARIANT, bool GUARD>
+__global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
+    __shared__ double ti[BW][4], tj[BW][4];
+    constexpr bool FARF = VARIANT == 1 && !GUARD && MDQT_N3_CUT;
+    const int t = threadIdx.x, q = t & (BW - 1), b = t / BW;
+    const int Pl = (int)blockIdx.x / a.nd, db = (int)blockIdx.x % a.nd;
+    const int P = a.Plo + Pl, Q = (P + db) % a.NB;
+    const int I = P * BW + q, J = Q * BW + b;
+    const bool tmeas = a.tailb != nullptr;
+    if (tmeas && t < 64) { ti[t >> 2][t & 3] = 0.; tj[t >> 2][t & 3] = 0.; }
+    if (tmeas) __syncthreads();
+    uint2 w = make_uint2(1u, 0xFFu);                // class -1 where the block kernel never looks
+    const bool half = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
+    if (!half && I < a.T && J < a.T && (db > 0 || J >= I)) {
+        const N3BRadii rad = n3b_radii<VARIANT, false>(a);
+        const double invL = 1. / a.L;
+        double g2;
+        const int pw = n3b_pack_class(n3b_classify<VARIANT == 1>(a, invL, rad, I, J, g2));
+        const int cls = (pw & 15) - 2;
+        w.x = (unsigned)pw;
+        if ((db > 0 || J > I) && (cls >= 0 || (tmeas && cls == -2))) {
+            const int T4 = 4 * a.T;
+            double sg[4][4];
+#pragma unroll
+            for (int sa = 0; sa < 4; ++sa)
+#pragma unroll
+                for (int sb = 0; sb < 4; ++sb) sg[sa][sb] = sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, invL);
+            unsigned groups = 0u, lvm = 0u;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const double gm = fmin(fmin(sg[0][d & 3], sg[1][(1 + d) & 3]), fmin(sg[2][(2 + d) & 3], sg[3][(3 + d) & 3]));
+                if (a.use_sort != 1 || gm <= rad.rc2) {
+                    const int x = !FARF ? 0 : gm > rad.ru32 ? 4 : gm > rad.ru2 ? 3 : gm > rad.rv2 ? 2 : gm > rad.rf2 ? 1 : 0;
+                    groups |= 1u << d;
+                    lvm |= 1u << (4 * x + d);
+                }
+            }
+            if (cls >= 0) w.y = groups | (lvm << 4);
+            if (tmeas) {
+                const double rcut2 = a.Rcut * a.Rcut;
+                const float invl = (float)a.invlDeb, cf = (float)(a.invlDeb * kNegLog2e);
+#pragma unroll
+                for (int sa = 0; sa < 4; ++sa)
+#pragma unroll
+                    for (int sb = 0; sb < 4; ++sb) {
+                        const bool drop = cls == -2 || !((groups >> ((sb - sa) & 3)) & 1u);
+                        if (drop && sg[sa][sb] < rcut2) {
+                            const double gd = tail_g(sg[sa][sb], invl, cf);
+                            atomicAdd(&ti[q][sa], sub_count(a.N, 4 * J + sb) * gd);
+                            atomicAdd(&tj[b][sb], sub_count(a.N, 4 * I + sa) * gd);
+                        }
+                    }
+            }
+        }
+    }
+    plan[((size_t)Pl * a.nd + db) * (BW * BW) + t] = w;
+    if (tmeas) {
+        __syncthreads();
+        if (t < 64) {
+            const int k = t >> 2, u = t & 3;
+            if (ti[k][u] > 0.) atomicAdd(a.tailb + 4 * (P * BW + k) + u, ti[k][u]);
+            if (tj[k][u] > 0.) atomicAdd(a.tailb + 4 * (Q * BW + k) + u, tj[k][u]);
+        }
+    }
 }
 
 // canonical per-ion sum of the slots this rank wrote: j-slots db = 0 .. nd-1, then i-slots.
@@ -904,6 +977,19 @@ hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s) {
 
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s) {
     const int nblk = (a.Phi - a.Plo) * a.R;
+    const int nplan = (a.Phi - a.Plo) * a.nd;
+    if (a.plan && nplan > 0) {
+        if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // spatial order only
+        if (variant == 1) {
+            if (a.guard) hipLaunchKernelGGL((k_n3b_plan<1, true>), dim3(nplan), dim3(256), 0, s, a, a.plan);
+            else hipLaunchKernelGGL((k_n3b_plan<1, false>), dim3(nplan), dim3(256), 0, s, a, a.plan);
+        } else {
+            if (a.guard) hipLaunchKernelGGL((k_n3b_plan<0, true>), dim3(nplan), dim3(256), 0, s, a, a.plan);
+            else hipLaunchKernelGGL((k_n3b_plan<0, false>), dim3(nplan), dim3(256), 0, s, a, a.plan);
+        }
+    } else if (a.tailb) {
+        return hipErrorInvalidValue;                // the tail sums come from the plan
+    }
     if (nblk > 0) {
         if (variant == 1) {
             if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<1, true>), dim3(nblk), dim3(BW * 64), 0, s, a);

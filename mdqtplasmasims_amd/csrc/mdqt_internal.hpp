@@ -424,8 +424,11 @@ struct N3BArgs {
     double* tailb;      // force_tail_mode 1: per 16-ion sub-tile [4T], the sum over the pairs the call
                         // drops inside L/2 (tail-skipped tile pairs, skipped sub-tile groups) of
                         // n_b g(sub-block gap) — the measured bound on what each of its ions loses
-                        // (zeroed before the launch; nullptr: not measured)
+                        // (zeroed before the launch, summed by k_n3b_plan; nullptr: not measured)
     const double* subboxes;   // [6][4T]: the 16-ion sub-tiles' centers and half extents (use_sort)
+    uint2* plan;        // force calls in spatial order: [(Phi - Plo) nd][256] tile-pair words, written by
+                        // k_n3b_plan (launch_forces_n3b) and read by k_pairs_n3b; nullptr: classified
+                        // in the block kernel (every sub-tile group exact; no tail sums)
 };
 struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]

@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B of the block-kernel variants at C3, C5, N = 1M (tools/force_ab.py): the product library, the
+# round-3 tree (expt/r03tree, its own package) and diagnostic builds (expt/<name>), alternating.
+#   bash tools/gpu/r04_force_ab.sh [rounds]
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+R="$GRAFT_REPO_ROOT"
+for i in $(seq 1 ${1:-2}); do
+  timeout -k 10 200 python3 tools/force_ab.py product || exit 1
+  timeout -k 10 200 env MDQT_ROOT="$R/expt/r03tree" python3 tools/force_ab.py r03 || exit 1
+  for v in ${VARIANTS:-}; do
+    [ -f expt/$v/lib/libmdqt.so ] && { timeout -k 10 200 env MDQT_LIB=expt/$v/lib/libmdqt.so python3 tools/force_ab.py $v || exit 1; }
+  done
+done
+exit 0

@@ -646,7 +646,11 @@ static void choose_segments(mdqt_ctx* s) {
         b.Phi = (int)((long)(s->p.rank + 1) * b.NB / W);
         const int nblk = std::max(b.Phi - b.Plo, 1);
         // ~4096 workgroups per rank (8 rounds of 2 per CU): short tail
-        int R = std::min(b.nd, (4096 + nblk - 1) / nblk);
+        static const int wg_target = [] {           // (A/B experiments: MDQT_N3B_WG workgroups per rank)
+            const char* e = getenv("MDQT_N3B_WG");
+            return e && atoi(e) > 0 ? atoi(e) : 16384;
+        }();
+        int R = std::min(b.nd, (wg_target + nblk - 1) / nblk);
         b.runlen = (b.nd + R - 1) / R;
         b.R = (b.nd + b.runlen - 1) / b.runlen;
     }

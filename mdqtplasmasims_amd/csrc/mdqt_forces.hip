@@ -434,8 +434,15 @@ void k_pairs_n3b(N3BArgs a) {
     __shared__ double etab[64];
     stage_exp_tab(etab);
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;   // q: wave-uniform
-    const int P = a.Plo + (int)blockIdx.x / a.R;
-    const int run = (int)blockIdx.x % a.R;
+#ifndef MDQT_N3B_ORDER
+#define MDQT_N3B_ORDER 1
+#endif
+    // workgroup order: run-major (MDQT_N3B_ORDER 1) dispatches every block's first run — the near
+    // block distances, the heaviest work — first and the far, mostly skipped runs last, so the
+    // kernel's last round is short; 0: block-major (round 3)
+    const int nP = a.Phi - a.Plo;
+    const int P = a.Plo + (MDQT_N3B_ORDER ? (int)blockIdx.x % nP : (int)blockIdx.x / a.R);
+    const int run = MDQT_N3B_ORDER ? (int)blockIdx.x / nP : (int)blockIdx.x % a.R;
     const int d0 = run * a.runlen, d1 = min(a.nd, d0 + a.runlen);
     const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2, etab};
     const int T = a.T, N = a.N, S = a.S;
@@ -482,6 +489,14 @@ void k_pairs_n3b(N3BArgs a) {
     double* fi = irun[q][0];
     fi[l] = 0.; fi[64 + l] = 0.; fi[128 + l] = 0.;
     const uint2* plan = POT ? nullptr : a.plan;
+    // every J step: the staging wave (the last; not one of the combining waves 0..2) loads J, one
+    // barrier, the pair work, one barrier, then waves 0..2 combine the 16 j accumulators of one
+    // component each into the j-slot and zero them for the next step — while the staging wave
+    // already loads the next J (no third barrier: nothing reads pj or the plan words after the
+    // second, and the accumulators are zero again before the combining waves reach the next one)
+    constexpr int kStage = BW - 1;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
     double* ax = accj[q][0];
     double* ay = accj[q][1];
     double* az = accj[q][2];
@@ -493,7 +508,7 @@ void k_pairs_n3b(N3BArgs a) {
         for (int b = 0; b < BW; ++b) {
             const int J = Q * BW + b;
             if (J >= T) break;
-            if (q == 0) {                           // stage J (by sub-tiles, twice over)
+            if (q == kStage) {                      // stage J (by sub-tiles, twice over)
                 const int j = J * 64 + l;
                 const bool vj = j < N;
                 const double* p = tile_ptr(J) + l;
@@ -519,8 +534,6 @@ void k_pairs_n3b(N3BArgs a) {
                     }
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
             __syncthreads();
             const int tw = __builtin_amdgcn_readfirstlane(tpw[q]);
             const int cls = (tw & 15) - 2;
@@ -591,12 +604,21 @@ void k_pairs_n3b(N3BArgs a) {
             __syncthreads();
             if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db
                 const int li = n3b_lds(l);
-                double v = 0.;
+                // the 16 waves' two copies, summed as a fixed pairwise tree (dependency depth 5,
+                // not 16), then zeroed for the next J step
+                double s16[BW];
 #pragma unroll
-                for (int w = 0; w < BW; ++w) v = v + (accj[w][q][li] + accj[w][q][li + 16]);
-                a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? v : -v;
+                for (int w = 0; w < BW; ++w) {
+                    s16[w] = accj[w][q][li] + accj[w][q][li + 16];
+                    accj[w][q][li] = 0.;
+                    accj[w][q][li + 16] = 0.;
+                }
+#pragma unroll
+                for (int h = BW / 2; h >= 1; h /= 2)
+#pragma unroll
+                    for (int w = 0; w < h; ++w) s16[w] = s16[2 * w] + s16[2 * w + 1];
+                a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? s16[0] : -s16[0];
             }
-            __syncthreads();
         }
         fi[l] += bx; fi[64 + l] += by; fi[128 + l] += bz;   // one wave's own LDS words: in order
     }

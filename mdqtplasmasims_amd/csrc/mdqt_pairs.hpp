@@ -20,7 +20,7 @@ struct PairC {
 // truncation 3.5e-17); <= 2 ulp.  Five FMAs instead of eleven for three integer operations and one
 // LDS read; the cutoff folded into the exponent as in exp2_neg_cut.
 #ifndef MDQT_EXP_TAB
-#define MDQT_EXP_TAB 0   // A/B (round 3): C2 MD step -0.2 us, C5 -2 %, N = 1M +7 % (block-kernel spills): off
+#define MDQT_EXP_TAB 1   // A/B round 4 (plan-based block kernel): C3 -3.5 %, C5 -0.8 %, N = 1M +0.3 %; round 3: C2 MD step -0.2 us
 #endif
 static __constant__ const double kExp2Tab64[64] = {
     0x1.0000000000000p+0, 0x1.02c9a3e778061p+0, 0x1.059b0d3158574p+0, 0x1.0874518759bc8p+0,

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 R="$GRAFT_REPO_ROOT"
 for i in $(seq 1 ${1:-2}); do
   timeout -k 10 200 python3 tools/force_ab.py product || exit 1
-  timeout -k 10 200 env MDQT_ROOT="$R/expt/r03tree" python3 tools/force_ab.py r03 || exit 1
+  timeout -k 10 200 env MDQT_ROOT="$R/expt/${BASE:-basetree}" python3 tools/force_ab.py ${BASE:-basetree} || exit 1
   for v in ${VARIANTS:-}; do
     [ -f expt/$v/lib/libmdqt.so ] && { timeout -k 10 200 env MDQT_LIB=expt/$v/lib/libmdqt.so python3 tools/force_ab.py $v || exit 1; }
   done

@@ -858,6 +858,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
     tmode, tmodel = int(sim.const("force_tail_mode")), sim.const("force_tail_model_bound")
     fixed, raw = sim.const("force_tail_fixed_tiles"), sim.const("force_tail_raw_bound")
+    rm, mid = sim.const("force_mid_radius"), sim.const("force_mid_bound")
     rf, far = sim.const("force_far_radius"), sim.const("force_far_bound")
     rv, vfar = sim.const("force_vfar_radius"), sim.const("force_vfar_bound")
     ru, ufar = sim.const("force_ufar_radius"), sim.const("force_ufar_bound")
@@ -924,16 +925,17 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
                            "tail_mode": "measured+enforced" if tmode == 1 else "a priori",
                            "tail_model_bound": tmodel if tmode == 1 else None,
                            "tiles_over_eps_fixed": fixed, "largest_tile_sum_before_fix": raw,
+                           "mid_radius": rm, "mid_bound": mid,
                            "far_radius": rf, "far_bound": far, "vfar_radius": rv, "vfar_bound": vfar,
                            "ufar_radius": ru, "ufar_bound": ufar, "ufar32_radius": ru32,
                            "note": "tile pairs >= skip_radius apart are skipped (tail_mode measured+enforced: every "
-                                   "call sums per tile n_J g(box distance) over its skipped tile pairs, tiles over "
-                                   "1e-12 get those pairs added exactly (tiles_over_eps_fixed), bound is the largest "
-                                   "remaining per-tile sum; a priori: (N - 1) g(skip_radius)), tile pairs >= far_radius / vfar_radius "
-                                   "apart take the far / very-far / ultra-far pair forms; every ion's force is "
-                                   "within bound + far_bound + vfar_bound + ufar_bound of the exact sum to L/2 (mdqt_engine.cpp "
-                                   "tail_radius / far_radius_l; 0 = exact). fp64 rates count all N(N-1)/2 pairs "
-                                   "(SURVEY 8d)"},
+                                   "call sums per 16-ion sub-tile n g(sub-box distance) over the pairs it drops, tiles over "
+                                   "1e-12 are recomputed exactly (tiles_over_eps_fixed), bound is the largest "
+                                   "remaining sub-tile sum; a priori: (N - 1) g(skip_radius)); sub-tile groups >= mid_radius / "
+                                   "far_radius / vfar_radius / ufar_radius apart take the mid / far / very-far / ultra-far pair "
+                                   "forms; every ion's force is within bound + mid_bound + far_bound + vfar_bound + ufar_bound "
+                                   "of the exact sum to L/2 (mdqt_engine.cpp tail_radius / far_radius_l; 0 = exact). fp64 "
+                                   "rates count all N(N-1)/2 pairs (SURVEY 8d)"},
             "substeps_ms_per_md_step": s_ms / max(ns, 1) if ns else None}
 
 

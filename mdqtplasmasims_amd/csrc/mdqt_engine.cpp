@@ -136,6 +136,10 @@ struct mdqt_ctx {
     // >= r_far apart evaluate their pairs within kFarRelErr (rsq1, degree-6 2^f), r_far the smallest
     // radius with (N - 1) g(r_far) kFarRelErr <= eps — so no ion's force moves by more than eps
     int far_exp = 13;
+    // the mid pair form (round 4; option "force_mid_exp" k, 0 = off): sub-tile groups >= r_mid apart
+    // take rsq1 and the table's 2^t with a degree-4 series, r_mid the smallest radius with (N - 1)
+    // g(r_mid) ((r_mid/lDeb + 3)(kRsq1RelErr + 2^-52) + kTab4RelErr) <= 10^-k
+    int mid_exp = 13;
     // the very-far pair form (option "force_vfar_exp" k, 0 = off): tile pairs >= r_vfar apart use
     // the raw rsq and a degree-5 2^f; r_vfar the smallest radius with
     // (N - 1) g(r) ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) <= 10^-k
@@ -945,6 +949,12 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
                              ? far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound) : (bound = 0., s->L / 2.);
         return n[10] == 'r' ? r : bound;
     }
+    if (!strcmp(n, "force_mid_radius") || !strcmp(n, "force_mid_bound")) {   // the mid form's radius
+        double bound;                                  // and force bound (0: off, r = L/2)
+        const double r = (MDQT_EXP_TAB && s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
+                             ? far_radius_l(s->N, s->L, s->lDeb, s->mid_exp, 5, &bound) : (bound = 0., s->L / 2.);
+        return n[10] == 'r' ? r : bound;
+    }
     if (!strcmp(n, "force_ufar_radius") || !strcmp(n, "force_ufar_bound")) {   // the ultra-far form's
         double bound;                                  // radius and force bound (0: off, r = L/2)
         double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
@@ -1340,6 +1350,7 @@ static int local_tail(mdqt_ctx* s) {
 // at distance r in the form (far: kFarRelErr; very far: (r/lDeb + 3) kRsqRawErr + kExp5RelErr) —
 // L/2 (= never) and bound 0 when k = 0 or that r is >= L/2; bound = (N - 1) g(r) err(r)
 static double far_err(double r, double lDeb, int level) {
+    if (level == 5) return (r / lDeb + 3.) * (kRsq1RelErr + 0x1p-52) + kTab4RelErr;   // the mid form
     if (level == 4) return (r / lDeb) * kUfar32A + kUfar32B;   // the f32 ultra-far form (MDQT_UFAR32)
     if (level == 3) return (r / lDeb) * (kRsqRawErr + 0x1p-24) + 3. * kRsqRawErr + kExp2fRelErr;
     return level == 2 ? (r / lDeb + 3.) * kRsqRawErr + kExp5RelErr : kFarRelErr;
@@ -1378,6 +1389,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     double bound;
     a.Rskip = skip_radius(s, &bound);
     a.tailb = nullptr;
+    a.Rmid = MDQT_EXP_TAB ? far_radius_l(s->N, s->L, s->lDeb, s->mid_exp, 5, &bound) : a.Rcut;
     a.Rfar = far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound);
     a.Rvfar = far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound);
     a.Rufar = far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound);
@@ -2705,6 +2717,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     if (!strcmp(name, "force_vfar_exp")) {             // very-far pair form: eps = 10^-value (0: off)
         if (value < 0 || value > 300) return fail("force_vfar_exp must be 0 (off) .. 300");
         s->vfar_exp = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_mid_exp")) {              // mid pair form: eps = 10^-value (0: off)
+        if (value < 0 || value > 300) return fail("force_mid_exp must be 0 (off) .. 300");
+        s->mid_exp = value;
         return 0;
     }
     if (!strcmp(name, "force_far_exp")) {              // far pair form: eps = 10^-value (0: off)

@@ -317,18 +317,23 @@ __device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, double xi,
 // -2 inside L/2 (the error-bounded tail: its pairs count in the tail sums) — else bit 0 = uniform
 // image (FAST: the fast variant) + 2 x the far level (1 far, 2 very far, 3 ultra far, 4 ultra far in
 // f32); g2 = the squared box gap.  Shared by k_pairs_n3b (the staging wave's lanes) and k_n3b_census.
-struct N3BRadii { double rc2, rf2, rv2, ru2, ru32; };
+struct N3BRadii { double rc2, rf2, rv2, ru2, ru32, rm2; };
 // the squared radii of the classes: skip below the cutoff only for the forces (error-bounded tail,
 // mdqt_engine.cpp tail_radius); the far forms are the fast force variant's
 template <int VARIANT, bool POT>
 __device__ __forceinline__ N3BRadii n3b_radii(const N3BArgs& a) {
     N3BRadii r;
     r.rc2 = POT ? a.Rcut * a.Rcut : a.Rskip * a.Rskip;
+    r.rm2 = (POT || VARIANT != 1 || !MDQT_EXP_TAB || !(a.Rmid < a.Rcut)) ? INFINITY : a.Rmid * a.Rmid;
     r.rf2 = (POT || VARIANT != 1 || !(a.Rfar < a.Rcut)) ? INFINITY : a.Rfar * a.Rfar;
     r.rv2 = (POT || VARIANT != 1 || !(a.Rvfar < a.Rcut)) ? INFINITY : a.Rvfar * a.Rvfar;
     r.ru2 = (POT || VARIANT != 1 || !(a.Rufar < a.Rcut)) ? INFINITY : a.Rufar * a.Rufar;
     r.ru32 = (POT || VARIANT != 1 || !MDQT_UFAR32 || !(a.Rufar32 < a.Rcut)) ? INFINITY : a.Rufar32 * a.Rufar32;
     return r;
+}
+// the far level of a squared gap: 0 exact, 1 mid, 2 far, 3 very far, 4 ultra far, 5 ultra far in f32
+__device__ __forceinline__ int n3b_level(double g2, const N3BRadii& r) {
+    return g2 > r.ru32 ? 5 : g2 > r.ru2 ? 4 : g2 > r.rv2 ? 3 : g2 > r.rf2 ? 2 : g2 > r.rm2 ? 1 : 0;
 }
 template <bool FAST>
 __device__ __forceinline__ double4 n3b_classify(const N3BArgs& a, double invL, const N3BRadii& r, int Iw, int J,
@@ -352,8 +357,7 @@ __device__ __forceinline__ double4 n3b_classify(const N3BArgs& a, double invL, c
     }
     const double cls = (a.use_sort == 1 && g2 > r.rc2) ? (g2 < a.Rcut * a.Rcut ? -2. : -1.)
                                                         : ((FAST && uni) ? 1. : 0.) +
-                                                              (g2 > r.ru32 ? 8. : g2 > r.ru2 ? 6. : g2 > r.rv2 ? 4. :
-                                                               g2 > r.rf2 ? 2. : 0.);
+                                                              2. * n3b_level(g2, r);
     return make_double4(n[0], n[1], n[2], cls);
 }
 
@@ -372,14 +376,17 @@ __device__ __forceinline__ double sub_gap2(const double* __restrict__ SB, int T4
 }
 // the sub-blocks (a, (a + d) & 3) of sub-tile group d as bits 4 a + b
 constexpr unsigned kGroupBits[4] = {0x8421u, 0x1842u, 0x2184u, 0x4218u};
-// each group's far level from the sub-blocks beyond r_far / r_vfar / r_ufar / r_ufar32 (bit 4 a + b):
-// the highest level all four of its sub-blocks reach, 4 bits per group
-__host__ __device__ __forceinline__ unsigned sub_group_levels(unsigned mf, unsigned mv, unsigned mu, unsigned m32) {
+// each group's far level from the sub-blocks beyond r_mid / r_far / r_vfar / r_ufar / r_ufar32 (bit
+// 4 a + b): the highest level all four of its sub-blocks reach, 4 bits per group (k_n3b_census: the
+// same levels as k_n3b_plan's least group gap, counted another way)
+__host__ __device__ __forceinline__ unsigned sub_group_levels(unsigned mm, unsigned mf, unsigned mv, unsigned mu,
+                                                              unsigned m32) {
     unsigned lv = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const unsigned g = kGroupBits[d];
-        const unsigned x = (m32 & g) == g ? 4u : (mu & g) == g ? 3u : (mv & g) == g ? 2u : (mf & g) == g ? 1u : 0u;
+        const unsigned x = (m32 & g) == g ? 5u : (mu & g) == g ? 4u : (mv & g) == g ? 3u : (mf & g) == g ? 2u
+                         : (mm & g) == g ? 1u : 0u;
         lv |= x << (4 * d);
     }
     return lv;
@@ -469,8 +476,8 @@ void k_pairs_n3b(N3BArgs a) {
     //    of the two ends; equal ends = one minimum-image multiple per axis for every pair, bit for
     //    bit what mic_r computes per pair (the fast variant then skips that rint per pair);
     //  * otherwise the per-pair minimum image.
-    // class: -1 / -2 skip; otherwise bit 0 = uniform image, + 2 x the far level (1 far pair form, 2
-    // very far, 3 ultra far, 4 ultra far in f32; forces only): 0 .. 9 (n3b_pack_class: tpw[q]).
+    // class: -1 / -2 skip; otherwise bit 0 = uniform image, + 2 x the far level (n3b_level: 1 mid, 2
+    // far, 3 very far, 4 ultra far, 5 ultra far in f32; forces only): 0 .. 11 (n3b_pack_class: tpw[q]).
     // The forces take them, with the sub-tile groups (tg[q]), from the call's plan (k_n3b_plan: one
     // 8-byte word per tile pair, loaded by lanes 0..15); without a plan (potentials, unsorted order)
     // the staging lanes classify the tile pairs themselves and every group runs in the exact form.
@@ -563,19 +570,22 @@ void k_pairs_n3b(N3BArgs a) {
                             n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(true, groups, l, sx, sy, sz, mi, pj, mj, ax, ay,
                                                                             az, tx, ty, tz, c, nsh);
                         } else {                    // each form over the groups at its level
-                            const unsigned g4 = level_groups(word, 4), g3 = level_groups(word, 3),
-                                           g2 = level_groups(word, 2), g1 = level_groups(word, 1),
-                                           g0 = level_groups(word, 0);
+                            const unsigned g5 = level_groups(word, 5), g4 = level_groups(word, 4),
+                                           g3 = level_groups(word, 3), g2 = level_groups(word, 2),
+                                           g1 = level_groups(word, 1), g0 = level_groups(word, 0);
+                            if (g4) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 4>(false, g4, l, sx, sy, sz, mi, pj, mj,
+                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
                             if (g3) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(false, g3, l, sx, sy, sz, mi, pj, mj,
                                                                                        ax, ay, az, tx, ty, tz, c, nsh);
                             if (g2) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(false, g2, l, sx, sy, sz, mi, pj, mj,
                                                                                        ax, ay, az, tx, ty, tz, c, nsh);
-                            if (g1) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 1>(false, g1, l, sx, sy, sz, mi, pj, mj,
-                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
+                            if (MDQT_EXP_TAB && g1)
+                                n3b_pair<VARIANT, GUARD, false, true, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(
+                                    false, g1, l, sx, sy, sz, mi, pj, mj, ax, ay, az, tx, ty, tz, c, nsh);
                             if (g0) n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(false, g0, l, sx, sy, sz, mi, pj, mj, ax,
                                                                                     ay, az, tx, ty, tz, c, nsh);
 #if !defined(MDQT_EXPT_UFAR_SKIP)                   // last: nothing after it keeps sx, nsh live (diagnostic build: skip it, wrong results)
-                            if (g4) n3b_pair_uf32(g4, l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
+                            if (g5) n3b_pair_uf32(g5, l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
 #endif
                         }
                     } else {
@@ -587,12 +597,15 @@ void k_pairs_n3b(N3BArgs a) {
                         n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(true, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                          az, tx, ty, tz, c);
                     } else {                        // (ultra far with a per-pair image: rare, very-far form)
-                        const unsigned g2 = level_groups(word, 2) | level_groups(word, 3) | level_groups(word, 4),
-                                       g1 = level_groups(word, 1), g0 = level_groups(word, 0);
+                        const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
+                                       g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
+                        if (g3) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3>(false, g3, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                                    ay, az, tx, ty, tz, c);
                         if (g2) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax,
                                                                                     ay, az, tx, ty, tz, c);
-                        if (g1) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 1>(false, g1, l, xi, yi, zi, mi, pj, mj, ax,
-                                                                                    ay, az, tx, ty, tz, c);
+                        if (MDQT_EXP_TAB && g1)
+                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(false, g1, l, xi, yi, zi, mi,
+                                                                                               pj, mj, ax, ay, az, tx, ty, tz, c);
                         if (g0) n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(false, g0, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                                  az, tx, ty, tz, c);
                     }
@@ -680,7 +693,7 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
     const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
     const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2, nullptr};
     const double rcut2 = a.Rcut * a.Rcut;
-    const N3BRadii none = {rcut2, INFINITY, INFINITY, INFINITY, INFINITY};
+    const N3BRadii none = {rcut2, INFINITY, INFINITY, INFINITY, INFINITY, INFINITY};
     const int T = a.T, N = a.N, PS = a.Npad;
     for (int k = blockIdx.x; k < n; k += gridDim.x) {
         const int I = __builtin_amdgcn_readfirstlane(list[k]);
@@ -747,7 +760,8 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
 // 0 skipped (boxes beyond L/2), 1 skipped by the tail radius, 2 ragged last tile (exact, per-pair
 // image), 3 exact per-pair image, 4 exact uniform image, 5 far per-pair, 6 far uniform, 7 very far
 // per-pair (ultra far with a per-pair image included), 8 very far uniform, 9 ultra far uniform (f64),
-// 10 ultra far uniform in f32, 11 skipped sub-tile groups of evaluated tile pairs.  One workgroup
+// 10 ultra far uniform in f32, 11 skipped sub-tile groups of evaluated tile pairs, 12 mid per-pair,
+// 13 mid uniform (round 4: appended, the earlier indices kept).  One workgroup
 // per (block P, block distance db); thread (b, q) takes tile pair (16 P + q, 16 Q + b) as the
 // kernel's wave q at J-step b does.
 __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long long* __restrict__ out) {
@@ -771,8 +785,8 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
         // the class of a group at far level gl (the kernel's dispatch)
         auto cls_of = [&](unsigned gl) {
             if (rag) return 2;
-            if (uni) return gl == 4 ? 10 : gl == 3 ? 9 : gl == 2 ? 8 : gl == 1 ? 6 : 4;
-            return gl >= 2 ? 7 : gl == 1 ? 5 : 3;
+            if (uni) return gl == 5 ? 10 : gl == 4 ? 9 : gl == 3 ? 8 : gl == 2 ? 6 : gl == 1 ? 13 : 4;
+            return gl >= 3 ? 7 : gl == 2 ? 5 : gl == 1 ? 12 : 3;
         };
         if (t4.w < 0.) {
             const int k = t4.w == -2. ? 1 : 0;
@@ -784,13 +798,14 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
             atomicAdd(&h[kCensus + k], (unsigned long long)(nI * (nI - 1) / 2));
         } else {
             const int T4 = 4 * a.T;
-            unsigned act = 0, mf = 0, mv = 0, mu = 0, m32 = 0;
+            unsigned act = 0, mm = 0, mf = 0, mv = 0, mu = 0, m32 = 0;
             double np[4] = {0., 0., 0., 0.};       // ion pairs per group
             for (int sa = 0; sa < 4; ++sa)
                 for (int sb = 0; sb < 4; ++sb) {
                     const double sg = sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, 1. / a.L);
                     const unsigned bit = 1u << (4 * sa + sb);
                     if (sg <= rad.rc2) act |= bit;
+                    if (sg > rad.rm2) mm |= bit;
                     if (sg > rad.rf2) mf |= bit;
                     if (sg > rad.rv2) mv |= bit;
                     if (sg > rad.ru2) mu |= bit;
@@ -798,7 +813,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                     np[(sb - sa) & 3] += sub_count(a.N, 4 * I + sa) * sub_count(a.N, 4 * J + sb);
                 }
             const unsigned g = a.use_sort == 1 ? sub_groups_of(act) : 0xFu;   // (2: nothing skipped)
-            const unsigned lv = sub_group_levels(mf, mv, mu, m32);
+            const unsigned lv = sub_group_levels(mm, mf, mv, mu, m32);
             for (int d = 0; d < 4; ++d) {
                 const int k = (g >> d) & 1u ? cls_of((lv >> (4 * d)) & 15u) : 11;
                 atomicAdd(&h[k], 1024ull);
@@ -860,7 +875,7 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
             for (int d = 0; d < 4; ++d) {
                 const double gm = fmin(fmin(sg[0][d & 3], sg[1][(1 + d) & 3]), fmin(sg[2][(2 + d) & 3], sg[3][(3 + d) & 3]));
                 if (a.use_sort != 1 || gm <= rad.rc2) {
-                    const int x = !FARF ? 0 : gm > rad.ru32 ? 4 : gm > rad.ru2 ? 3 : gm > rad.rv2 ? 2 : gm > rad.rf2 ? 1 : 0;
+                    const int x = !FARF ? 0 : n3b_level(gm, rad);
                     groups |= 1u << d;
                     lvm |= 1u << (4 * x + d);
                 }

@@ -254,6 +254,17 @@ constexpr double kNegLog2e = -1.4426950408889634;   // -log2(e)
 // 2^f by a degree-6 Chebyshev fit on [-1/2, 1/2] (2.6e-9 relative in double Horner, mpmath fit,
 // measured on 4,001 points) — 6 operations fewer per pair than the exact form.
 constexpr double kFarRelErr = 3e-9;
+// The mid tier (round 4, sub-tile groups >= r_mid apart): rsq1 — relative error 1.5 e^2 + 2u for the
+// raw rsq's e <= kRsqRawErr: <= kRsq1RelErr — and 2^t by the 64-entry table with a degree-4 series
+// (2.53e-15 measured, + the table entry's and the product's rounding: kTab4RelErr).  t carries ri's
+// error times r/lDeb, the force factor 3 ri's: a term is within (r/lDeb + 3)(kRsq1RelErr + 2^-52) +
+// kTab4RelErr of itself (mdqt_engine.cpp far_err, level 5).
+constexpr double kRsq1RelErr = 2.2e-14;
+// 2^t of the exact (and mid) pair forms by the 64-entry LDS table (mdqt_pairs.hpp exp2_neg_cut_tab)
+#ifndef MDQT_EXP_TAB
+#define MDQT_EXP_TAB 1   // A/B round 4 (plan-based block kernel): C3 -3.5 %, C5 -0.8 %, N = 1M +0.3 %; round 3: C2 MD step -0.2 us
+#endif
+constexpr double kTab4RelErr = 4e-15;
 __device__ __forceinline__ double rsq1(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double q = __builtin_amdgcn_rsq(x);
@@ -411,6 +422,8 @@ struct N3BArgs {
     const double* Rs;   // [3][Npad] positions in sorted order
     const int* perm;    // sorted index -> ion
     const double* boxes;// [12][T]: tile center (x, y, z), half extents, raw coordinate min, max
+    double Rmid;        // sub-tile groups >= Rmid apart take the mid pair form (rsq1 + table 2^t, ~2e-14
+                        // relative; forces only, MDQT_EXP_TAB); >= Rcut: never
     double Rfar;        // tile pairs whose boxes are >= Rfar apart take the far pair form (kFarRelErr;
                         // forces only, use_sort 1 or 2); >= Rcut: never
     double Rvfar;       // >= Rvfar apart: the very-far form (raw rsq, degree-5 2^f); >= Rcut: never
@@ -453,7 +466,7 @@ hipError_t launch_tail_max(const double* tailb, int T, double eps, unsigned long
 hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const int* list, double* out,
                            hipStream_t s);
 // census of k_pairs_n3b's work by tile-pair class (mdqt_forces.hip k_n3b_census): out[2 kCensus]
-constexpr int kCensus = 12;
+constexpr int kCensus = 14;
 hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 

@@ -19,9 +19,7 @@ struct PairC {
 // arithmetic) and 2^(g/64) = e^(g ln2/64) by its degree-5 Taylor series (|g ln2/64| <= 0.0055:
 // truncation 3.5e-17); <= 2 ulp.  Five FMAs instead of eleven for three integer operations and one
 // LDS read; the cutoff folded into the exponent as in exp2_neg_cut.
-#ifndef MDQT_EXP_TAB
-#define MDQT_EXP_TAB 1   // A/B round 4 (plan-based block kernel): C3 -3.5 %, C5 -0.8 %, N = 1M +0.3 %; round 3: C2 MD step -0.2 us
-#endif
+// (MDQT_EXP_TAB: mdqt_internal.hpp, where the engine's mid-tier radius sees it too)
 static __constant__ const double kExp2Tab64[64] = {
     0x1.0000000000000p+0, 0x1.02c9a3e778061p+0, 0x1.059b0d3158574p+0, 0x1.0874518759bc8p+0,
     0x1.0b5586cf9890fp+0, 0x1.0e3ec32d3d1a2p+0, 0x1.11301d0125b51p+0, 0x1.1429aaea92de0p+0,
@@ -49,6 +47,20 @@ __device__ __forceinline__ double exp2_neg_cut_tab(double t64, bool keep, const 
     p = fma(p, g, 0x1.c6b08d704a0c0p-23);
     p = fma(p, g, 0x1.ebfbdff82c58fp-15);
     p = fma(p, g, 0x1.62e42fefa39efp-7);
+    p = fma(p, g, 1.0);
+    return ldexp(p * tab[mi & 63], keep ? (mi >> 6) : -1100);
+}
+// the mid tier's 2^t (Newton-3 blocks, pairs >= r_mid apart): the same table times a degree-4 fit of
+// 2^(g/64) on g in [-1/2, 1/2] (Chebyshev interpolation in long double, coefficients rounded to double;
+// 2.53e-15 relative in double Horner, measured on 200,001 points) — one FMA fewer (kTab4RelErr)
+__device__ __forceinline__ double exp2_neg_cut_tab4(double t64, bool keep, const double* tab) {
+    const double m = __builtin_rint(t64);
+    const double g = t64 - m;
+    const int mi = (int)m;
+    double p = 0x1.3b2ad028fa84ap-31;
+    p = fma(p, g, 0x1.c6b0c40d96fd0p-23);
+    p = fma(p, g, 0x1.ebfbdff82ac88p-15);
+    p = fma(p, g, 0x1.62e42fefa0352p-7);
     p = fma(p, g, 1.0);
     return ldexp(p * tab[mi & 63], keep ? (mi >> 6) : -1100);
 }
@@ -144,6 +156,17 @@ __device__ __forceinline__ double pair_ft_cut(double dx, double dy, double dz, c
         return ((ri + c.invlDeb) * exp2_neg_cut_tab(dr * (c.invlDeb * (64. * kNegLog2e)), dr < c.Rcut, c.etab)) *
                (ri * ri);
     return ((ri + c.invlDeb) * exp2_neg_cut(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
+}
+
+// pair_ft_cut of a mid-range sub-tile group (Newton-3 blocks, gap >= r_mid; MDQT_EXP_TAB): rsq1 and
+// the table's 2^t with the degree-4 series — a term within (r/lDeb + 3)(kRsq1RelErr + 2^-52) +
+// kTab4RelErr of itself; the cutoff on the f64 r^2 (rsq1's r carries 2e-14: pairs at L/2 would flip)
+__device__ __forceinline__ double pair_ft_cut_mid(double dx, double dy, double dz, const PairC& c) {
+    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+    const double ri = rsq1(r2);
+    const double dr = r2 * ri;
+    return ((ri + c.invlDeb) * exp2_neg_cut_tab4(dr * (c.invlDeb * (64. * kNegLog2e)), r2 < c.rc2, c.etab)) *
+           (ri * ri);
 }
 
 // pair_ft_cut of a far tile pair (Newton-3 blocks): rsq1 and the degree-6 2^f, within kFarRelErr
@@ -243,10 +266,12 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
         return;
     }
     static_assert(!FAR || (CUT && !POT), "the far pair form is the fast force variant's");
-    // FAR: 0 exact form, 1 far, 2 very far, 3 ultra far (Newton-3 blocks, error-bounded)
-    double ft = FAR == 3 ? pair_ft_cut_ufar(dx, dy, dz, c)
-              : FAR == 2 ? pair_ft_cut_vfar(dx, dy, dz, c)
-              : FAR == 1 ? pair_ft_cut_far(dx, dy, dz, c)
+    static_assert(FAR != 1 || MDQT_EXP_TAB, "the mid tier's 2^t is the table's");
+    // FAR: 0 exact form, 1 mid, 2 far, 3 very far, 4 ultra far (Newton-3 blocks, error-bounded)
+    double ft = FAR == 4 ? pair_ft_cut_ufar(dx, dy, dz, c)
+              : FAR == 3 ? pair_ft_cut_vfar(dx, dy, dz, c)
+              : FAR == 2 ? pair_ft_cut_far(dx, dy, dz, c)
+              : FAR == 1 ? pair_ft_cut_mid(dx, dy, dz, c)
               : CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];
     ft *= m;

@@ -97,7 +97,7 @@ def test_large_config_forces_and_interval(cfg, orc):
     print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}, "
           f"max|dF| = {dabs:.3e}; skip radius {rt:.3f} (L/2 {L / 2:.3f}), tail bound {bound:.2e}; "
           f"far radius {rf:.3f}, far bound {fbound:.2e}")
-    vbound = s.const("force_vfar_bound") + s.const("force_ufar_bound")
+    vbound = s.const("force_vfar_bound") + s.const("force_ufar_bound") + s.const("force_mid_bound")
     assert err <= 1e-12
     assert dabs <= bound + fbound + vbound + 1e-13 * np.abs(G).max()
     mom = np.abs(F.sum(axis=1)).max() / (np.abs(F).sum() / N)
@@ -186,30 +186,36 @@ def test_error_bounded_tail_and_far_form(cfg):
     ion: the skip radius r_t < L/2 (force_tail_exp 12: |dF_i| <= (N - 1) g(r_t) <= 1e-12,
     mdqt_engine.cpp tail_radius; active at N ~ 1e6), the far pair form beyond r_far (force_far_exp
     13: (N - 1) g(r_far) kFarRelErr <= 1e-13) and the very-far form beyond r_vfar (force_vfar_exp
-    13: (N - 1) g(r) ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) <= 1e-13) — each alone and all
-    together, plus the summation-order rounding; r_t is a no-op at C3 and C5"""
+    13: (N - 1) g(r) ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) <= 1e-13), the ultra-far forms and the
+    mid form beyond r_mid (force_mid_exp 13, round 4: (N - 1) g(r) ((r/lDeb + 3)(kRsq1RelErr + 2^-52)
+    + kTab4RelErr) <= 1e-13) — each alone and all together, plus the summation-order rounding; r_t
+    is a no-op at C3 and C5"""
     import mdqtplasmasims_amd as M
     s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg]).init()
     L = s.const("L")
     rt, tb = s.const("force_skip_radius"), s.const("force_tail_bound")
+    rm, mb0 = s.const("force_mid_radius"), s.const("force_mid_bound")
     rf, fb = s.const("force_far_radius"), s.const("force_far_bound")
     rv, vb = s.const("force_vfar_radius"), s.const("force_vfar_bound")
     ru, ub = s.const("force_ufar_radius"), s.const("force_ufar_bound")
     ru32 = s.const("force_ufar32_radius")             # the f32 ultra-far shell (its bound is in ub)
     assert 0 < fb <= 1e-13 and rf < L / 2 and 0 < vb <= 1e-13 and rf < rv < L / 2
+    assert 0 < mb0 <= 1e-13 and rm < rf
     assert 0 < ub <= 2e-13 and rf < ru < L / 2 and ru <= ru32 <= L / 2   # ub: f64 + f32 shells, 1e-13 each
     # (C4: the measured bound needs a force call — read after the calls below)
     assert (rt < L / 2) if cfg == "C4" else (tb == 0 and rt == L / 2)
     out = {}
-    for te, fe, ve, ue in ((12, 13, 13, 13), (0, 13, 0, 0), (0, 0, 13, 0), (0, 0, 0, 13), (12, 0, 0, 0),
-                           (0, 0, 0, 0)):
+    for te, me, fe, ve, ue in ((12, 13, 13, 13, 13), (0, 0, 13, 0, 0), (0, 0, 0, 13, 0), (0, 0, 0, 0, 13),
+                               (12, 0, 0, 0, 0), (0, 13, 0, 0, 0), (0, 0, 0, 0, 0)):
         s.set_option("force_tail_exp", te)
+        s.set_option("force_mid_exp", me)
         s.set_option("force_far_exp", fe)
         s.set_option("force_vfar_exp", ve)
         s.set_option("force_ufar_exp", ue)
         s.forces()
-        out[te, fe, ve, ue] = s.get_state()["F"]
+        out[te, me, fe, ve, ue] = s.get_state()["F"]
     assert s.const("force_skip_radius") == L / 2 and s.const("force_far_bound") == 0
+    assert s.const("force_mid_bound") == 0 and s.const("force_mid_radius") == L / 2
     assert s.const("force_vfar_bound") == 0 and s.const("force_ufar_bound") == 0
     if cfg == "C4":
         # force_tail_mode 1: the bound is what the calls measured — per tile, n_J g(box distance)
@@ -226,18 +232,20 @@ def test_error_bounded_tail_and_far_form(cfg):
               f"tiles over 1e-12 {s.const('force_tail_fixed_tiles'):.0f}")
         assert 0 < tb <= 1e-12 and 0 < mb <= 1e-12 / 1.25 * (1 + 1e-9)     # kTailMargin
         assert s.const("force_tail_fixed_tiles") == 0 and s.const("force_tail_raw_bound") <= 1e-12
-    Fe = out[0, 0, 0, 0]
+    Fe = out[0, 0, 0, 0, 0]
     scale = 1e-13 * np.abs(Fe).max()
     d = {k: np.abs(v - Fe).max() for k, v in out.items()}
-    print(f"{cfg} N={s.N}: r_t {rt:.3f} (bound {tb:.2e}), r_far {rf:.3f} ({fb:.2e}), r_vfar {rv:.3f} ({vb:.2e}), "
-          f"r_ufar {ru:.3f} ({ub:.2e}), r_ufar32 {ru32:.3f}, L/2 {L / 2:.3f}; max_i |dF_i|: all {d[12, 13, 13, 13]:.3e}, far only "
-          f"{d[0, 13, 0, 0]:.3e}, very far only {d[0, 0, 13, 0]:.3e}, ultra far only {d[0, 0, 0, 13]:.3e}, tail only "
-          f"{d[12, 0, 0, 0]:.3e}; max|F| {np.abs(Fe).max():.3e}")
-    assert d[12, 13, 13, 13] <= tb + fb + vb + ub + scale
-    assert d[0, 13, 0, 0] <= fb + scale
-    assert d[0, 0, 13, 0] <= vb + scale
-    assert d[0, 0, 0, 13] <= ub + scale
-    assert d[12, 0, 0, 0] <= tb + scale
+    print(f"{cfg} N={s.N}: r_t {rt:.3f} (bound {tb:.2e}), r_mid {rm:.3f} ({mb0:.2e}), r_far {rf:.3f} ({fb:.2e}), "
+          f"r_vfar {rv:.3f} ({vb:.2e}), r_ufar {ru:.3f} ({ub:.2e}), r_ufar32 {ru32:.3f}, L/2 {L / 2:.3f}; max_i |dF_i|: "
+          f"all {d[12, 13, 13, 13, 13]:.3e}, mid only {d[0, 13, 0, 0, 0]:.3e}, far only {d[0, 0, 13, 0, 0]:.3e}, "
+          f"very far only {d[0, 0, 0, 13, 0]:.3e}, ultra far only {d[0, 0, 0, 0, 13]:.3e}, tail only "
+          f"{d[12, 0, 0, 0, 0]:.3e}; max|F| {np.abs(Fe).max():.3e}")
+    assert d[12, 13, 13, 13, 13] <= tb + mb0 + fb + vb + ub + scale
+    assert d[0, 13, 0, 0, 0] <= mb0 + scale
+    assert d[0, 0, 13, 0, 0] <= fb + scale
+    assert d[0, 0, 0, 13, 0] <= vb + scale
+    assert d[0, 0, 0, 0, 13] <= ub + scale
+    assert d[12, 0, 0, 0, 0] <= tb + scale
     s.close()
     if cfg == "C5":                                    # r_t >= L/2 at C3 too: exact skipping only
         x = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C3"])
@@ -291,7 +299,8 @@ def test_tail_bound_enforced_on_clustered_ions(cfg):
     assert s.const("force_scheme") == 3 and s.const("force_tail_mode") == 1
     rt0 = s.const("force_skip_radius")
     assert rt0 < L / 2
-    fb = s.const("force_far_bound") + s.const("force_vfar_bound") + s.const("force_ufar_bound")
+    fb = (s.const("force_far_bound") + s.const("force_vfar_bound") + s.const("force_ufar_bound")
+          + s.const("force_mid_bound"))
     out = {}
     # A: the product defaults; the model's r_t is too small here
     s.forces()
@@ -311,7 +320,7 @@ def test_tail_bound_enforced_on_clustered_ions(cfg):
     assert s.const("force_tail_bound") <= eps
     # C: the tail alone (far forms off), from the model's radius again (set_state resets the scale)
     s.set_state(*state)
-    for o in ("force_far_exp", "force_vfar_exp", "force_ufar_exp"):
+    for o in ("force_mid_exp", "force_far_exp", "force_vfar_exp", "force_ufar_exp"):
         s.set_option(o, 0)
     assert s.const("force_skip_radius") == rt0
     s.forces()

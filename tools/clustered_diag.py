@@ -22,7 +22,7 @@ L = s.const("L"); lD = s.const("lDeb")
 state = clustered_state(N0, L, frac, rc)
 s.set_state(*state)
 s.set_option("force_tail_exp", k)
-for o in ("force_far_exp", "force_vfar_exp", "force_ufar_exp"):
+for o in ("force_mid_exp", "force_far_exp", "force_vfar_exp", "force_ufar_exp"):
     s.set_option(o, 0)
 s.forces(); C = s.get_state()["F"]
 print("fixed tiles", s.const("force_tail_fixed_tiles"), "rt", s.const("force_skip_radius"), flush=True)

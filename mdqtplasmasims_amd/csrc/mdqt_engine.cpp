@@ -1407,7 +1407,8 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
         HIPCHK(launch_spatial_order(o, s->stream));
         a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes; a.subboxes = s->dSubBoxes;
         if (tail_measured(s) && a.Rskip < a.Rcut) a.tailb = s->dTail;
-        const size_t need = (size_t)std::max(a.Phi - a.Plo, 0) * a.nd * 256;   // the plan (k_n3b_plan)
+        // the plan (k_n3b_plan): 256 tile-pair words per (P, db), then one J-step mask per (P, db)
+        const size_t need = (size_t)std::max(a.Phi - a.Plo, 0) * a.nd * 257;
         if (need > s->capPlan) {
             if (s->dPlan) HIPCHK(hipFree(s->dPlan));
             s->dPlan = nullptr;

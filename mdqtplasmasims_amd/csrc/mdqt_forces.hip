@@ -508,13 +508,22 @@ void k_pairs_n3b(N3BArgs a) {
     double* ay = accj[q][1];
     double* az = accj[q][2];
     const size_t plane = (size_t)3 * a.Npad;
+    // the plan's J-step masks (after its tile-pair words): bit b = some tile pair of J step b has work
+    const unsigned* jsteps = plan ? (const unsigned*)(plan + (size_t)(a.Phi - a.Plo) * a.nd * (BW * BW)) : nullptr;
     for (int db = d0; db < d1; ++db) {
         if (!(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2) continue;   // the other half covers it
         const int Q = (P + db) % a.NB;
         double bx = 0., by = 0., bz = 0.;          // this block distance's i partial (3-level blocking)
+        const unsigned* jstep = jsteps ? jsteps + 2 * ((size_t)(P - a.Plo) * a.nd + db) : nullptr;
         for (int b = 0; b < BW; ++b) {
             const int J = Q * BW + b;
             if (J >= T) break;
+            // (the mask re-read every J step — a scalar load — rather than held across the pair loop)
+            if (jstep && !((*jstep >> b) & 1u)) {   // every tile pair of this J step skipped (wave-uniform):
+                if (q < (POT ? 1 : 3))              // J's rows get the combine's value, -0, and no barrier
+                    a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? 0. : -0.;
+                continue;
+            }
             if (q == kStage) {                      // stage J (by sub-tiles, twice over)
                 const int j = J * 64 + l;
                 const bool vj = j < N;
@@ -846,6 +855,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
 template <int VARIANT, bool GUARD>
 __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
     __shared__ double ti[BW][4], tj[BW][4];
+    __shared__ unsigned jm;
     constexpr bool FARF = VARIANT == 1 && !GUARD && MDQT_N3_CUT;
     const int t = threadIdx.x, q = t & (BW - 1), b = t / BW;
     const int Pl = (int)blockIdx.x / a.nd, db = (int)blockIdx.x % a.nd;
@@ -853,7 +863,8 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
     const int I = P * BW + q, J = Q * BW + b;
     const bool tmeas = a.tailb != nullptr;
     if (tmeas && t < 64) { ti[t >> 2][t & 3] = 0.; tj[t >> 2][t & 3] = 0.; }
-    if (tmeas) __syncthreads();
+    if (t == 0) jm = 0u;
+    __syncthreads();
     uint2 w = make_uint2(1u, 0xFFu);                // class -1 where the block kernel never looks
     const bool half = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
     if (!half && I < a.T && J < a.T && (db > 0 || J >= I)) {
@@ -899,8 +910,18 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
         }
     }
     plan[((size_t)Pl * a.nd + db) * (BW * BW) + t] = w;
+    // the J-step mask of (P, db): J step b has work iff one of its tile pairs has a class >= 0
+    // (threads 16 b .. 16 b + 15 are lanes 16 (b & 3) .. of wave b >> 2)
+    const unsigned long long wk = __ballot((int)(w.x & 15u) >= 2);
+    if ((t & 63) == 0) {
+        unsigned m4 = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m4 |= ((wk >> (16 * k)) & 0xFFFFull) ? 1u << k : 0u;
+        atomicOr(&jm, m4 << (4 * (t >> 6)));
+    }
+    __syncthreads();
+    if (t == 0) plan[(size_t)(a.Phi - a.Plo) * a.nd * (BW * BW) + (size_t)Pl * a.nd + db] = make_uint2(jm, 0u);
     if (tmeas) {
-        __syncthreads();
         if (t < 64) {
             const int k = t >> 2, u = t & 3;
             if (ti[k][u] > 0.) atomicAdd(a.tailb + 4 * (P * BW + k) + u, ti[k][u]);

@@ -439,9 +439,10 @@ struct N3BArgs {
                         // n_b g(sub-block gap) — the measured bound on what each of its ions loses
                         // (zeroed before the launch, summed by k_n3b_plan; nullptr: not measured)
     const double* subboxes;   // [6][4T]: the 16-ion sub-tiles' centers and half extents (use_sort)
-    uint2* plan;        // force calls in spatial order: [(Phi - Plo) nd][256] tile-pair words, written by
-                        // k_n3b_plan (launch_forces_n3b) and read by k_pairs_n3b; nullptr: classified
-                        // in the block kernel (every sub-tile group exact; no tail sums)
+    uint2* plan;        // force calls in spatial order: [(Phi - Plo) nd][256] tile-pair words, then
+                        // [(Phi - Plo) nd] J-step masks (.x), written by k_n3b_plan (launch_forces_n3b)
+                        // and read by k_pairs_n3b; nullptr: classified in the block kernel (every
+                        // sub-tile group exact; no tail sums)
 };
 struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Stall counters of the block kernel, product library vs the round-3 tree (expt/r03tree), at one
+# Stall counters of the block kernel, product library vs a baseline tree (expt/${BASE:-basetree}, a git worktree), at one
 # config of tools/force_ab.py (diagnostic A/B; one rocprofv3 --pmc pass each).
 #   bash tools/gpu/r04_diag_pmc.sh TAG [C3|C5|1M] [counters...]
 TAG=${1:-diag}
@@ -10,9 +10,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
-for v in product r03; do
+for v in product ${BASE:-basetree}; do
   cd /tmp
-  if [ $v = r03 ]; then export MDQT_ROOT="$R/expt/r03tree"; else unset MDQT_ROOT; fi
+  if [ $v != product ]; then export MDQT_ROOT="$R/expt/$v"; else unset MDQT_ROOT; fi
   MDQT_AB_CFGS=$CFG timeout -s KILL 200 rocprofv3 --pmc $PMC -d "$R/gpurun_out/${TAG}_$v" -o run -- python3 "$R/tools/force_ab.py" $v > "$R/gpurun_out/${TAG}_$v.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_$v.log"; exit 1; }
   cd "$R"
   python3 tools/pmc_summary.py $(ls gpurun_out/${TAG}_$v/*/*.db gpurun_out/${TAG}_$v/*.db 2>/dev/null | head -1) > gpurun_out/${TAG}_$v.json || exit 1

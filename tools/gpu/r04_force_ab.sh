@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the block-kernel variants at C3, C5, N = 1M (tools/force_ab.py): the product library, the
-# round-3 tree (expt/r03tree, its own package) and diagnostic builds (expt/<name>), alternating.
+# baseline tree (expt/basetree: a git worktree with its own build) and diagnostic builds (expt/<name>), alternating.
 #   bash tools/gpu/r04_force_ab.sh [rounds]
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out

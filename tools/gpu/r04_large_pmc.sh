@@ -12,7 +12,9 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
 BASE="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pump-lines --no-mcmd-lines --no-e2e-line --no-replicas-line --sharded-steps 1 --million-steps 1 --md-only-config none --sharded-config none --million-config none"
-db() { ls gpurun_out/$1/*/*.db gpurun_out/$1/*.db 2>/dev/null | head -1; }
+W=/tmp/large_pmc_$$                         # the databases stay on the box (gpurun_out/ is capped at 64 MiB)
+mkdir -p $W
+db() { ls $W/$1/*/*.db $W/$1/*.db 2>/dev/null | head -1; }
 for cfg in $CFGS; do
   case $cfg in
     c3) B="$BASE --md-only-config c3" ;;
@@ -21,10 +23,10 @@ for cfg in $CFGS; do
     *) echo "unknown config $cfg"; exit 2 ;;
   esac
   cd /tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_${cfg}_trace" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_trace.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_trace.log"; exit 1; }
-  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$R/gpurun_out/${TAG}_${cfg}_sq" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_sq.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_sq.log"; exit 1; }
-  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_${cfg}_fetch" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_fetch.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_fetch.log"; exit 1; }
-  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_${cfg}_write" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_write.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_write.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$W/${TAG}_${cfg}_trace" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_trace.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_trace.log"; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$W/${TAG}_${cfg}_sq" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_sq.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_sq.log"; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$W/${TAG}_${cfg}_fetch" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_fetch.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_fetch.log"; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$W/${TAG}_${cfg}_write" -o run -- python3 $B > "$R/gpurun_out/${TAG}_${cfg}_write.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_${cfg}_write.log"; exit 1; }
   cd "$R"
   python3 tools/pmc_summary.py $(db ${TAG}_${cfg}_sq) $(db ${TAG}_${cfg}_fetch) $(db ${TAG}_${cfg}_write) \
       --trace $(db ${TAG}_${cfg}_trace) --tag "bench.py ${cfg} line (steps 1): $B" > gpurun_out/${TAG}_${cfg}_pmc.json || exit 1

@@ -200,16 +200,22 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     exact (r_t = L/2); a no-op where the a-priori radius below is >= L/2 (every
  *                     BASELINE size but N ~ 1e6).  "force_skip_radius" reports r_t
  *   "force_tail_mode": how r_t is bounded.  1 (default, every world size) = measured and
- *                     enforced: r_t from a density model of the per-tile sums (<= the a-priori
- *                     radius); every force call sums, per tile, n_J g(box distance) over its
- *                     skipped tile pairs (all-reduced over the ranks), and every tile whose sum
- *                     exceeds eps gets those pairs added exactly (an exact pass over its skipped
- *                     tile pairs), so eps holds for any configuration; when that happened the next
- *                     host sync widens r_t (stderr says so).  "force_tail_bound" = the largest
- *                     per-tile sum the calls met (NaN before a measured call), "force_tail_raw_bound"
- *                     the largest before the exact pass, "force_tail_fixed_tiles" the tiles over
- *                     eps so far, "force_tail_model_bound" the model's sum at r_t.  0 = a priori:
+ *                     enforced: r_t from a density model of the per-sub-tile sums (<= the a-priori
+ *                     radius); every force call sums, per 16-ion sub-tile, n g(sub-box distance)
+ *                     over the pairs it drops inside L/2 (all-reduced over the ranks), and every
+ *                     tile with a sub-tile sum over eps gets its ions' forces recomputed exactly
+ *                     (all pairs to L/2), so eps holds for any configuration; when that happened
+ *                     the next host sync widens r_t (stderr says so).  "force_tail_bound" = the
+ *                     largest sub-tile sum of the other tiles over the measured calls (NaN before
+ *                     one; reset with the state, N or these options), "force_tail_raw_bound" the
+ *                     largest of all, "force_tail_fixed_tiles" the tiles recomputed so far,
+ *                     "force_tail_model_bound" the model's sum at r_t.  0 = a priori:
  *                     r_t the smallest radius with (N - 1) g(r_t) <= eps, "force_tail_bound" that
+ *   "force_mid_exp":  block pairs in spatial order: 16-ion sub-tile groups >= r_mid apart take the
+ *                     mid pair form (rsq + one Newton step, table 2^t with a degree-4 series; a
+ *                     term within (r/lDeb + 3)(2.2e-14 + 2^-52) + 4e-15 relative), r_mid the
+ *                     smallest radius with (N - 1) g(r) err(r) <= 10^-k; k = 13 default, 0 = off.
+ *                     "force_mid_radius" / "force_mid_bound"
  *   "force_far_exp":  block pairs in spatial order: tile pairs >= r_far apart evaluate their pairs
  *                     within 3e-9 relative (rsq + one Newton step, degree-6 2^f), r_far the
  *                     smallest radius with (N - 1) g(r_far) 3e-9 <= 10^-k: every ion's force

@@ -866,6 +866,7 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
     if (t == 0) jm = 0u;
     __syncthreads();
     uint2 w = make_uint2(1u, 0xFFu);                // class -1 where the block kernel never looks
+    double gi[4] = {0., 0., 0., 0.}, gj[4] = {0., 0., 0., 0.};   // this tile pair's tail terms per sub-tile
     const bool half = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
     if (!half && I < a.T && J < a.T && (db > 0 || J >= I)) {
         const N3BRadii rad = n3b_radii<VARIANT, false>(a);
@@ -902,14 +903,27 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
                         const bool drop = cls == -2 || !((groups >> ((sb - sa) & 3)) & 1u);
                         if (drop && sg[sa][sb] < rcut2) {
                             const double gd = tail_g(sg[sa][sb], invl, cf);
-                            atomicAdd(&ti[q][sa], sub_count(a.N, 4 * J + sb) * gd);
-                            atomicAdd(&tj[b][sb], sub_count(a.N, 4 * I + sa) * gd);
+                            gi[sa] += sub_count(a.N, 4 * J + sb) * gd;
+                            gj[sb] += sub_count(a.N, 4 * I + sa) * gd;
                         }
                     }
             }
         }
     }
     plan[((size_t)Pl * a.nd + db) * (BW * BW) + t] = w;
+    if (tmeas) {
+        // the workgroup's sums per sub-tile: I sub-tiles over b (lanes q, q + 16, q + 32, q + 48 of
+        // each wave, then one LDS add per wave), J sub-tiles over q (16 consecutive lanes: b's own)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            double vi = gi[u], vj = gj[u];
+            vi += __shfl_xor(vi, 16); vi += __shfl_xor(vi, 32);
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) vj += __shfl_xor(vj, off);
+            if ((t & 63) < 16 && vi > 0.) atomicAdd(&ti[q][u], vi);
+            if (q == 0) tj[b][u] = vj;              // (one writer per b)
+        }
+    }
     // the J-step mask of (P, db): J step b has work iff one of its tile pairs has a class >= 0
     // (threads 16 b .. 16 b + 15 are lanes 16 (b & 3) .. of wave b >> 2)
     const unsigned long long wk = __ballot((int)(w.x & 15u) >= 2);

@@ -644,7 +644,7 @@ static void choose_segments(mdqt_ctx* s) {
     memset(&b, 0, sizeof b);
     if (s->use_n3b) {
         b.N = N; b.T = nt; b.Npad = nt * 64;
-        b.NB = (nt + 15) / 16;
+        b.NB = (nt + kN3BBlock - 1) / kN3BBlock;
         b.nd = b.NB / 2 + 1;
         b.Plo = (int)((long)s->p.rank * b.NB / W);
         b.Phi = (int)((long)(s->p.rank + 1) * b.NB / W);
@@ -1408,7 +1408,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
         a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes; a.subboxes = s->dSubBoxes;
         if (tail_measured(s) && a.Rskip < a.Rcut) a.tailb = s->dTail;
         // the plan (k_n3b_plan): 256 tile-pair words per (P, db), then one J-step mask per (P, db)
-        const size_t need = (size_t)std::max(a.Phi - a.Plo, 0) * a.nd * 257;
+        const size_t need = (size_t)std::max(a.Phi - a.Plo, 0) * a.nd * (kN3BBlock * kN3BBlock + 1);
         if (need > s->capPlan) {
             if (s->dPlan) HIPCHK(hipFree(s->dPlan));
             s->dPlan = nullptr;

@@ -155,8 +155,8 @@ extern "C" int mdqt_expt_n3_stamps(unsigned long long* out, int n) {
 #endif
 
 // ------------------------------------------------------------------------------------------
-// Newton-3 over BLOCK pairs (large N, one GPU or sharded): blocks of 16 tiles (1024 ions); a
-// workgroup of 16 waves holds block P (wave q: tile I = 16P + q in registers) and walks the
+// Newton-3 over BLOCK pairs (large N, one GPU or sharded): blocks of BW tiles (kN3BBlock: 8, 512
+// ions; 16 until round 4); a workgroup of BW waves holds block P (wave q: tile I = BW P + q in registers) and walks the
 // block distances db of its run, db in [0, NB/2] of the cyclic half shell (block Q = P + db mod
 // NB; db = NB/2 only from P < NB/2 when NB is even; db = 0: tile pairs I <= J).  For every J
 // tile of Q all 16 waves run their (I, J) rotation (64 steps; 32 on the diagonal tile) against
@@ -166,7 +166,7 @@ extern "C" int mdqt_expt_n3_stamps(unsigned long long* out, int n) {
 // The canonical per-ion sum (k_n3b_reduce) takes the j-slots in db order, then the i-slots in
 // run order, skipping slots this rank does not write.
 // ------------------------------------------------------------------------------------------
-constexpr int BW = 16;                              // tiles per block = waves per workgroup
+constexpr int BW = kN3BBlock;                       // tiles per block = waves per workgroup
 #if defined(MDQT_EXPT_CLS)
 // diagnostic build only: tile-pair classes of k_pairs_n3b (skip, per pair, uniform image)
 __device__ unsigned long long g_cls_count[3];
@@ -431,13 +431,18 @@ __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0
 
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
 template <int VARIANT, bool GUARD, bool POT = false>
-// the fast variant fits 64 VGPRs (8 waves per SIMD); the exact one (libm exp, divisions) gets 128
-__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(VARIANT == 1 ? 8 : 4, VARIANT == 1 ? 8 : 4)))
+// the fast variant fits 80 VGPRs (6 waves per SIMD: three 8-wave workgroups per CU); the exact one (libm exp, divisions) gets 128
+#ifndef MDQT_N3B_IRUN_LDS
+#define MDQT_N3B_IRUN_LDS 1                         // the run's i accumulator in LDS (0: in the i-slot itself)
+#endif
+#ifndef MDQT_N3B_WPE                                // waves per SIMD of the fast variant (VGPR budget 512/WPE):
+#define MDQT_N3B_WPE (BW == 8 ? 6 : 8)              // 6 = three 8-wave workgroups per CU (41.5 KB LDS each)
+#endif
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(VARIANT == 1 ? MDQT_N3B_WPE : 4, VARIANT == 1 ? MDQT_N3B_WPE : 4)))
 void k_pairs_n3b(N3BArgs a) {
     __shared__ double pj[3][128];
     __shared__ double mj[128];
     __shared__ double accj[BW][3][128];
-    __shared__ double irun[BW][3][64];
     __shared__ double etab[64];
     stage_exp_tab(etab);
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;   // q: wave-uniform
@@ -491,10 +496,18 @@ void k_pairs_n3b(N3BArgs a) {
     auto sgpr_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
     const float cf32 = sgpr_f((float)(a.invlDeb * kNegLog2e)), invl32 = sgpr_f((float)a.invlDeb),
                 rc2f = sgpr_f((float)a.rc2);
-    // the run's i accumulator lives in LDS (read and written once per block distance) so that
-    // the three-level blocking fits the 64-VGPR budget of two 16-wave workgroups per CU
-    double* fi = irun[q][0];
-    fi[l] = 0.; fi[64 + l] = 0.; fi[128 + l] = 0.;
+    // the run's i accumulator: in LDS (read and written once per block distance, so that the
+    // three-level blocking fits the 64-VGPR budget), or (MDQT_N3B_IRUN_LDS 0) the i-slot itself —
+    // each wave's own rows, read, added and written once per block distance, in order
+#if MDQT_N3B_IRUN_LDS
+    __shared__ double irun[BW][3][64];
+    double* fi = irun[q][0] + l;
+    constexpr size_t FS = 64;
+#else
+    double* fi = a.slots + (size_t)(a.nd + run) * ((size_t)3 * a.Npad) + i;
+    const size_t FS = a.Npad;
+#endif
+    bool fi_first = true;
     const uint2* plan = POT ? nullptr : a.plan;
     // every J step: the staging wave (the last; not one of the combining waves 0..2) loads J, one
     // barrier, the pair work, one barrier, then waves 0..2 combine the 16 j accumulators of one
@@ -642,11 +655,17 @@ void k_pairs_n3b(N3BArgs a) {
                 a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? s16[0] : -s16[0];
             }
         }
-        fi[l] += bx; fi[64 + l] += by; fi[128 + l] += bz;   // one wave's own LDS words: in order
+        if (vI) {                                   // (0 + bx: the first block distance's partial as is)
+            fi[0] = fi_first ? 0. + bx : fi[0] + bx;
+            fi[FS] = fi_first ? 0. + by : fi[FS] + by;
+            fi[2 * FS] = fi_first ? 0. + bz : fi[2 * FS] + bz;
+        }
+        fi_first = false;
     }
     if (vI) {                                       // i side -> i-slot nd + run
         double* o = a.slots + (size_t)(a.nd + run) * plane + i;
-        o[0] = fi[l]; o[a.Npad] = fi[64 + l]; o[2 * (size_t)a.Npad] = fi[128 + l];
+        const double r0 = fi_first ? 0. : fi[0], r1 = fi_first ? 0. : fi[FS], r2 = fi_first ? 0. : fi[2 * FS];
+        if (MDQT_N3B_IRUN_LDS || fi_first) { o[0] = r0; o[a.Npad] = r1; o[2 * (size_t)a.Npad] = r2; }
     }
 }
 
@@ -862,7 +881,7 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
     const int P = a.Plo + Pl, Q = (P + db) % a.NB;
     const int I = P * BW + q, J = Q * BW + b;
     const bool tmeas = a.tailb != nullptr;
-    if (tmeas && t < 64) { ti[t >> 2][t & 3] = 0.; tj[t >> 2][t & 3] = 0.; }
+    if (tmeas && t < 4 * BW) { ti[t >> 2][t & 3] = 0.; tj[t >> 2][t & 3] = 0.; }
     if (t == 0) jm = 0u;
     __syncthreads();
     uint2 w = make_uint2(1u, 0xFFu);                // class -1 where the block kernel never looks
@@ -917,26 +936,28 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             double vi = gi[u], vj = gj[u];
-            vi += __shfl_xor(vi, 16); vi += __shfl_xor(vi, 32);
 #pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) vj += __shfl_xor(vj, off);
-            if ((t & 63) < 16 && vi > 0.) atomicAdd(&ti[q][u], vi);
+            for (int off = BW; off < 64; off <<= 1) vi += __shfl_xor(vi, off);
+#pragma unroll
+            for (int off = BW / 2; off >= 1; off >>= 1) vj += __shfl_xor(vj, off);
+            if ((t & 63) < BW && vi > 0.) atomicAdd(&ti[q][u], vi);
             if (q == 0) tj[b][u] = vj;              // (one writer per b)
         }
     }
     // the J-step mask of (P, db): J step b has work iff one of its tile pairs has a class >= 0
-    // (threads 16 b .. 16 b + 15 are lanes 16 (b & 3) .. of wave b >> 2)
+    // (threads BW b .. BW b + BW - 1 are lanes BW (b mod 64/BW) .. of wave b / (64/BW))
     const unsigned long long wk = __ballot((int)(w.x & 15u) >= 2);
     if ((t & 63) == 0) {
-        unsigned m4 = 0u;
+        constexpr int per = 64 / BW;
+        unsigned mw = 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) m4 |= ((wk >> (16 * k)) & 0xFFFFull) ? 1u << k : 0u;
-        atomicOr(&jm, m4 << (4 * (t >> 6)));
+        for (int k = 0; k < per; ++k) mw |= ((wk >> (BW * k)) & ((1ull << BW) - 1)) ? 1u << k : 0u;
+        atomicOr(&jm, mw << (per * (t >> 6)));
     }
     __syncthreads();
     if (t == 0) plan[(size_t)(a.Phi - a.Plo) * a.nd * (BW * BW) + (size_t)Pl * a.nd + db] = make_uint2(jm, 0u);
     if (tmeas) {
-        if (t < 64) {
+        if (t < 4 * BW) {
             const int k = t >> 2, u = t & 3;
             if (ti[k][u] > 0.) atomicAdd(a.tailb + 4 * (P * BW + k) + u, ti[k][u]);
             if (tj[k][u] > 0.) atomicAdd(a.tailb + 4 * (Q * BW + k) + u, tj[k][u]);
@@ -1053,11 +1074,11 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     if (a.plan && nplan > 0) {
         if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // spatial order only
         if (variant == 1) {
-            if (a.guard) hipLaunchKernelGGL((k_n3b_plan<1, true>), dim3(nplan), dim3(256), 0, s, a, a.plan);
-            else hipLaunchKernelGGL((k_n3b_plan<1, false>), dim3(nplan), dim3(256), 0, s, a, a.plan);
+            if (a.guard) hipLaunchKernelGGL((k_n3b_plan<1, true>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
+            else hipLaunchKernelGGL((k_n3b_plan<1, false>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
         } else {
-            if (a.guard) hipLaunchKernelGGL((k_n3b_plan<0, true>), dim3(nplan), dim3(256), 0, s, a, a.plan);
-            else hipLaunchKernelGGL((k_n3b_plan<0, false>), dim3(nplan), dim3(256), 0, s, a, a.plan);
+            if (a.guard) hipLaunchKernelGGL((k_n3b_plan<0, true>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
+            else hipLaunchKernelGGL((k_n3b_plan<0, false>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
         }
     } else if (a.tailb) {
         return hipErrorInvalidValue;                // the tail sums come from the plan
@@ -1093,7 +1114,7 @@ hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStrea
     if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // the classes need the boxes
     const int nblk = (a.Phi - a.Plo) * a.nd;
     if (hipMemsetAsync(out, 0, 2 * kCensus * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
-    if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(256), 0, s, a, out);
+    if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out);
     return hipGetLastError();
 }
 

@@ -468,6 +468,13 @@ hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const
                            hipStream_t s);
 // census of k_pairs_n3b's work by tile-pair class (mdqt_forces.hip k_n3b_census): out[2 kCensus]
 constexpr int kCensus = 14;
+// tiles per block of the Newton-3 block kernel (= its waves per workgroup): 8 (round 4, A/B vs 16:
+// C3 -2.7 %, C5 -2.5 %, N = 1M -4.3 % per force call — three 8-wave workgroups per CU at 80 VGPRs
+// instead of two 16-wave ones at 64: shorter J-step barriers, fewer spills; 4: slower)
+#ifndef MDQT_N3B_BW
+#define MDQT_N3B_BW 8
+#endif
+constexpr int kN3BBlock = MDQT_N3B_BW;
 hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 

@@ -8,8 +8,7 @@ the oracle on sampled ions (the full O(N^2) oracle is hours at N = 1e6).
 
 Per config:
   * forces() on the reference's init() state (C5: after 20 MD steps, so that the interval below
-    has quantum jumps): GPU F of ~1,000 sampled ions (one per 1,024-ion
-    block, the ragged last tile, both sides of the NB/2 half-shell boundary, random others) against
+    has quantum jumps): GPU F of ~1,000 sampled ions (one per 1,024 ions, the ragged last tile, both sides of the NB/2 half-shell boundary, random others) against
     the oracle's rows over all j (orc_forces_index: the reference's pair terms, compensated sum so
     that the check sees the GPU's rounding, not N eps of the oracle's own);
     gate: max |dF| <= 1e-12 x max |F| over the sample (stated tolerance: the GPU sums N/2 terms per
@@ -41,15 +40,19 @@ def threads():
     return max(1, min(16, os.cpu_count() or 1))
 
 
+BLOCK = 512                                         # ions per block of the block kernel (8 tiles)
+
+
 def sample_ions(N, nsamp, rng):
-    """one ion per 1,024-ion block, the ragged last tile, the blocks around NB/2, random others"""
-    NB = (N + 1023) // 1024
-    idx = [b * 1024 + int(rng.integers(0, min(1024, N - b * 1024))) for b in range(NB)]
+    """one ion per 1,024 ions (every other block), the ragged last tile, the blocks around NB/2,
+    random others"""
+    NB = (N + BLOCK - 1) // BLOCK
+    idx = [b * 1024 + int(rng.integers(0, min(1024, N - b * 1024))) for b in range((N + 1023) // 1024)]
     idx += list(range(max(0, N - 64), N))                          # ragged last tile
     for b in (NB // 2 - 1, NB // 2, NB // 2 + 1, NB - 1, 0):       # half-shell boundary blocks
         if 0 <= b < NB:
-            lo = b * 1024
-            idx += list(range(lo, min(N, lo + 8))) + list(range(max(lo, min(N, lo + 1024) - 8), min(N, lo + 1024)))
+            lo = b * BLOCK
+            idx += list(range(lo, min(N, lo + 8))) + list(range(max(lo, min(N, lo + BLOCK) - 8), min(N, lo + BLOCK)))
     rest = nsamp - len(set(idx))
     if rest > 0:
         idx += list(rng.integers(0, N, rest))
@@ -94,7 +97,7 @@ def test_large_config_forces_and_interval(cfg, orc):
     # and the far pair form (force_far_exp, default 13): <= far bound more
     rt, bound = s.const("force_skip_radius"), s.const("force_tail_bound")
     rf, fbound = s.const("force_far_radius"), s.const("force_far_bound")
-    print(f"{cfg}: N={N} NB={(N + 1023) // 1024} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}, "
+    print(f"{cfg}: N={N} NB={(N + BLOCK - 1) // BLOCK} N%64={N % 64} sampled {len(idx)}: max|dF|/max|F| = {err:.3e}, "
           f"max|dF| = {dabs:.3e}; skip radius {rt:.3f} (L/2 {L / 2:.3f}), tail bound {bound:.2e}; "
           f"far radius {rf:.3f}, far bound {fbound:.2e}")
     vbound = s.const("force_vfar_bound") + s.const("force_ufar_bound") + s.const("force_mid_bound")

@@ -26,7 +26,7 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def n3b_plan(N, world, rank, BW=16, target=4096):
+def n3b_plan(N, world, rank, BW=8, target=16384):
     """mdqt_engine.cpp:choose_segments (Newton-3 blocks): tiles, blocks, half-shell distances,
     this rank's blocks, runs of distances per block"""
     T = (N + 63) // 64
@@ -41,7 +41,7 @@ def n3b_plan(N, world, rank, BW=16, target=4096):
     return dict(T=T, NB=NB, nd=nd, Plo=Plo, Phi=Phi, R=R, runlen=runlen, BW=BW)
 
 
-def n3b_tile_pairs(N, world, rank, BW=16):
+def n3b_tile_pairs(N, world, rank, BW=8):
     """(I, J, diag) of every tile pair rank `rank` evaluates: mdqt_forces.hip:k_pairs_n3b's loops
     over workgroups (block P, run), distances db of the run, J tiles of block Q = P + db, waves I"""
     p = n3b_plan(N, world, rank, BW)

@@ -649,10 +649,11 @@ static void choose_segments(mdqt_ctx* s) {
         b.Plo = (int)((long)s->p.rank * b.NB / W);
         b.Phi = (int)((long)(s->p.rank + 1) * b.NB / W);
         const int nblk = std::max(b.Phi - b.Plo, 1);
-        // ~4096 workgroups per rank (8 rounds of 2 per CU): short tail
+        // up to 65,536 workgroups per rank (runs of one or a few block distances, dispatched run-major:
+        // a short last round; A/B with 8-tile blocks: N = 1M -1.2 % vs 16,384, C3 and C5 flat)
         static const int wg_target = [] {           // (A/B experiments: MDQT_N3B_WG workgroups per rank)
             const char* e = getenv("MDQT_N3B_WG");
-            return e && atoi(e) > 0 ? atoi(e) : 16384;
+            return e && atoi(e) > 0 ? atoi(e) : 65536;
         }();
         int R = std::min(b.nd, (wg_target + nblk - 1) / nblk);
         b.runlen = (b.nd + R - 1) / R;

@@ -26,7 +26,7 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def n3b_plan(N, world, rank, BW=8, target=16384):
+def n3b_plan(N, world, rank, BW=8, target=65536):
     """mdqt_engine.cpp:choose_segments (Newton-3 blocks): tiles, blocks, half-shell distances,
     this rank's blocks, runs of distances per block"""
     T = (N + 63) // 64

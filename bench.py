@@ -756,7 +756,11 @@ def end_to_end_line(local, cfg, md_steps):
             "value": b["N"] * dq / el, "unit": "particle-qsteps/s"}
 
 
-N3B_KERNEL = "void mdqt::k_pairs_n3b<1, false, false>(mdqt::N3BArgs)"   # the large-N dominant kernel
+# the large-N dominant kernel: its plain instance, or (C3, C5: the skip radius reaches the image
+# boundary) the one with the one-axis per-pair image (mdqt_forces.hip launch_forces_n3b)
+N3B_KERNELS = ("void mdqt::k_pairs_n3b<1, false, false, false>(mdqt::N3BArgs)",
+               "void mdqt::k_pairs_n3b<1, false, false, true>(mdqt::N3BArgs)")
+N3B_KERNEL = N3B_KERNELS[0]
 
 
 def latest_large_pmc(cfg):
@@ -794,7 +798,10 @@ def large_roofline(cfg, census, f_avg, N, world):
     meta = d.get("_meta", {})
     p = {"file": os.path.relpath(path, ROOT), "measured_src_hash": meta.get("src_hash"),
          "src_hash": kernel_source_hash(), "workload": meta.get("workload")}
-    e = d.get(N3B_KERNEL)
+    # the instance this config ran (the one the summary has dispatches of)
+    kname = max(N3B_KERNELS, key=lambda k: (d.get(k) or {}).get("dispatches", 0))
+    e = d.get(kname)
+    roof["kernel"] = kname
     if meta.get("src_hash") != p["src_hash"] or not e:
         roof["pmc"] = dict(p, status="stale: measured on other kernel sources" if e else "kernel not in the summary")
         return roof

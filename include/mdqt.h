@@ -194,6 +194,12 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     boxes are >= the skip radius apart (default), 2 = the same order, nothing
  *                     skipped (bit-identical to 1 where the skip radius is L/2 — every BASELINE size
  *                     but N ~ 1e6, where 1 also skips the error-bounded tail), 0 = storage order
+ *   "force_ax1":      block pairs in spatial order: 1 (default) = a tile pair whose minimum image
+ *                     varies on one axis only takes the image per pair on that axis alone (the
+ *                     other two shifted once per tile pair, as a uniform-image tile pair) — a
+ *                     kernel instance of its own, launched where the skip radius reaches within
+ *                     two tile widths of L/2 (C3, C5); 0 = the per-pair image on all three axes.
+ *                     Forces agree to rounding (1e-13 of max |F|)
  *   "force_tail_exp": block pairs in spatial order: tile pairs whose boxes are >= r_t apart are
  *                     skipped with every ion's force kept within eps = 10^-k of the exact sum to
  *                     L/2 (g(r) = one pair's |F| at distance r, SpeedUp:224); k = 12 default, 0 =

@@ -112,6 +112,7 @@ struct mdqt_ctx {
     double* dFr = nullptr;         // sharded n3b: this rank's dense partial forces [world][3][S]
     // spatial order of the n3b scheme (mdqt_sort.hip; option "force_sort", default on)
     int sort_mode = 1;             // 0 off, 1 sorted + tile-pair skipping, 2 sorted, nothing skipped (tests)
+    int ax1_mode = 1;              // option "force_ax1": the one-axis per-pair image instance (1, auto) or not (0)
     // error-bounded force tail (option "force_tail_exp" k: eps = 10^-k, 0 = off): tile pairs whose
     // boxes are >= r_t apart are skipped, r_t the smallest radius with (N - 1) g(r_t) <= eps,
     // g(r) = (1/r + 1/lDeb) e^(-r/lDeb) / r the pair force magnitude (SpeedUp:224) — so no ion's
@@ -912,6 +913,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_segments")) return s->nseg;
     if (!strcmp(n, "force_scheme")) return s->use_n3b ? 3 : s->use_n3 ? 2 : 1;
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
+    if (!strcmp(n, "force_ax1")) return s->ax1_mode;
     if (!strcmp(n, "force_skip_radius") || !strcmp(n, "force_tail_bound")) {   // the tile-pair skip radius
         double bound;                                  // and its force bound (0: exact, r = L/2)
         const double r = (s->use_n3b && s->sort_mode == 1) ? skip_radius(s, &bound) : (bound = 0., s->L / 2.);
@@ -1387,6 +1389,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
     a.micGuard = c.micGuard; a.guard = c.guard;
     a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr; a.subboxes = nullptr; a.plan = nullptr;
+    a.ax1 = s->ax1_mode;
     double bound;
     a.Rskip = skip_radius(s, &bound);
     a.tailb = nullptr;
@@ -2741,6 +2744,12 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (value < 0 || value > 1) return fail("force_tail_mode must be 0 (a priori) or 1 (measured)");
         if (value != s->tail_mode && tail_reset(s)) return -1;
         s->tail_mode = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_ax1")) {                  // Newton-3 blocks: the one-axis per-pair image instance
+        if (value < 0 || value > 1) return fail("force_ax1 must be 0 (off) or 1 (where the skip radius reaches L/2)");
+        if (settle_forces(s)) return -1;
+        s->ax1_mode = value;
         return 0;
     }
     if (!strcmp(name, "force_sort")) {                 // Newton-3 blocks: Hilbert order + tile-pair skipping

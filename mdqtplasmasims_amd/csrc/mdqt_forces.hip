@@ -15,6 +15,7 @@
 #include "mdqt_pairs.hpp"
 
 #include <math.h>
+#include <type_traits>
 
 namespace mdqt {
 
@@ -167,6 +168,12 @@ extern "C" int mdqt_expt_n3_stamps(unsigned long long* out, int n) {
 // run order, skipping slots this rank does not write.
 // ------------------------------------------------------------------------------------------
 constexpr int BW = kN3BBlock;                       // tiles per block = waves per workgroup
+#ifndef MDQT_N3B_AX1
+#define MDQT_N3B_AX1 1                              // the one-axis per-pair image (n3b_pack_class); 0: all three axes
+#endif
+#ifndef MDQT_N3B_AX1_LEVELS
+#define MDQT_N3B_AX1_LEVELS 0xE                     // bit x: far level x takes it (1 mid, 2 far, 3 very/ultra far)
+#endif
 #if defined(MDQT_EXPT_CLS)
 // diagnostic build only: tile-pair classes of k_pairs_n3b (skip, per pair, uniform image)
 __device__ unsigned long long g_cls_count[3];
@@ -218,7 +225,7 @@ __device__ __forceinline__ int n3b_lds(int l) { return 32 * (l >> 4) + (l & 15);
 
 // one sub-tile group: 16 rotation steps from LDS index b0 (the lane's first J ion) with weight w
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
-          bool POT = false, int FAR = 0, int NSTEP = 16>
+          bool POT = false, int FAR = 0, int NSTEP = 16, int MAX = -1>
 __device__ __forceinline__ void n3b_group(int b0, double w, double xi, double yi, double zi, double mi,
                                           const double (*pj)[128], const double* mj, double* ax, double* ay,
                                           double* az, double& fx, double& fy, double& fz, const PairC& c,
@@ -226,14 +233,14 @@ __device__ __forceinline__ void n3b_group(int b0, double w, double xi, double yi
     N3B_REBASE(b0);
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t)
-        n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(t, t == NSTEP - 1 ? w * w_last : w, xi, yi, zi, mi, pjb,
-                                                              mjb, axb, ayb, azb, fx, fy, fz, c, nsh);
+        n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX>(t, t == NSTEP - 1 ? w * w_last : w, xi, yi, zi, mi,
+                                                                   pjb, mjb, axb, ayb, azb, fx, fy, fz, c, nsh);
 }
 
 // a whole tile pair in one pair form: the groups of `groups` (off the diagonal) or the diagonal
 // tile's three groups
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = VARIANT == 1 && MDQT_N3_CUT,
-          bool POT = false, int FAR = 0>
+          bool POT = false, int FAR = 0, int MAX = -1>
 __device__ __forceinline__ void n3b_pair(bool diag, unsigned groups, int l, double xi, double yi, double zi,
                                          double mi, const double (*pj)[128], const double* mj, double* ax,
                                          double* ay, double* az, double& fx, double& fy, double& fz,
@@ -242,10 +249,10 @@ __device__ __forceinline__ void n3b_pair(bool diag, unsigned groups, int l, doub
     if (!diag) {
         for (int d = 0; d < 4; ++d) {
             if (!((groups >> d) & 1u)) continue;    // wave-uniform
-            n3b_group<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(32 * ((a + d) & 3) + m, 1., xi, yi, zi, mi, pj, mj,
-                                                                    ax, ay, az, fx, fy, fz, c, nsh);
+            n3b_group<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, 16, MAX>(32 * ((a + d) & 3) + m, 1., xi, yi, zi, mi, pj,
+                                                                             mj, ax, ay, az, fx, fy, fz, c, nsh);
         }
-    } else {
+    } else if constexpr (MAX < 0) {                 // (a tile with itself has one image)
         // sub-tile distance 1..8 inside each sub-tile, the 8th once (m < 8)
         n3b_group<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, 8>(32 * a + m + 1, 1., xi, yi, zi, mi, pj, mj, ax, ay, az,
                                                                    fx, fy, fz, c, nsh, m >= 8 ? 0. : 1.);
@@ -335,13 +342,15 @@ __device__ __forceinline__ N3BRadii n3b_radii(const N3BArgs& a) {
 __device__ __forceinline__ int n3b_level(double g2, const N3BRadii& r) {
     return g2 > r.ru32 ? 5 : g2 > r.ru2 ? 4 : g2 > r.rv2 ? 3 : g2 > r.rf2 ? 2 : g2 > r.rm2 ? 1 : 0;
 }
+// strad (when asked): bit c = axis c's minimum-image multiple varies over the tile pair's pairs
 template <bool FAST>
 __device__ __forceinline__ double4 n3b_classify(const N3BArgs& a, double invL, const N3BRadii& r, int Iw, int J,
-                                                double& g2) {
+                                                double& g2, int* strad = nullptr) {
     const double* B = a.boxes;
     const int T = a.T;
     g2 = 0.;
     bool uni = true;
+    int sm = 0;
     double n[3];
 #pragma unroll
     for (int c3 = 0; c3 < 3; ++c3) {
@@ -353,8 +362,10 @@ __device__ __forceinline__ double4 n3b_classify(const N3BArgs& a, double invL, c
         const double hi = B[(size_t)(9 + c3) * T + Iw] - B[(size_t)(6 + c3) * T + J];
         const double nlo = __builtin_rint(lo * invL), nhi = __builtin_rint(hi * invL);
         uni = uni && (nlo == nhi);
+        sm |= (nlo == nhi ? 0 : 1) << c3;
         n[c3] = nlo;
     }
+    if (strad) *strad = sm;
     const double cls = (a.use_sort == 1 && g2 > r.rc2) ? (g2 < a.Rcut * a.Rcut ? -2. : -1.)
                                                         : ((FAST && uni) ? 1. : 0.) +
                                                               2. * n3b_level(g2, r);
@@ -416,21 +427,27 @@ __device__ __forceinline__ double tail_g(double g2, float invl, float cf) {
 }
 // a tile pair's class and uniform-image multiples in one LDS word: bits 0-3 class + 2, 4-11 / 12-19 /
 // 20-27 n_x, n_y, n_z (signed); a uniform image with a multiple beyond +-127 (positions that far
-// outside the box) is taken per pair instead
-__device__ __forceinline__ int n3b_pack_class(double4 t4) {
+// outside the box) is taken per pair instead.  A per-pair image that varies on ONE axis only (strad:
+// n3b_classify's mask; FAST) carries that axis + 1 in bits 28-29 and the other two axes' multiples
+// (the varying axis's field 0): the block kernel then takes the minimum image per pair on that axis
+// alone (the tile pairs that straddle the image boundary, ~97 % of the per-pair-image ones, C3/C5)
+__device__ __forceinline__ int n3b_pack_class(double4 t4, int strad = 0) {
     int cls = (int)t4.w;
     const bool uni = cls >= 0 && (cls & 1);
     if (uni && !(fabs(t4.x) <= 127. && fabs(t4.y) <= 127. && fabs(t4.z) <= 127.)) cls -= 1;
     const bool u2 = cls >= 0 && (cls & 1);
-    const int nx = u2 ? (int)t4.x : 0, ny = u2 ? (int)t4.y : 0, nz = u2 ? (int)t4.z : 0;
-    return (cls + 2) | ((nx & 255) << 4) | ((ny & 255) << 12) | ((nz & 255) << 20);
+    const int ax1 = strad == 1 ? 1 : strad == 2 ? 2 : strad == 4 ? 3 : 0;
+    const bool one = MDQT_N3B_AX1 && cls >= 0 && !(cls & 1) && ax1 &&
+                     fabs(t4.x) <= 127. && fabs(t4.y) <= 127. && fabs(t4.z) <= 127.;
+    const int nx = (u2 || (one && ax1 != 1)) ? (int)t4.x : 0, ny = (u2 || (one && ax1 != 2)) ? (int)t4.y : 0,
+              nz = (u2 || (one && ax1 != 3)) ? (int)t4.z : 0;
+    return (cls + 2) | ((nx & 255) << 4) | ((ny & 255) << 12) | ((nz & 255) << 20) | ((one ? ax1 : 0) << 28);
 }
 // real ions of 16-ion sub-tile s (0 for the padding of the ragged last tile)
 __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0, min(16, N - 16 * s)); }
 
 
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
-template <int VARIANT, bool GUARD, bool POT = false>
 // the fast variant fits 80 VGPRs (6 waves per SIMD: three 8-wave workgroups per CU); the exact one (libm exp, divisions) gets 128
 #ifndef MDQT_N3B_IRUN_LDS
 #define MDQT_N3B_IRUN_LDS 1                         // the run's i accumulator in LDS (0: in the i-slot itself)
@@ -438,6 +455,10 @@ template <int VARIANT, bool GUARD, bool POT = false>
 #ifndef MDQT_N3B_WPE                                // waves per SIMD of the fast variant (VGPR budget 512/WPE):
 #define MDQT_N3B_WPE (BW == 8 ? 6 : 8)              // 6 = three 8-wave workgroups per CU (41.5 KB LDS each)
 #endif
+// AXP: the one-axis per-pair image (n3b_pack_class bits 28-29) in an instance of its own, launched
+// only where such tile pairs can lie inside the skip radius (launch_forces_n3b): compiled into the
+// one instance it cost the calls without any (N = 1M) 0.5 %.
+template <int VARIANT, bool GUARD, bool POT = false, bool AXP = false>
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(VARIANT == 1 ? MDQT_N3B_WPE : 4, VARIANT == 1 ? MDQT_N3B_WPE : 4)))
 void k_pairs_n3b(N3BArgs a) {
     __shared__ double pj[3][128];
@@ -556,7 +577,9 @@ void k_pairs_n3b(N3BArgs a) {
                         int w = 2;                  // class 0 (unsorted: every tile pair, per-pair image)
                         if (srt && P * BW + l < T) {
                             double g2;
-                            w = n3b_pack_class(n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2));
+                            int sm = 0;
+                            w = n3b_pack_class(n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2,
+                                                                          AXP ? &sm : nullptr), sm);
                         }
                         tpw[l] = w;
                         tg[l] = 0xFFu;
@@ -615,9 +638,47 @@ void k_pairs_n3b(N3BArgs a) {
                                                                                 ax, ay, az, tx, ty, tz, c, nsh);
                     }
                 } else if constexpr (FARF) {       // per-pair image
+                    const int ax1 = (tw >> 28) & 3;  // 1 + the one axis whose image varies (n3b_pack_class)
                     if (diag) {
                         n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(true, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
                                                                          az, tx, ty, tz, c);
+                    } else if (AXP && ax1) {        // one axis: the other two shifted once (xi - n L)
+                      if constexpr (AXP) {
+                        const double sx = fma(-(double)((tw << 20) >> 24), a.L, xi);   // (0 on the varying axis:
+                        const double sy = fma(-(double)((tw << 12) >> 24), a.L, yi);   //  fma(-0, L, x) = x)
+                        const double sz = fma(-(double)((tw << 4) >> 24), a.L, zi);
+                        const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
+                                       g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
+                        constexpr unsigned LV = MDQT_N3B_AX1_LEVELS;   // the levels that take it (bit x: level x)
+                        auto one_axis = [&](auto axc) {
+                            constexpr int AX = decltype(axc)::value;
+                            if ((LV & 8u) && g3)
+                                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3, AX>(false, g3, l, sx, sy, sz, mi, pj, mj,
+                                                                                        ax, ay, az, tx, ty, tz, c);
+                            if ((LV & 4u) && g2)
+                                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2, AX>(false, g2, l, sx, sy, sz, mi, pj, mj,
+                                                                                        ax, ay, az, tx, ty, tz, c);
+                            if ((LV & 2u) && MDQT_EXP_TAB && g1)
+                                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0, AX>(
+                                    false, g1, l, sx, sy, sz, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
+                        };
+                        if (ax1 == 1) one_axis(std::integral_constant<int, 0>{});
+                        else if (ax1 == 2) one_axis(std::integral_constant<int, 1>{});
+                        else one_axis(std::integral_constant<int, 2>{});
+                        // the other levels per pair (the exact level with a varying image: ~never, C3 1.6e-5
+                        // of the pairs)
+                        if (!(LV & 8u) && g3)
+                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3>(false, g3, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                                az, tx, ty, tz, c);
+                        if (!(LV & 4u) && g2)
+                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                                az, tx, ty, tz, c);
+                        if (!(LV & 2u) && MDQT_EXP_TAB && g1)
+                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(
+                                false, g1, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
+                        if (g0) n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(false, g0, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                                 ay, az, tx, ty, tz, c);
+                      }
                     } else {                        // (ultra far with a per-pair image: rare, very-far form)
                         const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
                                        g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
@@ -668,6 +729,7 @@ void k_pairs_n3b(N3BArgs a) {
         if (MDQT_N3B_IRUN_LDS || fi_first) { o[0] = r0; o[a.Npad] = r1; o[2 * (size_t)a.Npad] = r2; }
     }
 }
+
 
 // force_tail_mode 1, after the call's per-sub-tile tail sums are complete (all-reduced over the
 // ranks when sharded): every tile with a sub-tile sum that, with the sum's rounding (x (1 + 1e-12)),
@@ -891,7 +953,8 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
         const N3BRadii rad = n3b_radii<VARIANT, false>(a);
         const double invL = 1. / a.L;
         double g2;
-        const int pw = n3b_pack_class(n3b_classify<VARIANT == 1>(a, invL, rad, I, J, g2));
+        int sm;
+        const int pw = n3b_pack_class(n3b_classify<VARIANT == 1>(a, invL, rad, I, J, g2, &sm), VARIANT == 1 ? sm : 0);
         const int cls = (pw & 15) - 2;
         w.x = (unsigned)pw;
         if ((db > 0 || J > I) && (cls >= 0 || (tmeas && cls == -2))) {
@@ -1085,7 +1148,14 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     }
     if (nblk > 0) {
         if (variant == 1) {
+            // the AXP instance where tile pairs whose image varies on one axis can be evaluated: their
+            // pairs are >= L/2 - (the two tiles' extents) apart on that axis, so only when the skip
+            // radius reaches within two tile widths (L (64/N)^(1/3)) of L/2 (C3, C5: r_s = L/2; not
+            // N = 1M, r_s = 61 < 80.6 - 12.9).  A function of the call's parameters alone: every rank
+            // of a sharded run, and every call of one configuration, takes the same kernel.
+            const bool axp = a.ax1 && a.use_sort != 0 && a.Rskip > 0.5 * a.L - 2. * a.L * cbrt(64. / a.N);
             if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<1, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            else if (axp) hipLaunchKernelGGL((k_pairs_n3b<1, false, false, MDQT_N3B_AX1 != 0>), dim3(nblk), dim3(BW * 64), 0, s, a);
             else hipLaunchKernelGGL((k_pairs_n3b<1, false>), dim3(nblk), dim3(BW * 64), 0, s, a);
         } else {
             if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<0, true>), dim3(nblk), dim3(BW * 64), 0, s, a);

@@ -240,8 +240,11 @@ __device__ __forceinline__ void accum(double& f, double d, double ft) {
 // to the j accumulator ax only (both sides of a pair get +u)
 // the pair terms of one rotation step: the lane's i ion against the J-tile ion at LDS index idx —
 // the force components (px, py, pz) to the i accumulator; returns them for the j side (POT: u in px)
+// MAX >= 0 (Newton-3 blocks, a tile pair whose image varies on one axis only): the caller passes the
+// i position shifted on the other two axes (as SHIFT), and the minimum image is taken per pair on axis
+// MAX alone — mic_r's operations on that axis, none on the others
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          int FAR = 0>
+          int FAR = 0, int MAX = -1>
 __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi, double zi, double mi,
                                          const double (*pj)[128], const double* mj, double& fx, double& fy,
                                          double& fz, const PairC& c, const double* nsh, double& px, double& py,
@@ -253,6 +256,10 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
             dy = fma(-nsh[1], c.L, dy);
             dz = fma(-nsh[2], c.L, dz);
         }
+    } else if constexpr (MAX >= 0) {
+        static_assert(VARIANT == 1 && MDQT_SHIFT_I && MAX < 3, "one-axis image: the fast variant, i shifted");
+        double& d = MAX == 0 ? dx : MAX == 1 ? dy : dz;
+        d = fma(-__builtin_rint(d * c.invL), c.L, d);
     } else {
         mic_v<VARIANT, GUARD>(dx, dy, dz, c);
     }
@@ -283,14 +290,14 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
 // (ds_add_f64 at index idx, no return; one wave's LDS operations run in order, so the
 // accumulation order is fixed)
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          int FAR = 0>
+          int FAR = 0, int MAX = -1>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
                                         const double (*pj)[128], const double* mj, double* ax, double* ay,
                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
                                         const double* nsh = nullptr) {
     double px, py, pz;
-    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh, px, py,
-                                                           pz);
+    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh, px,
+                                                                py, pz);
 #if defined(MDQT_EXPT_NOJACC)
     (void)ax; (void)ay; (void)az;
 #else

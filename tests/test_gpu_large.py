@@ -183,6 +183,28 @@ def test_spatial_order_tile_skipping_is_exact(orc):
 
 
 @pytest.mark.gpu
+def test_one_axis_image_instance_matches_per_pair_image():
+    """force_ax1 (mdqt_forces.hip n3b_pack_class, launch_forces_n3b): a tile pair whose minimum image
+    varies on one axis only takes the image per pair on that axis alone and the other two axes'
+    multiples once per tile pair, as a uniform-image tile pair does — the same pair terms (SpeedUp:
+    218-224), the shifted axes rounded as in the uniform-image tile pairs.  At C3 (skip radius L/2,
+    so the instance runs) against force_ax1 0 (every per-pair image on all three axes): within
+    rounding, 1e-13 of max |F|"""
+    import mdqtplasmasims_amd as M
+    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C3"]).init()
+    assert s.const("force_ax1") == 1 and s.const("force_skip_radius") == s.const("L") / 2
+    out = {}
+    for mode in (1, 0):
+        s.set_option("force_ax1", mode)
+        s.forces()
+        out[mode] = s.get_state()["F"]
+    err = np.abs(out[1] - out[0]).max() / np.abs(out[0]).max()
+    print(f"C3 one-axis image vs per-pair image on all axes: max|dF|/max|F| = {err:.3e}")
+    assert err <= 1e-13
+    s.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["C4", "C5"])
 def test_error_bounded_tail_and_far_form(cfg):
     """The error-bounded parts of the Newton-3 block forces against the exact sum to L/2 on EVERY

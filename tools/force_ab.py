@@ -4,6 +4,7 @@ variants; only API calls every round's library has): init(), one warm call, then
 (HIP events around each forces(): sort + block kernel + reduction).
 
     MDQT_LIB=expt/<name>/lib/libmdqt.so python tools/force_ab.py NAME [K]
+    MDQT_AB_OPTS=force_ax1=0 python tools/force_ab.py NAME [K]      (engine options, comma-separated)
 """
 import os
 import sys
@@ -23,6 +24,9 @@ def main(name, k=3):
         if only and cfg not in only.split(","):
             continue
         s = M.Simulation(seed=12346, job=1, rng_mode=1, **kw).init()
+        for o in filter(None, os.environ.get("MDQT_AB_OPTS", "").split(",")):   # e.g. "force_ax1=0"
+            opt, val = o.split("=")
+            s.set_option(opt, int(val))
         s.forces()
         s.synchronize()
         s.enable_timing(1, kinds=1)

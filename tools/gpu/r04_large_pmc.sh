@@ -33,6 +33,6 @@ for cfg in $CFGS; do
   python3 tools/prof_summary.py $(db ${TAG}_${cfg}_trace) > gpurun_out/${TAG}_${cfg}_kernel_stats.txt
   python3 -c "
 import json; d=json.load(open('gpurun_out/${TAG}_${cfg}_pmc.json'))
-k='void mdqt::k_pairs_n3b<1, false, false>(mdqt::N3BArgs)'
+k=max(('void mdqt::k_pairs_n3b<1, false, false, false>(mdqt::N3BArgs)', 'void mdqt::k_pairs_n3b<1, false, false, true>(mdqt::N3BArgs)'), key=lambda k: (d.get(k) or {}).get('dispatches', 0))
 print('${cfg}', {x: d[k].get(x) for x in ('dispatches','duration_us','SQ_INSTS_VALU','SQ_WAVES','GRBM_GUI_ACTIVE','FETCH_SIZE','WRITE_SIZE')} if k in d else 'no n3b kernel')"
 done

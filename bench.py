@@ -32,6 +32,9 @@ B_Q_PER_ION = 520.0        # algorithmic bytes per ion per fused-substep launch 
 F_Q_PER_QSTEP = 1750.0     # fp64 flop per particle-qstep
 W_F_PER_PAIR = 30.0        # fp64 flop per distinct pair
 
+METRIC = "particle-steps/sec (MD+QT) at N=3.5k and N=1M; 1/2/4/8-GPU scaling"
+LINE_MAX_BYTES = 8192      # the driver parses the last stdout line; VERDICT r04 item 1
+
 CONFIGS = {
     # name: (params, qt, description)
     "c2": (dict(N0=3500), 1, "C2: N0=3500 full MDQT, detuning=-1, Om=1, density=2, fp64"),
@@ -56,8 +59,9 @@ def parse():
     ap.add_argument("--million-config", default="c1m", choices=["none", "c1m", "c4"],
                     help="the N=1M line of the metric (QT on), one system sharded over all ranks")
     ap.add_argument("--million-steps", type=int, default=2)
-    ap.add_argument("--md-only-config", default="c3", choices=["none", "c1", "c3", "c4"],
-                    help="MD-only line (force-kernel FP64 roofline run; BASELINE configs[2] = C3)")
+    ap.add_argument("--md-only-config", default="c3,c4",
+                    help="comma-separated MD-only lines (force-kernel FP64 roofline runs; BASELINE configs[2] = "
+                         "C3, configs[3] = C4), or none")
     ap.add_argument("--no-e2e-line", action="store_true",
                     help="skip the end-to-end line (reference cadence: output() every sampleFreq MD steps)")
     ap.add_argument("--e2e-md-steps", type=int, default=400)
@@ -87,6 +91,17 @@ def parse():
                     help="bracket every k-th kernel launch of the timed region with HIP events "
                          "(0: the steps, i.e. one sampled launch of each kernel, mid-window)")
     return ap.parse_args()
+
+
+def md_only_configs(spec):
+    """--md-only-config: 'none' or a comma-separated list of MD-only configs (c1, c3, c4)"""
+    if spec in ("", "none"):
+        return []
+    cfgs = [c.strip() for c in spec.split(",") if c.strip()]
+    for c in cfgs:
+        if c not in CONFIGS or CONFIGS[c][1]:
+            raise SystemExit(f"bench.py: --md-only-config: {c} is not an MD-only config (c1, c3, c4)")
+    return cfgs
 
 
 def kernel_source_hash():
@@ -340,6 +355,7 @@ def check_world(gpus, env):
 
 
 def main():
+    t_start = time.perf_counter()
     args = parse()
     if args.child_sharded:
         return child_main(args)
@@ -425,8 +441,8 @@ def main():
             # particle-qsteps, so its algorithmic bytes are 520 N nsub (the contract's "per-unit figure
             # x units per launch").  The launch keeps the state in registers across its substeps, so
             # the bytes it must move (compulsory) are 520 N once — the PMC traffic is measured against
-            # those; and the roof that binds it is neither: FP64 VALU issue at one wave per SIMD
-            # (DESIGN.md §3, §6), reported as binding_roof with F_q = 1.75 kflop per particle-qstep.
+            # those; and the roof that binds it is neither: FP64 VALU issue, the
+            # line's roofline, with F_q = 1.75 kflop per particle-qstep.
             qsteps_launch = N * nsub_per_launch
             bytes_launch = B_Q_PER_ION * qsteps_launch
             ach = bytes_launch / s_avg / 1e9
@@ -436,30 +452,33 @@ def main():
             traffic, tsrc = pmc_traffic(kname)
             kinst = tsrc.get("instance")
             fp64 = flops / s_avg / 1e12
-            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+            # the roof that binds a register-fused launch is FP64 VALU issue (VERDICT r04
+            # item 2): frac = 1,750 flop x particle-qsteps / launch time / 78.6 TF.  Beside it the HBM
+            # figures: 8(d)'s 520 B per particle-qstep (a virtual rate for a fused launch), the PMC
+            # traffic, and the compulsory 520 B per ion once.
+            roof = {"bound": "fp64", "achieved": fp64, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": fp64 / FP64_PEAK_TFS, "traffic": traffic,
                     "kernel": f"{kinst or kname} (fused {nsub_per_launch:g} x step+qstep)",
-                    "avg_launch_us": s_avg * 1e6, "algorithmic_bytes_per_launch": bytes_launch,
-                    "algorithmic_unit": f"{B_Q_PER_ION:g} B per particle-qstep x {qsteps_launch:.0f} particle-qsteps "
-                                        "per launch (SURVEY 8d)",
-                    "compulsory_bytes_per_launch": compulsory,
+                    "avg_launch_us": s_avg * 1e6, "flop_per_launch": flops,
+                    "algorithmic_unit": f"{F_Q_PER_QSTEP:g} flop per particle-qstep x {qsteps_launch:.0f} "
+                                        "particle-qsteps per launch (SURVEY 8d)",
+                    "hbm_frac_8d": ach / HBM_PEAK_GBS,
+                    "traffic_frac": traffic / s_avg / 1e9 / HBM_PEAK_GBS if traffic else None,
                     "compulsory_hbm_frac": compulsory / s_avg / 1e9 / HBM_PEAK_GBS,
-                    "fp64_tflops": fp64, "fp64_frac": fp64 / FP64_PEAK_TFS,
-                    "binding_roof": {"kind": "fp64 VALU issue (one wave per SIMD, dependent chains)",
-                                     "achieved": fp64, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                                     "frac": fp64 / FP64_PEAK_TFS,
-                                     "flop_unit": f"{F_Q_PER_QSTEP:g} flop per particle-qstep (SURVEY 8d)"},
-                    "hbm_frac": ach / HBM_PEAK_GBS}
+                    "hbm_8d": {"achieved_GBs": ach, "bytes_per_launch": bytes_launch,
+                               "unit": f"{B_Q_PER_ION:g} B per particle-qstep (SURVEY 8d)",
+                               "compulsory_bytes_per_launch": compulsory},
+                    "traffic_source": tsrc}
         else:
             pairs = N * (N - 1) / 2.0
             flops = W_F_PER_PAIR * pairs
             ach = flops / f_avg / 1e12
-            roof = {"bound": "hbm", "achieved": (24.0 * 2 * N) / f_avg / 1e9, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": (24.0 * 2 * N) / f_avg / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                    "kernel": "k_pairs<force> + segment reduction", "avg_launch_us": f_avg * 1e6,
-                    "fp64_tflops": ach, "fp64_frac": ach / FP64_PEAK_TFS}
+            roof = {"bound": "fp64", "achieved": ach, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": ach / FP64_PEAK_TFS, "traffic": None, "kernel": "forces() (Newton-3 tiles)",
+                    "avg_launch_us": f_avg * 1e6,
+                    "hbm_frac_8d": (24.0 * 2 * N) / f_avg / 1e9 / HBM_PEAK_GBS}
         out = {
-            "metric": "particle-steps/sec (MD+QT) at N=3.5k and N=1M; 1/2/4/8-GPU scaling",
+            "metric": METRIC,
             "value": value,
             "unit": "particle-qsteps/s",
             "n_gpus": world,
@@ -483,6 +502,7 @@ def main():
                                                             "other_kernel": "8 MD steps after the window"}},
             "roofline": roof,
             "cpu_baseline": None,
+            "timed_region_s": el_max,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(params, qt, args.cpu_seconds, 12345 + job, job)
@@ -495,7 +515,7 @@ def main():
     # rank bounds them: if one of them fails or does not finish in time, rank 0 prints the line
     # with what it has (and the reason) and every rank leaves, so the headline is never lost.
     out = out if rank == 0 else None
-    dog = Watchdog(args.secondary_deadline, rank, out)
+    dog = Watchdog(args.secondary_deadline, rank, out, t_start)
     if not args.no_replicas_line:
         dog.run("jobs_per_gpu", lambda: replicas_line(local, args.config))
     if world == 1 and not args.no_e2e_line:
@@ -519,16 +539,15 @@ def main():
             res["cpu_baseline"] = cpu_baseline_large(cfg)
         return res
 
-    if args.md_only_config != "none":
-        dog.run("md_only_" + args.md_only_config,
-                lambda: with_cpu(args.md_only_config, sharded(args.md_only_config, args.sharded_steps)))
+    for cfg in md_only_configs(args.md_only_config):
+        dog.run("md_only_" + cfg, lambda cfg=cfg: with_cpu(cfg, sharded(cfg, args.sharded_steps)))
     if args.sharded_config != "none":
         dog.run("sharded", lambda: with_cpu(args.sharded_config, sharded(args.sharded_config, args.sharded_steps)))
     if args.million_config != "none":
         dog.run("sharded_1m", lambda: with_cpu(args.million_config, sharded(args.million_config, args.million_steps)))
     dog.finish()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out, t_start)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -648,13 +667,95 @@ def qtt_line(local, steps=10):
             "tagged_moments_and_distribution_ms": kde_ms, "cpu_baseline": None}
 
 
+# the headline line: the contract's keys, the roofline and CPU baseline in brief, one compact entry per
+# secondary line; everything else (censuses, PMC blocks, tail notes, samples) is the detail line
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "comm_size", "steps", "warmup", "ms_per_step",
+             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "timed_region_s")
+HEAD_CONFIG_KEYS = ("workload", "N", "md_steps", "qsteps_per_md_step", "particle_md_steps_per_s", "parallelism", "rng")
+HEAD_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "avg_launch_us",
+                  "hbm_frac_8d", "traffic_frac", "compulsory_hbm_frac")
+HEAD_CPU_KEYS = ("value", "unit", "cores", "kind", "sample")
+LINE_KEYS = ("value", "unit", "N", "n_gpus", "ms_per_md_step")
+LINE_ROOF_KEYS = ("bound", "frac", "algorithmic_equivalent_frac", "pairs_evaluated_frac", "block_kernel_ms",
+                  "load_imbalance")
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def compact_secondary(name, v):
+    """one secondary line in brief: value, unit, N, ms per MD step, roofline frac and bound, parity ok,
+    the CPU baseline's value"""
+    if isinstance(v, list):                         # pump_models
+        return [compact_secondary(name, x) for x in v]
+    if not isinstance(v, dict):
+        return v
+    if "lines" in v:                                # jobs_per_gpu
+        return {"lines": [dict(_pick(x, ("jobs", "value", "unit", "ms_per_md_step"))) for x in v["lines"]]}
+    c = _pick(v, LINE_KEYS)
+    if name == "mcmd":
+        c.update(_pick(v, ("mc_steps_per_s", "md_steps_per_s", "md_particle_steps_per_s", "main_estimate_s")))
+        if isinstance(v.get("qt_tagging"), dict):
+            c["qt_tagging_particle_qsteps_per_s"] = v["qt_tagging"].get("particle_qsteps_per_s")
+    if "qt_model" in v:
+        c["qt_model"] = v["qt_model"]
+    r = v.get("roofline")
+    if isinstance(r, dict):
+        c["roofline"] = _pick(r, LINE_ROOF_KEYS)
+    p = v.get("parity")
+    if isinstance(p, dict):
+        c["parity_ok"] = p.get("ok", None)
+    cb = v.get("cpu_baseline")
+    if isinstance(cb, dict) and "value" in cb:
+        c["cpu_baseline"] = cb["value"]
+    elif isinstance(cb, dict) and "main_estimate_s" in cb:   # mcmd: the reference build's main() estimate
+        c["cpu_baseline_main_estimate_s"] = cb["main_estimate_s"]
+    ft = v.get("force_tail")
+    if isinstance(ft, dict) and "bound_met" in ft:
+        c["force_tail_bound_met"] = ft["bound_met"]
+    return c
+
+
+def compact_line(out):
+    """the headline JSON line (<= LINE_MAX_BYTES): the secondary lines are dropped from the end, largest
+    first, if it ever grows past the budget (they stay in the detail line)"""
+    h = _pick(out, HEAD_KEYS)
+    h["config"] = _pick(out.get("config", {}), HEAD_CONFIG_KEYS)
+    h["roofline"] = _pick(out.get("roofline") or {}, HEAD_ROOF_KEYS)
+    cb = out.get("cpu_baseline")
+    h["cpu_baseline"] = _pick(cb, HEAD_CPU_KEYS) if isinstance(cb, dict) else None
+    if isinstance(cb, dict) and isinstance(cb.get("single_thread"), dict):
+        h["cpu_baseline"]["single_thread_value"] = cb["single_thread"].get("value")
+    sec = {k: compact_secondary(k, v) for k, v in out.items() if k not in HEAD_KEYS and k not in
+           ("config", "roofline", "cpu_baseline", "secondary_errors", "run_s")}
+    h["lines"] = sec
+    if out.get("secondary_errors"):
+        h["secondary_errors"] = {k: str(e)[:200] for k, e in out["secondary_errors"].items()}
+    if "run_s" in out:
+        h["run_s"] = out["run_s"]
+    while len(json.dumps(h)) > LINE_MAX_BYTES and h["lines"]:
+        big = max(h["lines"], key=lambda k: len(json.dumps(h["lines"][k])))
+        h["lines"].pop(big)
+        h.setdefault("lines_in_detail_only", []).append(big)
+    return h
+
+
+def emit(out, t_start=None):
+    """the detail line (BENCH_DETAIL, stderr) then the headline line, last on stdout"""
+    if t_start is not None:
+        out["run_s"] = time.perf_counter() - t_start
+    print("BENCH_DETAIL " + json.dumps(out), file=sys.stderr, flush=True)
+    print(json.dumps(compact_line(out)), flush=True)
+
+
 class Watchdog:
     """Bounds the secondary line items: exceptions are recorded in the line, and if the deadline
     passes (e.g. a collective that never completes) rank 0 prints what it has and every rank exits."""
 
-    def __init__(self, seconds, rank, out):
+    def __init__(self, seconds, rank, out, t_start):
         import threading
-        self.rank, self.out, self.lock = rank, out, threading.Lock()
+        self.rank, self.out, self.lock, self.t_start = rank, out, threading.Lock(), t_start
         self.done = threading.Event()
         self.current = None
         self.t = threading.Thread(target=self._wait, args=(seconds,), daemon=True)
@@ -667,7 +768,7 @@ class Watchdog:
             if self.rank == 0:
                 self.out.setdefault("secondary_errors", {})[self.current or "?"] = \
                     f"did not finish within {seconds:.0f} s (watchdog)"
-                print(json.dumps(self.out), flush=True)
+                emit(self.out, self.t_start)
             sys.stdout.flush()
             os._exit(0)
 
@@ -770,26 +871,34 @@ def latest_large_pmc(cfg):
     return os.path.join(d, fs[-1]) if fs else None
 
 
-def large_roofline(cfg, census, f_avg, N, world):
-    """Roofline of a large line's dominant kernel, k_pairs_n3b.  FP64 VALU is the
-    roof (30 flop per distinct pair, ~0 B per pair after staging).  Two rates:
-    algorithmic — all N(N-1)/2 pairs, what 8(d) defines — and on the pairs the kernel actually
-    evaluates (the census: skipped tile pairs excluded, lane-steps of the evaluated ones, every tier).
-    With a PMC summary of the same config measured on this tree's kernel sources (world 1): VALU /
-    SALU / LDS instructions per evaluated pair, the VALU issue-slot fraction (VALU x 4 cycles over
-    1,024 SIMDs x the kernel's cycles GRBM_GUI_ACTIVE / 8), and the kernel's own duration from the
-    kernel trace of the same command."""
+def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None):
+    """Roofline of a large line's dominant kernel, k_pairs_n3b.  FP64 VALU is the roof (30
+    flop per distinct pair, ~0 B per pair after staging).  `frac` is the block kernel's own rate on the
+    pairs it evaluates: 30 flop x the census's evaluated lane-steps (skipped tile
+    pairs and sub-tile groups excluded, every pair form counted) / the kernel's average duration from
+    its own HIP dispatch timestamps (k_avg, the timed force calls) / (world x 78.6 TF).  Beside it:
+    algorithmic_equivalent_frac — all N(N-1)/2 pairs in the same time, what 8(d) defines — and
+    pairs_evaluated_frac, the evaluated share; force_call_frac — all pairs over the whole forces() call
+    (sort, plan, kernel, reduction, tail pass, collectives).  With a PMC summary of the same config
+    measured on this tree's kernel sources (world 1): VALU / SALU / LDS instructions per evaluated
+    pair, the VALU issue-slot fraction, and the kernel's duration from the kernel trace."""
     tot = N * (N - 1) / 2.0
     ev = sum(v[0] for k, v in census.items() if not k.startswith("skip"))
-    peak = FP64_PEAK_TFS
+    peak = FP64_PEAK_TFS * world
+    t = k_avg if k_avg else f_avg
     roof = {"bound": "fp64", "kernel": N3B_KERNEL, "unit": "TFLOP/s", "peak": peak,
-            "achieved": W_F_PER_PAIR * tot / f_avg / 1e12, "frac": W_F_PER_PAIR * tot / f_avg / 1e12 / peak,
-            "fp64_frac_algorithmic": W_F_PER_PAIR * tot / f_avg / 1e12 / peak,
-            "fp64_frac_evaluated": W_F_PER_PAIR * ev / f_avg / 1e12 / peak,
-            "evaluated_lane_steps": ev, "evaluated_per_pair": ev / tot,
-            "time": "force() HIP events: spatial sort + block kernel + slot reduction (+ tail pass)",
+            "achieved": W_F_PER_PAIR * ev / t / 1e12, "frac": W_F_PER_PAIR * ev / t / 1e12 / peak,
+            "algorithmic_equivalent_frac": W_F_PER_PAIR * tot / t / 1e12 / peak,
+            "pairs_evaluated_frac": ev / tot,
+            "force_call_frac": W_F_PER_PAIR * tot / f_avg / 1e12 / peak,
+            "block_kernel_ms": k_avg * 1e3 if k_avg else None, "force_call_ms": f_avg * 1e3,
+            "evaluated_lane_steps": ev,
+            "time": "k_pairs_n3b's own dispatch timestamps (HIP events, every timed force call; max over ranks)"
+                    if k_avg else "force() HIP events (no block-kernel timestamps)",
             "tiers": {k: {"lane_steps": v[0], "ion_pairs": v[1], "pairs_frac": v[1] / tot} for k, v in census.items()},
             "traffic": None, "pmc": None}
+    if imbalance is not None:
+        roof["load_imbalance"] = imbalance
     path = latest_large_pmc(cfg)
     if world != 1 or not path:
         return roof
@@ -854,12 +963,14 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     sim.synchronize()
     barrier()
     el = time.perf_counter() - t0
-    f_ms, nf, s_ms, ns = sim.kernel_time_totals()
+    kt = sim.kernel_times()
+    f_ms, nf, s_ms, ns = kt["force_ms"], kt["n_force"], kt["substep_ms"], kt["n_substep"]
+    k_avg = kt["block_ms"] / kt["n_block"] * 1e-3 if kt["n_block"] else 0.0
     sim.enable_timing(False)
-    tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+    tt = torch.tensor([el, k_avg], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    el = float(tt[0])
+    el, k_avg = float(tt[0]), float(tt[1])
     N = sim.N
     L = sim.const("L")
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
@@ -873,14 +984,21 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     tail_eps = 10.0 ** -12                          # force_tail_exp default
     bound_met = bool(rt >= L / 2 or (tmode == 1 and tail <= tail_eps) or tmode == 0)
     census = None                                  # the block kernel's work by tile-pair class
+    imbalance = None
     if int(sim.const("force_scheme")) == 3 and int(sim.const("force_sort")) == 1:
         census = sim.force_census()                # (this rank's block pairs: summed over the ranks)
         if world > 1:
             keys = list(census)
+            ev_r = sum(v[0] for k, v in census.items() if not k.startswith("skip"))
             t = torch.tensor([x for k in keys for x in census[k]], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             v = t.tolist()
             census = {k: (v[2 * i], v[2 * i + 1]) for i, k in enumerate(keys)}
+            # load balance: this rank's evaluated lane-steps, max over mean
+            m = torch.tensor([ev_r], dtype=torch.float64, device="cuda")
+            dist.all_reduce(m, op=dist.ReduceOp.MAX)
+            ev_t = sum(v[0] for k, v in census.items() if not k.startswith("skip"))
+            imbalance = float(m[0]) / (ev_t / world) if ev_t else None
     parity = None
     if check:
         # the sharded result against a world-1 context built from the same inputs
@@ -926,7 +1044,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force,
-            "roofline": large_roofline(cfg, census, f_avg, N, world) if census and f_avg else None,
+            "roofline": large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance) if census and f_avg else None,
             "parity": parity if check else {"note": "world 1: this line is the reference the sharded runs are checked against"},
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail, "bound_met": bound_met,
                            "tail_mode": "measured+enforced" if tmode == 1 else "a priori",

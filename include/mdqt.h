@@ -297,6 +297,10 @@ int         mdqt_enable_timing_kinds(mdqt_ctx* c, int period, int kinds);
 int         mdqt_enable_timing_at(mdqt_ctx* c, int period, int kinds, int offset);
 int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
                                     int* nsub);
+/* the same with the Newton-3 block kernel (k_pairs_n3b, N > 65,536) timed on its own inside every
+ * timed force call (its dispatch timestamps: the plan, the slot reduction, the tail pass and the
+ * collectives excluded): out[6] = force_ms, n_force, substep_ms, n_substep, block_ms, n_block */
+int         mdqt_kernel_times(mdqt_ctx* c, double* out, int n);
 
 #ifdef __cplusplus
 }

@@ -143,6 +143,7 @@ SIGNATURES = [
     ("mdqt_allreduce_sum", C.c_int, [C.c_void_p, _dp, C.c_size_t]),
     ("mdqt_force_census", C.c_int, [C.c_void_p, _dp, C.c_int]),
     ("mdqt_kernel_time_totals", C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int), _dp, C.POINTER(C.c_int)]),
+    ("mdqt_kernel_times", C.c_int, [C.c_void_p, _dp, C.c_int]),
     ("mdqt_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_enable_timing_kinds", C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     ("mdqt_enable_timing_at", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),

@@ -130,6 +130,7 @@ struct mdqt_ctx {
     int* dTailList = nullptr;      // [T]: this call's tiles over eps (this rank's)
     double tail_scale = 1.;        // r_t from 2 tail_scale B(r) <= eps: raised when a call exceeded eps
     unsigned long long tail_seen = 0;   // tiles over eps the host has reacted to
+    int tail_warned = 0;                // stderr lines printed by tail_check
     bool tail_pending = false;     // in-process group: the sums wait for the group's (local_reduce)
     N3BArgs tail_args;             // ... with the call's arguments
     mutable double tail_key[5] = {0, 0, 0, 0, 0}, tail_val[2] = {0, 0};   // tail_radius_sum memo (N, L, lDeb, k, scale)
@@ -216,17 +217,21 @@ struct mdqt_ctx {
     unsigned tperiod = 1, tcount[2] = {0, 0};   // bracket launches k = toffset mod tperiod of each kind
     unsigned toffset = 0;                        // tperiod / 2 unless mdqt_enable_timing_at
                                                 // (mid-period: not the first launch after a sync)
-    std::vector<hipEvent_t> evpool[2];
-    int evused[2] = {0, 0};
+    std::vector<hipEvent_t> evpool[3];          // 2: the Newton-3 block kernel's own timestamps (a timed force call)
+    int evused[3] = {0, 0, 0};
 };
 
 static int settle_forces(mdqt_ctx* s);
 static int tail_check(mdqt_ctx* s);
 static double u64_as_double(unsigned long long u) { double d; memcpy(&d, &u, sizeof d); return d; }
 
-// force_tail_mode 1: forget what earlier calls measured (a new state, size or tail option)
-static int tail_reset(mdqt_ctx* s) {
-    s->tail_scale = 1.;
+// force_tail_mode 1: forget what earlier calls measured (a new size or tail option).  keep_scale (new
+// positions of the same system, e.g. a driver that uploads R every MD step): the statistics restart
+// but the widened r_t stays — a clustered configuration does not rerun the exact pass, and warn, at
+// every upload.  Callers settle pending forces first (they were measured with the old
+// options: their enforcement must complete before the sums are cleared).
+static int tail_reset(mdqt_ctx* s, bool keep_scale = false) {
+    if (!keep_scale) s->tail_scale = 1.;
     s->tail_seen = 0;
     s->tail_pending = false;
     if (s->dTailSt) HIPCHK(hipMemsetAsync(s->dTailSt, 0, 8 * sizeof(unsigned long long), s->stream));
@@ -1043,10 +1048,12 @@ static int upload(mdqt_ctx* s, const double* R, const double* V, size_t ld, cons
 extern "C" int mdqt_set_state(mdqt_ctx* s, int N, const double* R, const double* V, size_t ld,
                               const double* psi, const double* tPart, double t) {
     if (!s) return fail("NULL context");
-    if (N != s->N && resize(s, N)) return -1;
+    if (settle_forces(s)) return -1;                   // pending partials of the previous positions
+    const bool sameN = N == s->N;
+    if (!sameN && resize(s, N)) return -1;
     if (ld < (size_t)N) return fail("ld < N");
     if (upload(s, R, V, ld, psi, tPart)) return -1;
-    if (R && tail_reset(s)) return -1;                 // new positions: the tail measurements restart
+    if (R && tail_reset(s, sameN)) return -1;          // new positions: the tail statistics restart
     s->t = t;
     return 0;
 }
@@ -1280,7 +1287,9 @@ static double tail_radius_sum(const mdqt_ctx* s, double* bound) {
 }
 // the context's skip radius: mode 1 (measured and enforced) in spatial order at every world size
 // (the per-tile sums are all-reduced, so 1 and W ranks run the same algorithm), else a priori
-static bool tail_measured(const mdqt_ctx* s) { return s->tail_mode == 1 && s->sort_mode == 1; }
+// — for the fast pair form only: k_tail_fix recomputes the listed tiles in that form (pair_ft<1>, the
+// cutoff on dr < Rcut), so the other variants keep the a-priori radius
+static bool tail_measured(const mdqt_ctx* s) { return s->tail_mode == 1 && s->sort_mode == 1 && s->force_variant == 1; }
 static double skip_radius(const mdqt_ctx* s, double* bound) {
     return tail_measured(s) ? tail_radius_sum(s, bound) : tail_radius(s->N, s->L, s->lDeb, s->tail_exp, bound);
 }
@@ -1303,9 +1312,10 @@ static int tail_check(mdqt_ctx* s) {
     // a power of two: the sums' last bits (atomic order, the ranks' partial sums) cannot move it
     s->tail_scale = std::max(2. * s->tail_scale, std::isfinite(u) && u < 1e300 ? exp2(ceil(log2(u))) : 1e300);
     const double r1 = tail_radius_sum(s, &b1);
-    fprintf(stderr, "mdqt: force tail over 1e-%d on %llu tile(s) so far (largest per-tile sum %.3e; the model's "
-            "%.3e at r_t = %.4f): corrected by the exact pass; r_t widened to %.4f\n", s->tail_exp,
-            (unsigned long long)h[2], raw, b0, r0, r1);
+    if (s->tail_warned++ < 8)                       // (rate-limited: a few lines per context)
+        fprintf(stderr, "mdqt: force tail over 1e-%d on %llu tile(s) so far (largest per-tile sum %.3e; the model's "
+                "%.3e at r_t = %.4f): corrected by the exact pass; r_t widened to %.4f\n", s->tail_exp,
+                (unsigned long long)h[2], raw, b0, r0, r1);
     s->tail_seen = h[2];
     return 0;
 }
@@ -1556,7 +1566,9 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
             HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)4 * a.T * sizeof(double), s->stream));
             HIPCHK(hipMemsetAsync(s->dTailSt + 3, 0, sizeof(unsigned long long), s->stream));
         }
-        HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream));
+        hipEvent_t e0 = nullptr, e1 = nullptr;     // timed call: the block kernel alone as well
+        if (tm && take_events(s, 2, &e0, &e1)) return -1;
+        HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream, e0, e1));
         if (a.tailb) {                  // measured tail: complete the per-tile sums, then enforce eps
             if (W > 1 && s->comm) {
                 NCCLCHK(ncclAllReduce(a.tailb, a.tailb, (size_t)4 * a.T, ncclDouble, ncclSum, s->comm, s->stream));
@@ -2736,13 +2748,13 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     }
     if (!strcmp(name, "force_tail_exp")) {             // error-bounded tail: eps = 10^-value (0: exact)
         if (value < 0 || value > 300) return fail("force_tail_exp must be 0 (exact) .. 300");
-        if (value != s->tail_exp && tail_reset(s)) return -1;
+        if (value != s->tail_exp && (settle_forces(s) || tail_reset(s))) return -1;
         s->tail_exp = value;
         return 0;
     }
     if (!strcmp(name, "force_tail_mode")) {            // 0: a-priori bound, 1: measured and enforced
         if (value < 0 || value > 1) return fail("force_tail_mode must be 0 (a priori) or 1 (measured)");
-        if (value != s->tail_mode && tail_reset(s)) return -1;
+        if (value != s->tail_mode && (settle_forces(s) || tail_reset(s))) return -1;
         s->tail_mode = value;
         return 0;
     }
@@ -2771,6 +2783,7 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     }
     if (!strcmp(name, "force_kernel")) {
         if (value < 0 || value > 1) return fail("force_kernel must be 0 (exact) or 1 (fast)");
+        if (value != s->force_variant && (settle_forces(s) || tail_reset(s))) return -1;   // tail_measured changes
         s->force_variant = value;
         return 0;
     }
@@ -2811,7 +2824,7 @@ extern "C" int mdqt_enable_timing_at(mdqt_ctx* s, int on, int kinds, int offset)
     s->toffset = on > 0 ? (unsigned)offset : 0u;
     s->tkinds = (unsigned)kinds;
     s->tcount[0] = s->tcount[1] = 0;
-    s->evused[0] = s->evused[1] = 0;
+    s->evused[0] = s->evused[1] = s->evused[2] = 0;
     return 0;
 }
 extern "C" int mdqt_enable_timing_kinds(mdqt_ctx* s, int on, int kinds) {
@@ -2819,21 +2832,33 @@ extern "C" int mdqt_enable_timing_kinds(mdqt_ctx* s, int on, int kinds) {
 }
 extern "C" int mdqt_enable_timing(mdqt_ctx* s, int on) { return mdqt_enable_timing_kinds(s, on, 3); }
 
-extern "C" int mdqt_kernel_time_totals(mdqt_ctx* s, double* force_ms, int* nforce, double* sub_ms, int* nsub) {
+extern "C" int mdqt_kernel_times(mdqt_ctx* s, double* out, int n) {
+    if (!s || !out) return fail("mdqt_kernel_times: NULL argument");
+    if (n < 6) return fail("mdqt_kernel_times: need 6 doubles");
     HIPCHK(hipSetDevice(s->dev));
     HIPCHK(hipStreamSynchronize(s->stream));
-    double tot[2] = {0., 0.};
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < 3; ++k) {
+        double tot = 0.;
         for (int i = 0; i + 1 < s->evused[k]; i += 2) {
             float ms = 0.f;
             HIPCHK(hipEventElapsedTime(&ms, s->evpool[k][i], s->evpool[k][i + 1]));
-            tot[k] += ms;
+            tot += ms;
         }
-    if (force_ms) *force_ms = tot[0];
-    if (nforce) *nforce = s->evused[0] / 2;
-    if (sub_ms) *sub_ms = tot[1];
-    if (nsub) *nsub = s->evused[1] / 2;
-    s->evused[0] = s->evused[1] = 0;
+        out[2 * k] = tot;
+        out[2 * k + 1] = (double)(s->evused[k] / 2);
+        s->evused[k] = 0;
+    }
+    return 0;
+}
+
+extern "C" int mdqt_kernel_time_totals(mdqt_ctx* s, double* force_ms, int* nforce, double* sub_ms, int* nsub) {
+    if (!s) return fail("NULL context");
+    double t[6];
+    if (mdqt_kernel_times(s, t, 6)) return -1;
+    if (force_ms) *force_ms = t[0];
+    if (nforce) *nforce = (int)t[1];
+    if (sub_ms) *sub_ms = t[2];
+    if (nsub) *nsub = (int)t[3];
     return 0;
 }
 

@@ -1131,7 +1131,7 @@ hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s) {
+hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     const int nblk = (a.Phi - a.Plo) * a.R;
     const int nplan = (a.Phi - a.Plo) * a.nd;
     if (a.plan && nplan > 0) {
@@ -1154,13 +1154,16 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
             // N = 1M, r_s = 61 < 80.6 - 12.9).  A function of the call's parameters alone: every rank
             // of a sharded run, and every call of one configuration, takes the same kernel.
             const bool axp = a.ax1 && a.use_sort != 0 && a.Rskip > 0.5 * a.L - 2. * a.L * cbrt(64. / a.N);
-            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<1, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
-            else if (axp) hipLaunchKernelGGL((k_pairs_n3b<1, false, false, MDQT_N3B_AX1 != 0>), dim3(nblk), dim3(BW * 64), 0, s, a);
-            else hipLaunchKernelGGL((k_pairs_n3b<1, false>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            if (a.guard) launch_timed(k_pairs_n3b<1, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
+            else if (axp) launch_timed(k_pairs_n3b<1, false, false, MDQT_N3B_AX1 != 0>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
+            else launch_timed(k_pairs_n3b<1, false>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
         } else {
-            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<0, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
-            else hipLaunchKernelGGL((k_pairs_n3b<0, false>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            if (a.guard) launch_timed(k_pairs_n3b<0, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
+            else launch_timed(k_pairs_n3b<0, false>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
         }
+    } else if (ev0) {                                   // (no block of this rank: an empty interval)
+        hipEventRecord(ev0, s);
+        hipEventRecord(ev1, s);
     }
     hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, a, out);
     return hipGetLastError();

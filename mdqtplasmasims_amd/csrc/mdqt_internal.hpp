@@ -460,7 +460,10 @@ struct SortArgs {
 };
 hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s);
 size_t spatial_order_tmp_bytes(int N);
-hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
+// ev0/ev1: the block kernel's own dispatch timestamps (timing on; k_pairs_n3b alone, not the plan or
+// the reduction)
+hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0 = nullptr,
+                             hipEvent_t ev1 = nullptr);
 // force_tail_mode 1 (mdqt_forces.hip): the per-sub-tile tail sums [4T] against eps — st[0] running
 // max of the tiles within eps, st[1] of all, st[2] tiles over eps (cumulative), st[3] this call's
 // list length, st[4] measured calls — and the exact recomputation of the listed tiles' forces,

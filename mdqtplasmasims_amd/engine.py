@@ -348,5 +348,13 @@ class Simulation:
         check(lib().mdqt_kernel_time_totals(self.h, C.byref(a), C.byref(na), C.byref(b), C.byref(nb)))
         return a.value, na.value, b.value, nb.value
 
+    def kernel_times(self):
+        """{force_ms, n_force, substep_ms, n_substep, block_ms, n_block} since the last call (block: the
+        Newton-3 block kernel alone inside the timed force calls; include/mdqt.h mdqt_kernel_times)"""
+        out = (C.c_double * 6)()
+        check(lib().mdqt_kernel_times(self.h, out, 6), "kernel_times")
+        keys = ("force_ms", "n_force", "substep_ms", "n_substep", "block_ms", "n_block")
+        return {k: (int(out[i]) if k.startswith("n_") else out[i]) for i, k in enumerate(keys)}
+
 
 __all__ = ["forces_raw", "potentials_raw", "Simulation", "MdqtError", "default_params", "device_count", "slab", "NBINS", "NUM_STATES"]

@@ -295,6 +295,10 @@ int         mdqt_enable_timing_kinds(mdqt_ctx* c, int period, int kinds);
 /* the same with the bracketed launches at index `offset` mod period (0 <= offset < period;
  * enable_timing_kinds takes period / 2) */
 int         mdqt_enable_timing_at(mdqt_ctx* c, int period, int kinds, int offset);
+/* the Newton-3 block kernel's evaluated lane-steps per block of this rank (every tile-pair class but the
+ * skipped ones) for the current positions: out[0 .. *nblocks) for blocks Plo .. Phi - 1; at world 1
+ * every block, so the work of any partition of the blocks over ranks follows (load balance) */
+int         mdqt_force_block_work(mdqt_ctx* c, double* out, int n, int* nblocks);
 int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
                                     int* nsub);
 /* the same with the Newton-3 block kernel (k_pairs_n3b, N > 65,536) timed on its own inside every

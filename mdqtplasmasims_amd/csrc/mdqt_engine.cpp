@@ -990,6 +990,8 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "qt_kernel")) return s->last_qt_kernel;     // instance of the last substep launch (QTKernel)
     if (!strcmp(n, "qt_kernel_nseg")) return s->last_qt_nseg;  // force partials its prologue summed
     if (!strcmp(n, "force_slots")) return s->nslots;           // Newton-3 tile slots (0: other schemes)
+    if (!strcmp(n, "n3b_blocks")) return s->use_n3b ? s->n3b.Phi - s->n3b.Plo : 0;   // this rank's blocks
+    if (!strcmp(n, "n3b_block_count")) return s->use_n3b ? s->n3b.NB : 0;             // all blocks
     if (!strcmp(n, "slab_S")) return s->S;
     if (!strncmp(n, "gs", 2)) return s->gs[atoi(n + 2)];
     return NAN;
@@ -1528,6 +1530,32 @@ extern "C" int mdqt_force_census(mdqt_ctx* s, double* out, int n) {
     (void)hipFree(d);
     if (e != hipSuccess) return fail("mdqt_force_census: %s", hipGetErrorString(e));
     for (int k = 0; k < 2 * kCensus; ++k) out[k] = (double)h[k];
+    return 0;
+}
+
+// the block kernel's evaluated lane-steps per block of this rank for the current positions (k_n3b_census's
+// per-block sums): out[P - Plo], P = Plo .. Phi - 1 (*nblocks = Phi - Plo) — what each block's workgroups
+// do; at world 1 every block, so the work of any rank partition follows
+extern "C" int mdqt_force_block_work(mdqt_ctx* s, double* out, int n, int* nblocks) {
+    if (!s || !out || !nblocks) return fail("mdqt_force_block_work: NULL argument");
+    if (!s->use_n3b || !s->sort_mode) return fail("mdqt_force_block_work: Newton-3 blocks in spatial order only");
+    const int nb = std::max(s->n3b.Phi - s->n3b.Plo, 0);
+    *nblocks = nb;
+    if (n < nb) return fail("mdqt_force_block_work: need %d doubles", nb);
+    if (nb == 0) return 0;
+    HIPCHK(hipSetDevice(s->dev));
+    N3BArgs a;
+    if (n3b_args(s, a)) return -1;
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc(&d, (2 * kCensus + (size_t)nb) * sizeof(unsigned long long)));
+    std::vector<unsigned long long> h((size_t)nb);
+    hipError_t e = launch_n3b_census(a, d, s->stream, d + 2 * kCensus);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d + 2 * kCensus, (size_t)nb * sizeof(unsigned long long),
+                                            hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail("mdqt_force_block_work: %s", hipGetErrorString(e));
+    for (int k = 0; k < nb; ++k) out[k] = (double)h[k];
     return 0;
 }
 

@@ -854,11 +854,21 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
 // 13 mid uniform (round 4: appended, the earlier indices kept).  One workgroup
 // per (block P, block distance db); thread (b, q) takes tile pair (16 P + q, 16 Q + b) as the
 // kernel's wave q at J-step b does.
-__global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long long* __restrict__ out) {
+// bw (optional): the evaluated lane-steps (every class but the skipped ones) per block of this rank,
+// bw[P - Plo] — the work each block's workgroups do, for the ranks' load balance (mdqt_force_block_work)
+__global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long long* __restrict__ out,
+                                                    unsigned long long* __restrict__ bw) {
     __shared__ unsigned long long h[2 * kCensus];
+    __shared__ unsigned long long hb;
     const int t = threadIdx.x;
     if (t < 2 * kCensus) h[t] = 0;
+    if (t == 0) hb = 0;
     __syncthreads();
+    auto add = [&](int k, unsigned long long steps, unsigned long long pairs) {
+        atomicAdd(&h[k], steps);
+        atomicAdd(&h[kCensus + k], pairs);
+        if (k != 0 && k != 1 && k != 11) atomicAdd(&hb, steps);
+    };
     const int P = a.Plo + (int)blockIdx.x / a.nd, db = (int)blockIdx.x % a.nd;
     const int q = t & (BW - 1), b = t / BW;
     const int Q = (P + db) % a.NB;
@@ -879,13 +889,9 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
             return gl >= 3 ? 7 : gl == 2 ? 5 : gl == 1 ? 12 : 3;
         };
         if (t4.w < 0.) {
-            const int k = t4.w == -2. ? 1 : 0;
-            atomicAdd(&h[k], 4096ull);
-            atomicAdd(&h[kCensus + k], (unsigned long long)(nI * nJ));
+            add(t4.w == -2. ? 1 : 0, 4096ull, (unsigned long long)(nI * nJ));
         } else if (diag) {
-            const int k = cls_of(0);
-            atomicAdd(&h[k], 2560ull);
-            atomicAdd(&h[kCensus + k], (unsigned long long)(nI * (nI - 1) / 2));
+            add(cls_of(0), 2560ull, (unsigned long long)(nI * (nI - 1) / 2));
         } else {
             const int T4 = 4 * a.T;
             unsigned act = 0, mm = 0, mf = 0, mv = 0, mu = 0, m32 = 0;
@@ -904,15 +910,13 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                 }
             const unsigned g = a.use_sort == 1 ? sub_groups_of(act) : 0xFu;   // (2: nothing skipped)
             const unsigned lv = sub_group_levels(mm, mf, mv, mu, m32);
-            for (int d = 0; d < 4; ++d) {
-                const int k = (g >> d) & 1u ? cls_of((lv >> (4 * d)) & 15u) : 11;
-                atomicAdd(&h[k], 1024ull);
-                atomicAdd(&h[kCensus + k], (unsigned long long)np[d]);
-            }
+            for (int d = 0; d < 4; ++d)
+                add((g >> d) & 1u ? cls_of((lv >> (4 * d)) & 15u) : 11, 1024ull, (unsigned long long)np[d]);
         }
     }
     __syncthreads();
     if (t < 2 * kCensus && h[t]) atomicAdd(out + t, h[t]);
+    if (bw && t == 0 && hb) atomicAdd(bw + (P - a.Plo), hb);
 }
 
 // The block kernel's plan (force calls in spatial order): every tile pair of this rank's block pairs
@@ -1162,8 +1166,7 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
             else launch_timed(k_pairs_n3b<0, false>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
         }
     } else if (ev0) {                                   // (no block of this rank: an empty interval)
-        hipEventRecord(ev0, s);
-        hipEventRecord(ev1, s);
+        if (hipEventRecord(ev0, s) != hipSuccess || hipEventRecord(ev1, s) != hipSuccess) return hipGetLastError();
     }
     hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, a, out);
     return hipGetLastError();
@@ -1183,11 +1186,13 @@ hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const
     return hipGetLastError();
 }
 
-hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s) {
+hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s, unsigned long long* bw) {
     if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // the classes need the boxes
     const int nblk = (a.Phi - a.Plo) * a.nd;
     if (hipMemsetAsync(out, 0, 2 * kCensus * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
-    if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out);
+    if (bw && a.Phi > a.Plo && hipMemsetAsync(bw, 0, (size_t)(a.Phi - a.Plo) * sizeof(unsigned long long), s) != hipSuccess)
+        return hipGetLastError();
+    if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out, bw);
     return hipGetLastError();
 }
 

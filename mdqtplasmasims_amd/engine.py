@@ -342,6 +342,17 @@ class Simulation:
         check(lib().mdqt_force_census(self.h, out, 2 * n), "force_census")
         return {k: (out[i], out[n + i]) for i, k in enumerate(self.CENSUS_CLASSES)}
 
+    def force_block_work(self):
+        """the block kernel's evaluated lane-steps per block of this rank (numpy array; include/mdqt.h
+        mdqt_force_block_work)"""
+        import numpy as np
+        nb = C.c_int()
+        n = max(1, int(self.const("n3b_blocks")))
+        out = np.zeros(n)
+        check(lib().mdqt_force_block_work(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(nb)),
+              "force_block_work")
+        return out[:nb.value].copy()
+
     def kernel_time_totals(self):
         """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""
         a = C.c_double(); b = C.c_double(); na = C.c_int(); nb = C.c_int()

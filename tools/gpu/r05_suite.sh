@@ -22,3 +22,5 @@ tail -1 gpurun_out/${TAG}_bench.out > gpurun_out/${TAG}_full_bench.json
 grep "^BENCH_DETAIL " gpurun_out/${TAG}_bench.err | sed 's/^BENCH_DETAIL //' > gpurun_out/${TAG}_bench_detail.json
 wc -c gpurun_out/${TAG}_full_bench.json
 python3 tools/bench_brief.py gpurun_out/${TAG}_full_bench.json
+timeout -k 10 300 python3 -u tools/load_balance.py c4 c5 c1m > gpurun_out/${TAG}_load_balance.json 2> gpurun_out/${TAG}_load_balance.err || { tail -20 gpurun_out/${TAG}_load_balance.err; exit 1; }
+cat gpurun_out/${TAG}_load_balance.err

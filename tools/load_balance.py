@@ -1,0 +1,61 @@
+"""Load balance of the sharded Newton-3 block kernel, measured on one GPU.
+
+Rank r of W owns blocks [r NB / W, (r + 1) NB / W) (mdqt_engine.cpp plan sizing); its block kernel
+does the evaluated lane-steps of those blocks' workgroups.  mdqt_force_block_work at world 1 gives
+every block's evaluated lane-steps for the reference's init() positions (k_n3b_census, the block
+kernel's own classification), so each partition's per-rank work follows; reported: max / mean over
+the ranks for W = 2, 4, 8, with the equal-count partition the engine uses, and after 3 MD steps.
+
+    python tools/load_balance.py [c4 c5 c1m] > profiles/r05_load_balance.json
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import mdqtplasmasims_amd as M  # noqa: E402
+
+
+def partition(work, W):
+    NB = len(work)
+    per = np.array([work[r * NB // W:(r + 1) * NB // W].sum() for r in range(W)])
+    return per
+
+
+def main():
+    cfgs = sys.argv[1:] or ["c4", "c5", "c1m"]
+    out = {}
+    for cfg in cfgs:
+        params, qt, desc = bench.CONFIGS[cfg]
+        t0 = time.perf_counter()
+        sim = M.Simulation(device=0, seed=12346, job=1, qt_enabled=qt, **params).init()
+        res = {"workload": desc, "N": sim.N, "blocks": int(sim.const("n3b_block_count"))}
+        for tag, steps in (("init", 0), ("after_3_md_steps", 3)):
+            if steps:
+                sim.md_steps(steps)
+            w = sim.force_block_work()
+            cen = sim.force_census()
+            ev = sum(v[0] for k, v in cen.items() if not k.startswith("skip"))
+            assert abs(w.sum() - ev) <= 1e-9 * ev, (w.sum(), ev)     # the per-block sums are the census
+            row = {"evaluated_lane_steps": ev, "block_min_over_mean": float(w.min() / w.mean()),
+                   "block_max_over_mean": float(w.max() / w.mean())}
+            for W in (2, 4, 8):
+                per = partition(w, W)
+                row[f"world{W}_max_over_mean"] = float(per.max() / per.mean())
+                row[f"world{W}_min_over_mean"] = float(per.min() / per.mean())
+            res[tag] = row
+        sim.close()
+        res["seconds"] = time.perf_counter() - t0
+        out[cfg] = res
+        print(cfg, json.dumps(res), file=sys.stderr, flush=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

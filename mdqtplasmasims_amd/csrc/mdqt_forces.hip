@@ -212,6 +212,33 @@ __device__ __forceinline__ const double* tile_base(const double* Rall, int tile,
 // (the sub-tile pairs (0, 2), (1, 3) once); group 3 would repeat group 1's pairs.
 __device__ __forceinline__ int n3b_lds(int l) { return 32 * (l >> 4) + (l & 15); }   // J ion l's first copy
 
+// The lane index recomputed where it is used (MDQT_N3B_REMAT): two VALU (v_mbcnt) in volatile asm, which
+// the compiler neither hoists nor merges — so no VGPR holds the lane index, or a value derived from it,
+// across the block kernel's J-step loop (at its 80-VGPR budget such values were spilled and reloaded
+// with a vmcnt(0) wait at every pair-form dispatch)
+#ifndef MDQT_N3B_REMAT
+#define MDQT_N3B_REMAT 1
+#endif
+// One LDS-DMA load (global_load_lds_dwordx4: 16 bytes per lane from the lane's address g, into LDS at the
+// wave-uniform byte offset lds + 16 x lane), in inline asm so that the compiler's wait-count pass does
+// not see it: with the builtin it waited vmcnt(0) before every LDS atomic of the pair loops (a DMA
+// writing LDS might alias them), retiring the DMA at once.  The caller counts and waits for it.
+__device__ __forceinline__ void lds_dma16(const void* g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+template <typename T>
+__device__ __forceinline__ unsigned lds_offset(T* p) {          // a __shared__ object's LDS byte offset
+    return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) T*)p);
+}
+__device__ __forceinline__ int lane_opaque(int l) {
+    if constexpr (!MDQT_N3B_REMAT) return l;
+    int r;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+    return r;
+}
+
 // every 16 steps the LDS arrays are re-based at the lane's index (an opaque register), so the 16
 // unrolled steps address them with immediate offsets t, 128 + t, 256 + t: without it the compiler's
 // strength reduction moved the base past the arrays and spent a v_add_u32 per ds_add_f64 (3.5 VALU
@@ -245,6 +272,7 @@ __device__ __forceinline__ void n3b_pair(bool diag, unsigned groups, int l, doub
                                          double mi, const double (*pj)[128], const double* mj, double* ax,
                                          double* ay, double* az, double& fx, double& fy, double& fz,
                                          const PairC& c, const double* nsh = nullptr) {
+    l = lane_opaque(l);
     const int a = l >> 4, m = l & 15;
     if (!diag) {
         for (int d = 0; d < 4; ++d) {
@@ -311,6 +339,7 @@ __device__ __forceinline__ void n3b_group_uf32(int b0, double xi, double yi, dou
 __device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, double xi, double yi, double zi,
                                               const double (*pj)[128], double* ax, double* ay, double* az,
                                               double& fx, double& fy, double& fz, float cf, float invlf, float rc2f) {
+    l = lane_opaque(l);
     const int a = l >> 4, m = l & 15;
     for (int d = 0; d < 4; ++d) {
         if (!((groups >> d) & 1u)) continue;        // wave-uniform
@@ -455,18 +484,34 @@ __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0
 #ifndef MDQT_N3B_WPE                                // waves per SIMD of the fast variant (VGPR budget 512/WPE):
 #define MDQT_N3B_WPE (BW == 8 ? 6 : 8)              // 6 = three 8-wave workgroups per CU (41.5 KB LDS each)
 #endif
+#ifndef MDQT_N3B_DBUF
+#define MDQT_N3B_DBUF 1                             // double-buffered J staging by LDS-DMA (plan path)
+#endif
+// the block kernel's LDS, one object (k_pairs_n3b)
+template <int W>
+struct N3BShared {
+    double pj[2][3][128];                           // J positions by sub-tiles twice over (n3b_lds), 2 buffers
+    double accj[W][3][128];                         // per-wave j accumulators
+    double mjs[2][128];                             // J validity weights: all ones / the ragged last tile's
+    double etab[64];                                // 2^(k/64) (MDQT_EXP_TAB)
+#if MDQT_N3B_IRUN_LDS
+    double irun[W][3][64];                          // the run's i accumulators
+#endif
+    uint2 pw[2][W];                                 // plan words (class, sub-tile groups), 2 buffers
+};
 // AXP: the one-axis per-pair image (n3b_pack_class bits 28-29) in an instance of its own, launched
 // only where such tile pairs can lie inside the skip radius (launch_forces_n3b): compiled into the
 // one instance it cost the calls without any (N = 1M) 0.5 %.
 template <int VARIANT, bool GUARD, bool POT = false, bool AXP = false>
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(VARIANT == 1 ? MDQT_N3B_WPE : 4, VARIANT == 1 ? MDQT_N3B_WPE : 4)))
 void k_pairs_n3b(N3BArgs a) {
-    __shared__ double pj[3][128];
-    __shared__ double mj[128];
-    __shared__ double accj[BW][3][128];
-    __shared__ double etab[64];
+    // all LDS in one object: beside an LDS-DMA (the plan path's J staging) a second __shared__ object
+    // can make the compiler wait for the DMA before unrelated LDS reads (cdna_hip_programming.md §5)
+    __shared__ N3BShared<BW> sh;
+    double* const etab = sh.etab;
     stage_exp_tab(etab);
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;   // q: wave-uniform
+    const int l0 = l;                               // (lane_opaque's fallback)
 #ifndef MDQT_N3B_ORDER
 #define MDQT_N3B_ORDER 1
 #endif
@@ -493,6 +538,10 @@ void k_pairs_n3b(N3BArgs a) {
         const double* p = tile_ptr(I) + l;
         xi = p[0]; yi = p[PS]; zi = p[2 * PS]; mi = 1.;
     }
+    // waited for here, once: as load results the compiler waited vmcnt(0) for them at every pair-form
+    // dispatch (it cannot count past the staging wave's LDS-DMA on the loop's back edge), which retired
+    // the DMA just issued instead of letting it land during the pair work
+    asm volatile("" : "+v"(xi), "+v"(yi), "+v"(zi));
     // Tile-pair classes in spatial order (SpeedUp:222 keeps a pair only below r = L/2), decided
     // for all BW waves' tile pairs (I, J) by the staging wave's lanes 0..BW-1:
     //  * skip (force_sort 1): boxes beyond the skip radius in the minimum image — at L/2 no pair
@@ -507,8 +556,6 @@ void k_pairs_n3b(N3BArgs a) {
     // The forces take them, with the sub-tile groups (tg[q]), from the call's plan (k_n3b_plan: one
     // 8-byte word per tile pair, loaded by lanes 0..15); without a plan (potentials, unsorted order)
     // the staging lanes classify the tile pairs themselves and every group runs in the exact form.
-    __shared__ int tpw[BW];                         // class and uniform-image multiples
-    __shared__ unsigned tg[BW];                     // sub-tile groups by pair form (k_n3b_plan)
     constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
     constexpr bool FARF = VARIANT == 1 && !POT && !GUARD && CUT;   // the error-bounded pair forms
     const N3BRadii rad = n3b_radii<VARIANT, POT>(a);
@@ -521,11 +568,10 @@ void k_pairs_n3b(N3BArgs a) {
     // three-level blocking fits the 64-VGPR budget), or (MDQT_N3B_IRUN_LDS 0) the i-slot itself —
     // each wave's own rows, read, added and written once per block distance, in order
 #if MDQT_N3B_IRUN_LDS
-    __shared__ double irun[BW][3][64];
-    double* fi = irun[q][0] + l;
+    auto fiptr = [&]() { return sh.irun[q][0] + lane_opaque(l0); };
     constexpr size_t FS = 64;
 #else
-    double* fi = a.slots + (size_t)(a.nd + run) * ((size_t)3 * a.Npad) + i;
+    auto fiptr = [&]() { return a.slots + (size_t)(a.nd + run) * ((size_t)3 * a.Npad) + I * 64 + lane_opaque(l0); };
     const size_t FS = a.Npad;
 #endif
     bool fi_first = true;
@@ -537,15 +583,63 @@ void k_pairs_n3b(N3BArgs a) {
     // second, and the accumulators are zero again before the combining waves reach the next one)
     constexpr int kStage = BW - 1;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { accj[q][k][l] = 0.; accj[q][k][l + 64] = 0.; }
-    double* ax = accj[q][0];
-    double* ay = accj[q][1];
-    double* az = accj[q][2];
+    for (int k = 0; k < 3; ++k) { sh.accj[q][k][l] = 0.; sh.accj[q][k][l + 64] = 0.; }
+    double* ax = sh.accj[q][0];
+    double* ay = sh.accj[q][1];
+    double* az = sh.accj[q][2];
+    // the J tile's validity weights (RAGGED pair steps): all ones, or the ragged last tile's pattern —
+    // constant over the launch, written once (a J tile takes mjs[J == T - 1])
+    if (q == kStage) {
+        const int li = n3b_lds(l);
+        const double m1 = (T - 1) * 64 + l < N ? 1. : 0.;
+        sh.mjs[0][li] = 1.; sh.mjs[0][li + 16] = 1.;
+        sh.mjs[1][li] = m1; sh.mjs[1][li + 16] = m1;
+    }
     const size_t plane = (size_t)3 * a.Npad;
     // the plan's J-step masks (after its tile-pair words): bit b = some tile pair of J step b has work
     const unsigned* jsteps = plan ? (const unsigned*)(plan + (size_t)(a.Phi - a.Plo) * a.nd * (BW * BW)) : nullptr;
+    auto half_db = [&](int db) { return !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2; };   // the other half covers it
+    // Double-buffered J staging (MDQT_N3B_DBUF, the plan path): at the top of every J step with work the
+    // staging wave issues the LDS-DMA loads (global_load_lds_dwordx4: J's positions by sub-tiles twice
+    // over, and the step's 8 plan words) of the NEXT step with work into the other buffer, then all waves
+    // compute on this one; the DMA lands during the pair work and is retired by the staging wave's wait
+    // at the step's second barrier.  The first barrier is a raw s_barrier after lgkmcnt(0) (the
+    // combine's zeroing), so the DMA in flight is not drained there.  Without a plan (potentials,
+    // unsorted order) the staging wave loads and classifies J itself before the first barrier.
+    // Rs holds the pad ions' values (k_gather_sorted), so the DMA copies what the register path computes.
+    constexpr bool kDbuf = MDQT_N3B_DBUF != 0;
+    int buf = 0;
+    auto next_step = [&](int db, int b, int& odb, int& ob) {   // the first step with work at or after (db, b)
+        for (; db < d1; ++db, b = 0) {
+            if (half_db(db)) continue;
+            const unsigned msk = jsteps[2 * ((size_t)(P - a.Plo) * a.nd + db)];
+            const int Qn = (P + db) % a.NB;
+            for (; b < BW && Qn * BW + b < T; ++b)
+                if ((msk >> b) & 1u) { odb = db; ob = b; return; }
+        }
+        odb = d1; ob = 0;
+    };
+    auto dma_stage = [&](int bf, int db, int b) {   // (staging wave) J step (db, b) into buffer bf
+        const int J = ((P + db) % a.NB) * BW + b;
+        const int l = lane_opaque(l0);
+        const double* src = a.Rs + (size_t)J * 64 + 16 * (l >> 4) + ((2 * l) & 15);
+        // lanes 0 .. BW/2 - 1: the step's BW plan words, 16 bytes each (an LDS-DMA writes base + 16 x lane
+        // for every active lane, so only those lanes issue it)
+        const uint2* pws = plan + ((size_t)(P - a.Plo) * a.nd + db) * (BW * BW) + b * BW + 2 * (l & (BW / 2 - 1));
+        // every address formed before the first DMA: a spill reload between them would be waited for
+        // with vmcnt(0), retiring the DMA already issued
+        asm volatile("" : "+v"(src), "+v"(pws));
+        if (l < BW / 2) lds_dma16(pws, lds_offset(&sh.pw[bf][0]));
+#pragma unroll
+        for (int c3 = 0; c3 < 3; ++c3) lds_dma16(src + (size_t)c3 * a.Npad, lds_offset(&sh.pj[bf][c3][0]));
+    };
+    if (kDbuf && plan && q == kStage) {             // the launch's first step with work into buffer 0
+        int fdb, fb;
+        next_step(d0, 0, fdb, fb);
+        if (fdb < d1) dma_stage(0, fdb, fb);
+    }
     for (int db = d0; db < d1; ++db) {
-        if (!(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2) continue;   // the other half covers it
+        if (half_db(db)) continue;
         const int Q = (P + db) % a.NB;
         double bx = 0., by = 0., bz = 0.;          // this block distance's i partial (3-level blocking)
         const unsigned* jstep = jsteps ? jsteps + 2 * ((size_t)(P - a.Plo) * a.nd + db) : nullptr;
@@ -555,44 +649,58 @@ void k_pairs_n3b(N3BArgs a) {
             // (the mask re-read every J step — a scalar load — rather than held across the pair loop)
             if (jstep && !((*jstep >> b) & 1u)) {   // every tile pair of this J step skipped (wave-uniform):
                 if (q < (POT ? 1 : 3))              // J's rows get the combine's value, -0, and no barrier
-                    a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? 0. : -0.;
+                    a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + lane_opaque(l0)] = POT ? 0. : -0.;
                 continue;
             }
-            if (q == kStage) {                      // stage J (by sub-tiles, twice over)
-                const int j = J * 64 + l;
-                const bool vj = j < N;
-                const double* p = tile_ptr(J) + l;
-                const double xj = vj ? p[0] : pad, yj = vj ? p[PS] : pad, zj = vj ? p[2 * PS] : pad;
-                const int li = n3b_lds(l);
-                pj[0][li] = xj; pj[0][li + 16] = xj;
-                pj[1][li] = yj; pj[1][li + 16] = yj;
-                pj[2][li] = zj; pj[2][li + 16] = zj;
-                mj[li] = vj ? 1. : 0.; mj[li + 16] = mj[li];
-                if (l < BW) {
-                    if (plan) {                     // (P, db, b): 16 words, one per wave
-                        const uint2 w = plan[((size_t)(P - a.Plo) * a.nd + db) * (BW * BW) + b * BW + l];
-                        tpw[l] = (int)w.x;
-                        tg[l] = w.y;
+            if (kDbuf && plan) {
+                if (q == kStage) {                  // the next step with work into the other buffer
+                    int ndb, nb;
+                    next_step(db, b + 1, ndb, nb);
+                    // this buffer's DMA was retired at the previous step's second barrier, or (the first
+                    // step) it is retired here: everything but the 4 DMA loads just issued
+                    if (ndb < d1) {
+                        dma_stage(buf ^ 1, ndb, nb);
+                        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                     } else {
-                        int w = 2;                  // class 0 (unsorted: every tile pair, per-pair image)
-                        if (srt && P * BW + l < T) {
-                            double g2;
-                            int sm = 0;
-                            w = n3b_pack_class(n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2,
-                                                                          AXP ? &sm : nullptr), sm);
-                        }
-                        tpw[l] = w;
-                        tg[l] = 0xFFu;
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                 }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            } else {
+                if (q == kStage) {                  // stage J (by sub-tiles, twice over)
+                    const int j = J * 64 + l;
+                    const bool vj = j < N;
+                    const double* p = tile_ptr(J) + l;
+                    const double xj = vj ? p[0] : pad, yj = vj ? p[PS] : pad, zj = vj ? p[2 * PS] : pad;
+                    const int li = n3b_lds(l);
+                    sh.pj[buf][0][li] = xj; sh.pj[buf][0][li + 16] = xj;
+                    sh.pj[buf][1][li] = yj; sh.pj[buf][1][li + 16] = yj;
+                    sh.pj[buf][2][li] = zj; sh.pj[buf][2][li + 16] = zj;
+                    if (l < BW) {
+                        if (plan) {                 // (P, db, b): one word per wave
+                            sh.pw[buf][l] = plan[((size_t)(P - a.Plo) * a.nd + db) * (BW * BW) + b * BW + l];
+                        } else {
+                            int w = 2;              // class 0 (unsorted: every tile pair, per-pair image)
+                            if (srt && P * BW + l < T) {
+                                double g2;
+                                int sm = 0;
+                                w = n3b_pack_class(n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2,
+                                                                              AXP ? &sm : nullptr), sm);
+                            }
+                            sh.pw[buf][l] = make_uint2((unsigned)w, 0xFFu);
+                        }
+                    }
+                }
+                __syncthreads();
             }
-            __syncthreads();
-            const int tw = __builtin_amdgcn_readfirstlane(tpw[q]);
+            const double (*pj)[128] = sh.pj[buf];
+            const double* mj = sh.mjs[J == T - 1];
+            const int tw = __builtin_amdgcn_readfirstlane((int)sh.pw[buf][q].x);
             const int cls = (tw & 15) - 2;
             const bool mine = vI && (db > 0 || J >= I);
             const bool diag = (db == 0 && J == I);
             // this wave's sub-tile groups, by pair form (k_n3b_plan)
-            const unsigned word = __builtin_amdgcn_readfirstlane(tg[q]);
+            const unsigned word = __builtin_amdgcn_readfirstlane(sh.pw[buf][q].y);
             const unsigned groups = word & 15u;
             if (mine && cls >= 0 && groups) {
                 const int ci = cls;                 // bit 0 uniform image (the tile pair's)
@@ -697,17 +805,20 @@ void k_pairs_n3b(N3BArgs a) {
                                                                      tx, ty, tz, c);
                 bx += tx; by += ty; bz += tz;
             }
+            if (kDbuf && plan && q == kStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA retired
             __syncthreads();
+            if (kDbuf && plan) buf ^= 1;
             if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db
+                const int l = lane_opaque(l0);
                 const int li = n3b_lds(l);
                 // the 16 waves' two copies, summed as a fixed pairwise tree (dependency depth 5,
                 // not 16), then zeroed for the next J step
                 double s16[BW];
 #pragma unroll
                 for (int w = 0; w < BW; ++w) {
-                    s16[w] = accj[w][q][li] + accj[w][q][li + 16];
-                    accj[w][q][li] = 0.;
-                    accj[w][q][li + 16] = 0.;
+                    s16[w] = sh.accj[w][q][li] + sh.accj[w][q][li + 16];
+                    sh.accj[w][q][li] = 0.;
+                    sh.accj[w][q][li + 16] = 0.;
                 }
 #pragma unroll
                 for (int h = BW / 2; h >= 1; h /= 2)
@@ -717,6 +828,7 @@ void k_pairs_n3b(N3BArgs a) {
             }
         }
         if (vI) {                                   // (0 + bx: the first block distance's partial as is)
+            double* fi = fiptr();
             fi[0] = fi_first ? 0. + bx : fi[0] + bx;
             fi[FS] = fi_first ? 0. + by : fi[FS] + by;
             fi[2 * FS] = fi_first ? 0. + bz : fi[2 * FS] + bz;
@@ -724,7 +836,8 @@ void k_pairs_n3b(N3BArgs a) {
         fi_first = false;
     }
     if (vI) {                                       // i side -> i-slot nd + run
-        double* o = a.slots + (size_t)(a.nd + run) * plane + i;
+        double* fi = fiptr();
+        double* o = a.slots + (size_t)(a.nd + run) * plane + I * 64 + lane_opaque(l0);
         const double r0 = fi_first ? 0. : fi[0], r1 = fi_first ? 0. : fi[FS], r2 = fi_first ? 0. : fi[2 * FS];
         if (MDQT_N3B_IRUN_LDS || fi_first) { o[0] = r0; o[a.Npad] = r1; o[2 * (size_t)a.Npad] = r2; }
     }

@@ -79,8 +79,9 @@ __global__ __launch_bounds__(256) void k_gather_sorted(const double* __restrict_
         Rs[t] = p[0];
         Rs[(size_t)Npad + t] = p[S];
         Rs[2 * (size_t)Npad + t] = p[2 * (size_t)S];
-    } else {                                               // padding of the ragged last tile
-        Rs[t] = 0.; Rs[(size_t)Npad + t] = 0.; Rs[2 * (size_t)Npad + t] = 0.;
+    } else {                                               // padding of the ragged last tile: the block
+        const double pad = (double)((t & 63) + 1) * 0x1p-10;   // kernel's pad ions (distinct points, weight 0),
+        Rs[t] = pad; Rs[(size_t)Npad + t] = pad; Rs[2 * (size_t)Npad + t] = pad;   // staged as they are
     }
 }
 

@@ -157,6 +157,7 @@ struct mdqt_ctx {
     double* dBoxes = nullptr;      // [12][T] tile boxes, raw coordinate bounds
     double* dSubBoxes = nullptr;   // [6][4T] the 16-ion sub-tiles' boxes (the block kernel's sub-tile groups)
     uint2* dPlan = nullptr;        // [(Phi - Plo) nd][256] the block kernel's tile-pair words (k_n3b_plan)
+    int tmask_mode = 1;            // option force_reduce_mask: k_n3b_reduce reads only the j-slots written
     size_t capPlan = 0;
     int capSortN = 0;
     // overlapped MD step (option "overlap", OFF by default — measured slower): the
@@ -919,6 +920,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_scheme")) return s->use_n3b ? 3 : s->use_n3 ? 2 : 1;
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
     if (!strcmp(n, "force_ax1")) return s->ax1_mode;
+    if (!strcmp(n, "force_reduce_mask")) return s->tmask_mode;
     if (!strcmp(n, "force_skip_radius") || !strcmp(n, "force_tail_bound")) {   // the tile-pair skip radius
         double bound;                                  // and its force bound (0: exact, r = L/2)
         const double r = (s->use_n3b && s->sort_mode == 1) ? skip_radius(s, &bound) : (bound = 0., s->L / 2.);
@@ -1401,6 +1403,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
     a.micGuard = c.micGuard; a.guard = c.guard;
     a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr; a.subboxes = nullptr; a.plan = nullptr;
+    a.tmask = nullptr; a.tmw = 0;
     a.ax1 = s->ax1_mode;
     double bound;
     a.Rskip = skip_radius(s, &bound);
@@ -1424,7 +1427,11 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
         a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes; a.subboxes = s->dSubBoxes;
         if (tail_measured(s) && a.Rskip < a.Rcut) a.tailb = s->dTail;
         // the plan (k_n3b_plan): 256 tile-pair words per (P, db), then one J-step mask per (P, db)
-        const size_t need = (size_t)std::max(a.Phi - a.Plo, 0) * a.nd * (kN3BBlock * kN3BBlock + 1);
+        // and the per-J-tile masks of the block distances whose j-slots the block kernel writes (k_n3b_reduce
+        // reads only those): T x ceil(nd / 64) words
+        const size_t nplan = (size_t)std::max(a.Phi - a.Plo, 0) * a.nd * (kN3BBlock * kN3BBlock + 1);
+        const int tmw = (a.nd + 63) / 64;
+        const size_t need = nplan + (size_t)a.T * tmw;
         if (need > s->capPlan) {
             if (s->dPlan) HIPCHK(hipFree(s->dPlan));
             s->dPlan = nullptr;
@@ -1432,6 +1439,8 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
             s->capPlan = need;
         }
         a.plan = s->dPlan;
+        a.tmw = s->tmask_mode ? tmw : 0;
+        a.tmask = s->tmask_mode ? (unsigned long long*)(s->dPlan + nplan) : nullptr;
     }
     return 0;
 }
@@ -2784,6 +2793,12 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (value < 0 || value > 1) return fail("force_tail_mode must be 0 (a priori) or 1 (measured)");
         if (value != s->tail_mode && (settle_forces(s) || tail_reset(s))) return -1;
         s->tail_mode = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_reduce_mask")) {          // Newton-3 blocks: the reduction reads only written j-slots
+        if (value < 0 || value > 1) return fail("force_reduce_mask must be 0 (every j-slot) or 1 (the written ones)");
+        if (settle_forces(s)) return -1;
+        s->tmask_mode = value;
         return 0;
     }
     if (!strcmp(name, "force_ax1")) {                  // Newton-3 blocks: the one-axis per-pair image instance

@@ -648,9 +648,9 @@ void k_pairs_n3b(N3BArgs a) {
             if (J >= T) break;
             // (the mask re-read every J step — a scalar load — rather than held across the pair loop)
             if (jstep && !((*jstep >> b) & 1u)) {   // every tile pair of this J step skipped (wave-uniform):
-                if (q < (POT ? 1 : 3))              // J's rows get the combine's value, -0, and no barrier
+                if (q < (POT ? 1 : 3) && !a.tmask)  // J's rows get the combine's value, -0, and no barrier (with
                     a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + lane_opaque(l0)] = POT ? 0. : -0.;
-                continue;
+                continue;                           // the reduction's masks: nothing, the slot is not read)
             }
             if (kDbuf && plan) {
                 if (q == kStage) {                  // the next step with work into the other buffer
@@ -1136,6 +1136,9 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
     }
     __syncthreads();
     if (t == 0) plan[(size_t)(a.Phi - a.Plo) * a.nd * (BW * BW) + (size_t)Pl * a.nd + db] = make_uint2(jm, 0u);
+    // the reduction's per-J-tile masks: J step b has work -> the block kernel writes J's j-slot db
+    if (a.tmask && t < BW && ((jm >> t) & 1u))
+        atomicOr(a.tmask + (size_t)(Q * BW + t) * a.tmw + (db >> 6), 1ull << (db & 63));
     if (tmeas) {
         if (t < 4 * BW) {
             const int k = t >> 2, u = t & 3;
@@ -1147,6 +1150,10 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
 
 // canonical per-ion sum of the slots this rank wrote: j-slots db = 0 .. nd-1, then i-slots.
 // out: world 1 -> F [3][S]; sharded -> the rank's dense partial [world][3][S] (reduce-scattered)
+// With the plan's per-J-tile masks (a.tmask) only the j-slots the block kernel wrote are read — the
+// others held the -0 of empty J steps, and acc + -0 = acc: the same sum, bit for bit, without ~2/3 of
+// the reads at N = 1M.  The masks are wave-uniform (a wave is one J tile): 8 slot loads in flight per
+// round, added in ascending db order.
 __global__ __launch_bounds__(256) void k_n3b_reduce(N3BArgs a, double* __restrict__ out) {
     const int g = blockIdx.x * 256 + threadIdx.x;
     const int k = blockIdx.y;
@@ -1155,10 +1162,31 @@ __global__ __launch_bounds__(256) void k_n3b_reduce(N3BArgs a, double* __restric
     const size_t plane = (size_t)3 * a.Npad;
     const double* p = a.slots + (size_t)k * a.Npad + g;
     double acc = 0.;
-    for (int db = 0; db < a.nd; ++db) {
-        const int P = (B - db + a.NB) % a.NB;
-        const bool skip = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
-        if (!skip && P >= a.Plo && P < a.Phi) acc = acc + p[(size_t)db * plane];
+    if (a.tmask) {
+        const unsigned long long* tm = a.tmask + (size_t)(g >> 6) * a.tmw;
+        for (int w = 0; w < a.tmw; ++w) {
+            unsigned long long m = __builtin_amdgcn_readfirstlane((unsigned)tm[w]) |
+                                   ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(tm[w] >> 32)) << 32);
+            while (m) {
+                int idx[8];
+                int n = 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (m) { idx[u] = 64 * w + __builtin_ctzll(m); m &= m - 1; n = u + 1; }
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = u < n ? p[(size_t)idx[u] * plane] : 0.;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (u < n) acc = acc + v[u];
+            }
+        }
+    } else {
+        for (int db = 0; db < a.nd; ++db) {
+            const int P = (B - db + a.NB) % a.NB;
+            const bool skip = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
+            if (!skip && P >= a.Plo && P < a.Phi) acc = acc + p[(size_t)db * plane];
+        }
     }
     if (B >= a.Plo && B < a.Phi)
         for (int r = 0; r < a.R; ++r) acc = acc + p[(size_t)(a.nd + r) * plane];
@@ -1253,6 +1281,8 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     const int nplan = (a.Phi - a.Plo) * a.nd;
     if (a.plan && nplan > 0) {
         if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // spatial order only
+        if (a.tmask && hipMemsetAsync(a.tmask, 0, (size_t)a.T * a.tmw * sizeof(unsigned long long), s) != hipSuccess)
+            return hipGetLastError();
         if (variant == 1) {
             if (a.guard) hipLaunchKernelGGL((k_n3b_plan<1, true>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
             else hipLaunchKernelGGL((k_n3b_plan<1, false>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
@@ -1321,7 +1351,9 @@ hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipS
             else hipLaunchKernelGGL((k_pairs_n3b<0, false, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
         }
     }
-    hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 1), dim3(256), 0, s, a, out);   // component 0
+    N3BArgs r = a;                                  // (no plan: every j-slot written, every one read)
+    r.tmask = nullptr;
+    hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 1), dim3(256), 0, s, r, out);   // component 0
     return hipGetLastError();
 }
 

@@ -445,6 +445,8 @@ struct N3BArgs {
                         // [(Phi - Plo) nd] J-step masks (.x), written by k_n3b_plan (launch_forces_n3b)
                         // and read by k_pairs_n3b; nullptr: classified in the block kernel (every
                         // sub-tile group exact; no tail sums)
+    unsigned long long* tmask;   // with a plan: [T][tmw] bit db of J tile's words = the block kernel wrote J's
+    int tmw;                     // j-slot db (a J step with work); k_n3b_reduce reads only those (nullptr: all)
 };
 struct SortArgs {
     const double* Rall; // gathered positions [world][3][S]

@@ -531,3 +531,57 @@ def test_exp2f_error_within_the_ultra_far_bound():
     err = float(re.search(r"exp2f: ([0-9.e+-]+)", out).group(1))
     print(out.strip())
     assert err <= 2.0 ** -22
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_masked_reduction_bit_identical(world):
+    """k_n3b_reduce with the plan's per-J-tile masks (force_reduce_mask 1, the default) reads only the
+    j-slots the block kernel wrote and skips the -0 of empty J steps: F bit for bit the same as reading
+    every slot (option 0), at world 1 and in a world-2 in-process group (N0 = 250,000: the tail radius
+    and the ultra-far tiers leave ~2/3 of the J steps empty at the far block distances)"""
+    import mdqtplasmasims_amd as M
+    from mdqtplasmasims_amd.engine import comm_init_local
+    kw = dict(N0=250000, detuningDP=1.0, seed=SEED, job=1)
+    ref = M.Simulation(**kw).init()
+    st = ref.get_state()
+    ref.close()
+    out = {}
+    for mode in (1, 0):
+        sims = [M.Simulation(world_size=world, rank=r, **kw) for r in range(world)]
+        for s in sims:
+            s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+            s.set_option("force_reduce_mask", mode)
+            assert s.const("force_reduce_mask") == mode
+        if world > 1:
+            comm_init_local(sims)
+            for s in sims:
+                s.allgather_positions()
+        for s in sims:
+            s.forces()
+        F = np.zeros_like(st["R"])
+        for s in sims:
+            lo, hi = s.slab_bounds()
+            F[:, lo:hi] = s.get_state()["F"][:, lo:hi]
+            s.close()
+        out[mode] = F
+    assert np.array_equal(out[1], out[0])
+
+
+@pytest.mark.gpu
+def test_block_work_sums_to_the_census():
+    """mdqt_force_block_work (the load-balance census): one entry per block, summing to the census's
+    evaluated lane-steps; at world 2 each rank's blocks are its half of the world-1 array"""
+    import mdqtplasmasims_amd as M
+    kw = dict(N0=100000, Ge=1.0 / 12, qt_enabled=0, seed=SEED, job=1)
+    s = M.Simulation(**kw).init()
+    w = s.force_block_work()
+    cen = s.force_census()
+    ev = sum(v[0] for k, v in cen.items() if not k.startswith("skip"))
+    assert len(w) == int(s.const("n3b_block_count")) and w.min() > 0
+    assert w.sum() == ev
+    NB = len(w)
+    print(f"C3 blocks {NB}: per-block evaluated lane-steps min/mean/max {w.min() / w.mean():.3f} / 1 / "
+          f"{w.max() / w.mean():.3f}; world-8 partition max/mean "
+          f"{max(w[r * NB // 8:(r + 1) * NB // 8].sum() for r in range(8)) / (w.sum() / 8):.4f}")
+    s.close()

@@ -642,12 +642,13 @@ void k_pairs_n3b(N3BArgs a) {
         if (half_db(db)) continue;
         const int Q = (P + db) % a.NB;
         double bx = 0., by = 0., bz = 0.;          // this block distance's i partial (3-level blocking)
-        const unsigned* jstep = jsteps ? jsteps + 2 * ((size_t)(P - a.Plo) * a.nd + db) : nullptr;
+        // the block distance's J-step mask, read once and held in an SGPR (wave-uniform; read per J step
+        // it was a vector load and a vmcnt(0) wait at the top of every step)
+        const unsigned jmask = jsteps ? __builtin_amdgcn_readfirstlane(jsteps[2 * ((size_t)(P - a.Plo) * a.nd + db)]) : ~0u;
         for (int b = 0; b < BW; ++b) {
             const int J = Q * BW + b;
             if (J >= T) break;
-            // (the mask re-read every J step — a scalar load — rather than held across the pair loop)
-            if (jstep && !((*jstep >> b) & 1u)) {   // every tile pair of this J step skipped (wave-uniform):
+            if (jsteps && !((jmask >> b) & 1u)) {   // every tile pair of this J step skipped (wave-uniform):
                 if (q < (POT ? 1 : 3) && !a.tmask)  // J's rows get the combine's value, -0, and no barrier (with
                     a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + lane_opaque(l0)] = POT ? 0. : -0.;
                 continue;                           // the reduction's masks: nothing, the slot is not read)

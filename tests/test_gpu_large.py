@@ -304,7 +304,7 @@ CLUSTERED = {"70k": (70000, 4, 0.5, 2.0), "1M": (1000000, 12, 0.2, 12.0)}
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["70k", "1M"])
-def test_tail_bound_enforced_on_clustered_ions(cfg):
+def test_tail_bound_enforced_on_clustered_ions(cfg, orc):
     """force_tail_mode 1 on a configuration the density model gets wrong: a dense ball of ions.
     The skip radius r_t the model picks leaves some tiles with a tail sum over eps; the engine must
     catch it — k_tail_fix recomputes those tiles' forces exactly, so EVERY ion's force stays within
@@ -343,8 +343,13 @@ def test_tail_bound_enforced_on_clustered_ions(cfg):
     fixed_b = s.const("force_tail_fixed_tiles") - fixed
     print(f"{cfg}: at r_t {rt1:.3f}: tiles over eps {fixed_b:.0f}, bound {s.const('force_tail_bound'):.3e}")
     assert s.const("force_tail_bound") <= eps
-    # C: the tail alone (far forms off), from the model's radius again (set_state resets the scale)
+    # new positions of the same system keep the widened radius (a driver that uploads R every MD step
+    # does not rerun the exact pass at every call)
     s.set_state(*state)
+    assert s.const("force_skip_radius") == rt1
+    # C: the tail alone (far forms off), from the model's radius again (a tail option resets the scale)
+    s.set_option("force_tail_mode", 0)
+    s.set_option("force_tail_mode", 1)
     for o in ("force_mid_exp", "force_far_exp", "force_vfar_exp", "force_ufar_exp"):
         s.set_option(o, 0)
     assert s.const("force_skip_radius") == rt0
@@ -378,6 +383,16 @@ def test_tail_bound_enforced_on_clustered_ions(cfg):
     assert sharp.mean() > 0.5
     assert np.all(d["C"] <= eps + rnd)
     assert np.all(d["A"] <= eps + fb + rnd) and np.all(d["B"] <= eps + fb + rnd)
+    # the ions where that check is not sharp (the ball: the exact pass's tiles), against the oracle's
+    # compensated rows instead of the engine's exact mode, so that only A's own rounding is allowed
+    # (ADVICE r04): within eps + the far bounds + 1e-15 P_i of the compensated sum
+    loose = np.flatnonzero(~sharp)
+    idx = np.sort(np.random.default_rng(7).choice(loose, min(256, len(loose)), replace=False))
+    G = orc.forces_index(R, idx, L, lD, nthreads=threads())
+    dA = np.abs(out["A"][:, idx] - G).max(axis=0)
+    print(f"{cfg}: {len(idx)} of the {len(loose)} ball ions against the compensated oracle: max |dF_i| {dA.max():.3e}, "
+          f"max |dF_i| / P_i {(dA / P[idx]).max():.2e}")
+    assert np.all(dA <= eps + fb + rnd[idx])
 
 
 @pytest.mark.gpu
@@ -414,6 +429,42 @@ def test_tail_bound_enforced_in_sharded_local_group():
     assert worst < 1e-13
     assert counts[0] == counts[1] == ref.const("force_tail_fixed_tiles") > 0
     assert sims[0].const("force_skip_radius") == sims[1].const("force_skip_radius") == ref.const("force_skip_radius")
+    for x in sims:
+        x.close()
+    ref.close()
+
+
+@pytest.mark.gpu
+def test_tail_option_change_between_forces_and_reduce():
+    """a tail option changed on one rank of an in-process group after forces() and before
+    the deferred reduce must not drop the enforcement — set_option settles the pending partials first
+    (with the eps they were measured for), so both ranks still match world 1"""
+    import mdqtplasmasims_amd as M
+    from mdqtplasmasims_amd.engine import comm_init_local
+    N0, k, frac, rc = CLUSTERED["70k"]
+    ref = M.Simulation(N0=N0, seed=SEED, rng_mode=1)
+    state = clustered_state(N0, ref.const("L"), frac, rc)
+    ref.set_state(*state)
+    ref.set_option("force_tail_exp", k)
+    ref.forces()
+    G = ref.get_state()["F"]
+    assert ref.const("force_tail_fixed_tiles") > 0
+    sims = [M.Simulation(N0=N0, seed=SEED, rng_mode=1, world_size=2, rank=r) for r in range(2)]
+    for x in sims:
+        x.set_state(*state)
+        x.set_option("force_tail_exp", k)
+    comm_init_local(sims)
+    for x in sims:
+        x.allgather_positions()
+    for x in sims:
+        x.forces()
+    sims[0].set_option("force_tail_exp", k + 1)        # between forces() and the reduce
+    worst = 0.0
+    for x in sims:
+        lo, hi = x.slab_bounds()
+        worst = max(worst, np.abs(x.get_state()["F"][:, lo:hi] - G[:, lo:hi]).max() / np.abs(G).max())
+    print(f"tail option changed before the reduce: world 2 vs 1 max|dF|/max|F| = {worst:.3e}")
+    assert worst < 1e-13
     for x in sims:
         x.close()
     ref.close()

@@ -11,6 +11,8 @@
 // tiles; the MC + MD program, whose lattice start puts pairs exactly on the cutoff and on the
 // image boundary) has variant 1's values with variant 0's pair set: the exact minimum image and
 // the cutoff as r2 < rc2, rc2 the smallest double with sqrt(rc2) >= Rcut.
+#include <vector>
+#include <cstdio>
 #include "mdqt_internal.hpp"
 #include "mdqt_pairs.hpp"
 
@@ -1166,8 +1168,9 @@ __global__ __launch_bounds__(256) void k_n3b_reduce(N3BArgs a, double* __restric
     if (a.tmask) {
         const unsigned long long* tm = a.tmask + (size_t)(g >> 6) * a.tmw;
         for (int w = 0; w < a.tmw; ++w) {
-            unsigned long long m = __builtin_amdgcn_readfirstlane((unsigned)tm[w]) |
-                                   ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(tm[w] >> 32)) << 32);
+            // (readfirstlane returns int: each half zero-extended, not sign-extended)
+            unsigned long long m = (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)tm[w]) |
+                                   ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(tm[w] >> 32)) << 32);
             while (m) {
                 int idx[8];
                 int n = 0;
@@ -1313,6 +1316,29 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
         if (hipEventRecord(ev0, s) != hipSuccess || hipEventRecord(ev1, s) != hipSuccess) return hipGetLastError();
     }
     hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, a, out);
+#if defined(MDQT_EXPT_TMASK_DEBUG)
+    if (a.plan && a.tmask) {                        // diagnostic build: the masks' bit counts
+        (void)hipStreamSynchronize(s);
+        const size_t nj = (size_t)(a.Phi - a.Plo) * a.nd;
+        std::vector<uint2> js(nj);
+        std::vector<unsigned long long> tm((size_t)a.T * a.tmw);
+        (void)hipMemcpy(js.data(), a.plan + nj * (BW * BW), nj * sizeof(uint2), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(tm.data(), a.tmask, tm.size() * 8, hipMemcpyDeviceToHost);
+        long cj = 0, ct = 0, miss = 0;
+        for (size_t k = 0; k < nj; ++k) cj += __builtin_popcount(js[k].x);
+        for (auto v : tm) ct += __builtin_popcountll(v);
+        for (size_t k = 0; k < nj; ++k) {
+            const int P = a.Plo + (int)(k / a.nd), db = (int)(k % a.nd), Q = (P + db) % a.NB;
+            for (int b = 0; b < BW; ++b)
+                if ((js[k].x >> b) & 1u) {
+                    const int J = Q * BW + b;
+                    if (!((tm[(size_t)J * a.tmw + (db >> 6)] >> (db & 63)) & 1ull)) ++miss;
+                }
+        }
+        fprintf(stderr, "tmask debug: jstep bits %ld, tmask bits %ld, jstep bits missing in tmask %ld (T %d tmw %d nd %d NB %d)\n",
+                cj, ct, miss, a.T, a.tmw, a.nd, a.NB);
+    }
+#endif
     return hipGetLastError();
 }
 

@@ -200,6 +200,10 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     kernel instance of its own, launched where the skip radius reaches within
  *                     two tile widths of L/2 (C3, C5); 0 = the per-pair image on all three axes.
  *                     Forces agree to rounding (1e-13 of max |F|)
+ *   "force_reduce_mask": block pairs in spatial order: 1 (default) = the slot reduction reads only the
+ *                     j-slots the block kernel wrote (per-J-tile masks of the block distances whose J
+ *                     step has work, from the plan), 0 = every j-slot (empty J steps write -0).  Bit
+ *                     for bit the same forces (acc + -0 = acc)
  *   "force_tail_exp": block pairs in spatial order: tile pairs whose boxes are >= r_t apart are
  *                     skipped with every ion's force kept within eps = 10^-k of the exact sum to
  *                     L/2 (g(r) = one pair's |F| at distance r, SpeedUp:224); k = 12 default, 0 =
@@ -213,7 +217,8 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     (all pairs to L/2), so eps holds for any configuration; when that happened
  *                     the next host sync widens r_t (stderr says so).  "force_tail_bound" = the
  *                     largest sub-tile sum of the other tiles over the measured calls (NaN before
- *                     one; reset with the state, N or these options), "force_tail_raw_bound" the
+ *                     one; reset with new positions, N or these options — new positions of the same N
+ *                     keep the widened r_t), "force_tail_raw_bound" the
  *                     largest of all, "force_tail_fixed_tiles" the tiles recomputed so far,
  *                     "force_tail_model_bound" the model's sum at r_t.  0 = a priori:
  *                     r_t the smallest radius with (N - 1) g(r_t) <= eps, "force_tail_bound" that

@@ -387,6 +387,8 @@ def test_tail_bound_enforced_on_clustered_ions(cfg, orc):
     # compensated rows instead of the engine's exact mode, so that only A's own rounding is allowed
     # (ADVICE r04): within eps + the far bounds + 1e-15 P_i of the compensated sum
     loose = np.flatnonzero(~sharp)
+    if not len(loose):                                  # (eps 1e-4 at 70k: every ion's check is sharp)
+        return
     idx = np.sort(np.random.default_rng(7).choice(loose, min(256, len(loose)), replace=False))
     G = orc.forces_index(R, idx, L, lD, nthreads=threads())
     dA = np.abs(out["A"][:, idx] - G).max(axis=0)

@@ -616,6 +616,7 @@ def test_masked_reduction_bit_identical(world):
         for s in sims:
             lo, hi = s.slab_bounds()
             F[:, lo:hi] = s.get_state()["F"][:, lo:hi]
+        for s in sims:                                  # (after every rank's reduce: they share partials)
             s.close()
         out[mode] = F
     assert np.array_equal(out[1], out[0])

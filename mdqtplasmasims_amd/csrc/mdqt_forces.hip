@@ -486,8 +486,12 @@ __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0
 #ifndef MDQT_N3B_WPE                                // waves per SIMD of the fast variant (VGPR budget 512/WPE):
 #define MDQT_N3B_WPE (BW == 8 ? 6 : 8)              // 6 = three 8-wave workgroups per CU (41.5 KB LDS each)
 #endif
+// double-buffered J staging by LDS-DMA (plan path), one step ahead.  Measured (round 5, force-call A/B,
+// 2 alternations, tools/gpu/r05_ab.sh): slower than the synchronous staging — C3 6.585 vs 6.54 ms, C5
+// 31.93 vs 31.73, N = 1M 205.1 vs 203.0: the J-step barrier wait is the waves' unequal pair work, not
+// the staging load.  Off by default, kept as an option
 #ifndef MDQT_N3B_DBUF
-#define MDQT_N3B_DBUF 1                             // double-buffered J staging by LDS-DMA (plan path)
+#define MDQT_N3B_DBUF 0
 #endif
 // the block kernel's LDS, one object (k_pairs_n3b)
 template <int W>

@@ -158,6 +158,10 @@ struct mdqt_ctx {
     double* dSubBoxes = nullptr;   // [6][4T] the 16-ion sub-tiles' boxes (the block kernel's sub-tile groups)
     uint2* dPlan = nullptr;        // [(Phi - Plo) nd][256] the block kernel's tile-pair words (k_n3b_plan)
     int tmask_mode = 1;            // option force_reduce_mask: k_n3b_reduce reads only the j-slots written
+    int balance_opt = 1;           // option force_balance: sharded block ranges by census weight (1) or count (0)
+    bool balanced = false;         // the block ranges of this N have been weighted (n3b_balance)
+    double balance_ratio = NAN;    // max / mean of the ranks' evaluated lane-steps (the weighted ranges)
+    double balance_ratio_eq = NAN; // the same for the equal-count ranges
     size_t capPlan = 0;
     int capSortN = 0;
     // overlapped MD step (option "overlap", OFF by default — measured slower): the
@@ -617,6 +621,22 @@ extern "C" int mdqt_slab(int N, int world, int rank, int* lo, int* hi, int* S) {
     return 0;
 }
 
+// this rank's blocks [lo, hi) of the Newton-3 block kernel and its runs: up to 65,536 workgroups per rank
+// (runs of one or a few block distances, dispatched run-major: a short last round; A/B with 8-tile
+// blocks: N = 1M -1.2 % vs 16,384, C3 and C5 flat)
+static void n3b_set_range(N3BArgs& b, int lo, int hi) {
+    b.Plo = lo;
+    b.Phi = hi;
+    const int nblk = std::max(b.Phi - b.Plo, 1);
+    static const int wg_target = [] {               // (A/B experiments: MDQT_N3B_WG workgroups per rank)
+        const char* e = getenv("MDQT_N3B_WG");
+        return e && atoi(e) > 0 ? atoi(e) : 65536;
+    }();
+    int R = std::min(b.nd, (wg_target + nblk - 1) / nblk);
+    b.runlen = (b.nd + R - 1) / R;
+    b.R = (b.nd + b.runlen - 1) / b.runlen;
+}
+
 // j segmentation of the force sum: a function of N only (partition invariance across world
 // sizes); enough (row x segment) threads to fill 256 CUs at small N, segments >= 64 ions.
 static void choose_segments(mdqt_ctx* s) {
@@ -653,18 +673,8 @@ static void choose_segments(mdqt_ctx* s) {
         b.N = N; b.T = nt; b.Npad = nt * 64;
         b.NB = (nt + kN3BBlock - 1) / kN3BBlock;
         b.nd = b.NB / 2 + 1;
-        b.Plo = (int)((long)s->p.rank * b.NB / W);
-        b.Phi = (int)((long)(s->p.rank + 1) * b.NB / W);
-        const int nblk = std::max(b.Phi - b.Plo, 1);
-        // up to 65,536 workgroups per rank (runs of one or a few block distances, dispatched run-major:
-        // a short last round; A/B with 8-tile blocks: N = 1M -1.2 % vs 16,384, C3 and C5 flat)
-        static const int wg_target = [] {           // (A/B experiments: MDQT_N3B_WG workgroups per rank)
-            const char* e = getenv("MDQT_N3B_WG");
-            return e && atoi(e) > 0 ? atoi(e) : 65536;
-        }();
-        int R = std::min(b.nd, (wg_target + nblk - 1) / nblk);
-        b.runlen = (b.nd + R - 1) / R;
-        b.R = (b.nd + b.runlen - 1) / b.runlen;
+        n3b_set_range(b, (int)((long)s->p.rank * b.NB / W), (int)((long)(s->p.rank + 1) * b.NB / W));
+        s->balanced = false;
     }
 }
 
@@ -921,6 +931,11 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
     if (!strcmp(n, "force_ax1")) return s->ax1_mode;
     if (!strcmp(n, "force_reduce_mask")) return s->tmask_mode;
+    if (!strcmp(n, "force_balance")) return s->balance_opt;
+    if (!strcmp(n, "force_balance_ratio")) return s->balance_ratio;           // max / mean rank work (NaN: not sharded yet)
+    if (!strcmp(n, "force_balance_ratio_equal")) return s->balance_ratio_eq;  // the same for equal block counts
+    if (!strcmp(n, "n3b_block_lo")) return s->use_n3b ? s->n3b.Plo : 0;
+    if (!strcmp(n, "n3b_block_hi")) return s->use_n3b ? s->n3b.Phi : 0;
     if (!strcmp(n, "force_skip_radius") || !strcmp(n, "force_tail_bound")) {   // the tile-pair skip radius
         double bound;                                  // and its force bound (0: exact, r = L/2)
         const double r = (s->use_n3b && s->sort_mode == 1) ? skip_radius(s, &bound) : (bound = 0., s->L / 2.);
@@ -1568,6 +1583,62 @@ extern "C" int mdqt_force_block_work(mdqt_ctx* s, double* out, int n, int* nbloc
     return 0;
 }
 
+// Sharded Newton-3 blocks: the ranks' block ranges by work.  The blocks' evaluated
+// lane-steps vary several-fold along the Hilbert order (N = 1M: 0.49 .. 1.52 of the mean), and equal
+// block counts left world 8 at 1.13 x the mean work on its busiest rank (world 2 and 4: 1.002;
+// profiles/r05a_load_balance.json).  Once per size, at the first sharded force call (positions
+// gathered): the census of EVERY block (k_n3b_census; integer counts, so every rank computes the same
+// numbers from the same positions), then rank r takes the blocks [c_r, c_r+1) whose prefix work is
+// nearest r / W of the total.  Any partition covers every block pair exactly once (the ownership is by
+// P alone; tests/test_n3b_protocol.py); only the partial sums' order changes with it.
+static int n3b_balance(mdqt_ctx* s) {
+    const int W = s->p.world_size;
+    if (s->balanced || W == 1 || !s->use_n3b || !s->sort_mode) return 0;
+    s->balanced = true;
+    N3BArgs& b = s->n3b;
+    const int NB = b.NB;
+    if (NB < W) return 0;
+    N3BArgs a;
+    if (n3b_args(s, a)) return -1;                  // (the spatial order and boxes of these positions)
+    a.Plo = 0; a.Phi = NB;
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc(&d, (2 * kCensus + (size_t)NB) * sizeof(unsigned long long)));
+    std::vector<unsigned long long> w((size_t)NB);
+    hipError_t e = launch_n3b_census(a, d, s->stream, d + 2 * kCensus);
+    if (e == hipSuccess) e = hipMemcpyAsync(w.data(), d + 2 * kCensus, (size_t)NB * sizeof(unsigned long long),
+                                            hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail("force balance census: %s", hipGetErrorString(e));
+    std::vector<double> pre((size_t)NB + 1, 0.);
+    for (int k = 0; k < NB; ++k) pre[k + 1] = pre[k] + (double)w[k];
+    const double tot = pre[NB];
+    std::vector<int> cut((size_t)W + 1, 0);
+    cut[W] = NB;
+    for (int r = 1; r < W; ++r) {
+        const double t = tot * r / W;
+        int k = (int)(std::lower_bound(pre.begin(), pre.end(), t) - pre.begin());   // pre[k] >= t
+        if (k > 0 && t - pre[k - 1] < pre[k] - t) --k;                             // the nearer boundary
+        cut[r] = std::min(std::max(k, cut[r - 1] + 1), NB - (W - r));               // >= 1 block per rank
+    }
+    auto ratio = [&](const std::vector<int>& c) {
+        double mx = 0.;
+        for (int r = 0; r < W; ++r) mx = std::max(mx, pre[c[r + 1]] - pre[c[r]]);
+        return tot > 0. ? mx / (tot / W) : 1.;
+    };
+    std::vector<int> eq((size_t)W + 1);
+    for (int r = 0; r <= W; ++r) eq[r] = (int)((long)r * NB / W);
+    s->balance_ratio_eq = ratio(eq);
+    if (s->balance_opt) {
+        s->balance_ratio = ratio(cut);
+        n3b_set_range(b, cut[s->p.rank], cut[s->p.rank + 1]);
+        if (ensure_aux(s)) return -1;               // (the runs, hence the i-slots, follow the range)
+    } else {
+        s->balance_ratio = s->balance_ratio_eq;
+    }
+    return 0;
+}
+
 extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:192-236
     if (!s) return fail("NULL context");
     if (s->nloc == 0) return 0;
@@ -1596,6 +1667,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         s->f_pending = !one_slot;  // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots;
     } else if (s->use_n3b) {
+        if (n3b_balance(s)) return -1;
         N3BArgs a;
         if (n3b_args(s, a)) return -1;
         const int W = s->p.world_size;
@@ -2793,6 +2865,20 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (value < 0 || value > 1) return fail("force_tail_mode must be 0 (a priori) or 1 (measured)");
         if (value != s->tail_mode && (settle_forces(s) || tail_reset(s))) return -1;
         s->tail_mode = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_balance")) {              // sharded Newton-3 blocks: ranges by work (1) or by count (0)
+        if (value < 0 || value > 1) return fail("force_balance must be 0 (equal block counts) or 1 (by work)");
+        if (value != s->balance_opt) {
+            if (settle_forces(s)) return -1;
+            s->balance_opt = value;
+            if (s->use_n3b) {                           // back to the equal ranges; weighted again at the next call
+                const int W = s->p.world_size;
+                n3b_set_range(s->n3b, (int)((long)s->p.rank * s->n3b.NB / W), (int)((long)(s->p.rank + 1) * s->n3b.NB / W));
+                s->balanced = false;
+                if (ensure_aux(s)) return -1;
+            }
+        }
         return 0;
     }
     if (!strcmp(name, "force_reduce_mask")) {          // Newton-3 blocks: the reduction reads only written j-slots

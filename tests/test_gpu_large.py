@@ -639,3 +639,43 @@ def test_block_work_sums_to_the_census():
           f"{w.max() / w.mean():.3f}; world-8 partition max/mean "
           f"{max(w[r * NB // 8:(r + 1) * NB // 8].sum() for r in range(8)) / (w.sum() / 8):.4f}")
     s.close()
+
+
+@pytest.mark.gpu
+def test_weighted_block_ranges_local_group():
+    """force_balance 1 (default): the sharded ranks' block ranges by the census's work (n3b_balance) —
+    a partition of all blocks, the same on every rank, no rank's work above the equal-count split's
+    worst, and the forces still world 1's within 1e-13"""
+    import mdqtplasmasims_amd as M
+    from mdqtplasmasims_amd.engine import comm_init_local
+    kw = dict(N0=250000, detuningDP=1.0, seed=SEED, job=1)
+    ref = M.Simulation(**kw).init()
+    st = ref.get_state()
+    ref.forces()
+    G = ref.get_state()["F"]
+    NB = int(ref.const("n3b_block_count"))
+    ref.close()
+    W = 4
+    sims = [M.Simulation(world_size=W, rank=r, **kw) for r in range(W)]
+    for s in sims:
+        s.set_state(st["R"], st["V"], st["psi"], st["tPart"], st["t"])
+    comm_init_local(sims)
+    for s in sims:
+        s.allgather_positions()
+    for s in sims:
+        s.forces()
+    ranges = [(int(s.const("n3b_block_lo")), int(s.const("n3b_block_hi"))) for s in sims]
+    assert ranges[0][0] == 0 and ranges[-1][1] == NB
+    assert all(ranges[r][1] == ranges[r + 1][0] for r in range(W - 1))
+    ratios = {(s.const("force_balance_ratio"), s.const("force_balance_ratio_equal")) for s in sims}
+    assert len(ratios) == 1                              # every rank computed the same partition
+    wr, er = ratios.pop()
+    print(f"C5 world {W}: weighted ranges {ranges}; max/mean work {wr:.4f} (equal counts {er:.4f})")
+    assert wr <= er + 1e-12 and wr < 1.02
+    worst = 0.0
+    for s in sims:
+        lo, hi = s.slab_bounds()
+        worst = max(worst, np.abs(s.get_state()["F"][:, lo:hi] - G[:, lo:hi]).max() / np.abs(G).max())
+    assert worst < 1e-13
+    for s in sims:
+        s.close()

@@ -26,14 +26,15 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def n3b_plan(N, world, rank, BW=8, target=65536):
-    """mdqt_engine.cpp:choose_segments (Newton-3 blocks): tiles, blocks, half-shell distances,
-    this rank's blocks, runs of distances per block"""
+def n3b_plan(N, world, rank, BW=8, target=65536, cuts=None):
+    """mdqt_engine.cpp:choose_segments / n3b_set_range (Newton-3 blocks): tiles, blocks, half-shell
+    distances, this rank's blocks (equal counts, or the cut points `cuts` of n3b_balance), runs of
+    distances per block"""
     T = (N + 63) // 64
     NB = (T + BW - 1) // BW
     nd = NB // 2 + 1
-    Plo = rank * NB // world
-    Phi = (rank + 1) * NB // world
+    Plo = rank * NB // world if cuts is None else cuts[rank]
+    Phi = (rank + 1) * NB // world if cuts is None else cuts[rank + 1]
     nblk = max(Phi - Plo, 1)
     R = min(nd, (target + nblk - 1) // nblk)
     runlen = (nd + R - 1) // R
@@ -41,10 +42,10 @@ def n3b_plan(N, world, rank, BW=8, target=65536):
     return dict(T=T, NB=NB, nd=nd, Plo=Plo, Phi=Phi, R=R, runlen=runlen, BW=BW)
 
 
-def n3b_tile_pairs(N, world, rank, BW=8):
+def n3b_tile_pairs(N, world, rank, BW=8, cuts=None):
     """(I, J, diag) of every tile pair rank `rank` evaluates: mdqt_forces.hip:k_pairs_n3b's loops
     over workgroups (block P, run), distances db of the run, J tiles of block Q = P + db, waves I"""
-    p = n3b_plan(N, world, rank, BW)
+    p = n3b_plan(N, world, rank, BW, cuts=cuts)
     T, NB, nd = p["T"], p["NB"], p["nd"]
     out = []
     for wg in range((p["Phi"] - p["Plo"]) * p["R"]):
@@ -64,6 +65,44 @@ def n3b_tile_pairs(N, world, rank, BW=8):
                     if I < T and (db > 0 or J >= I):
                         out.append((I, J, db == 0 and J == I))
     return out
+
+
+def balance_cuts(w, world):
+    """mdqt_engine.cpp:n3b_balance: cut points with each rank's prefix work nearest r / W of the total,
+    at least one block per rank"""
+    pre = np.concatenate([[0.0], np.cumsum(np.asarray(w, dtype=float))])
+    NB, tot = len(w), pre[-1]
+    cut = [0] * (world + 1)
+    cut[world] = NB
+    for r in range(1, world):
+        t = tot * r / world
+        k = int(np.searchsorted(pre, t, side="left"))
+        if k > 0 and t - pre[k - 1] < pre[k] - t:
+            k -= 1
+        cut[r] = min(max(k, cut[r - 1] + 1), NB - (world - r))
+    return cut
+
+
+@pytest.mark.parametrize("N,BW", [(64 * 40 + 17, 2), (64 * 97 - 5, 4), (64 * 64, 16)])
+def test_weighted_block_ranges_cover_every_tile_pair_once(N, BW):
+    """the work-weighted block ranges (force_balance 1) are another partition of the blocks: every
+    distinct tile pair still exactly once, for skewed work profiles and world sizes 2-8"""
+    T = (N + 63) // 64
+    NB = (T + BW - 1) // BW
+    rng = np.random.default_rng(2)
+    for prof in (rng.uniform(0.2, 1.8, NB), np.linspace(0.3, 1.7, NB), np.r_[np.full(NB // 2, 5.0), np.ones(NB - NB // 2)]):
+        for world in range(2, min(8, NB) + 1):        # (n3b_balance keeps equal counts when NB < W)
+            cuts = balance_cuts(prof, world)
+            assert cuts[0] == 0 and cuts[-1] == NB and all(b > a for a, b in zip(cuts, cuts[1:]))
+            seen = {}
+            for rank in range(world):
+                for I, J, diag in n3b_tile_pairs(N, world, rank, BW, cuts=cuts):
+                    key = (min(I, J), max(I, J))
+                    seen[key] = seen.get(key, 0) + 1
+            assert len(seen) == T * (T + 1) // 2 and set(seen.values()) == {1}, (N, BW, world)
+            per = [prof[cuts[r]:cuts[r + 1]].sum() for r in range(world)]
+            # within one block's work of the ideal share
+            assert max(per) <= prof.sum() / world + prof.max() + 1e-9
 
 
 @pytest.mark.parametrize("N,BW", [(64 * 40 + 17, 2), (64 * 48, 3), (64 * 33 + 1, 4), (64 * 64, 16), (64 * 97 - 5, 4)])

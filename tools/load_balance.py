@@ -4,7 +4,8 @@ Rank r of W owns blocks [r NB / W, (r + 1) NB / W) (mdqt_engine.cpp plan sizing)
 does the evaluated lane-steps of those blocks' workgroups.  mdqt_force_block_work at world 1 gives
 every block's evaluated lane-steps for the reference's init() positions (k_n3b_census, the block
 kernel's own classification), so each partition's per-rank work follows; reported: max / mean over
-the ranks for W = 2, 4, 8, with the equal-count partition the engine uses, and after 3 MD steps.
+the ranks for W = 2, 4, 8, with equal block counts and with the work-weighted ranges the engine takes
+(mdqt_engine.cpp n3b_balance, option force_balance), at init() and after 3 MD steps.
 
     python tools/load_balance.py [c4 c5 c1m] > profiles/r05_load_balance.json
 """
@@ -22,10 +23,26 @@ import bench  # noqa: E402
 import mdqtplasmasims_amd as M  # noqa: E402
 
 
-def partition(work, W):
+def partition(work, W, cuts=None):
     NB = len(work)
-    per = np.array([work[r * NB // W:(r + 1) * NB // W].sum() for r in range(W)])
-    return per
+    if cuts is None:
+        cuts = [r * NB // W for r in range(W + 1)]
+    return np.array([work[cuts[r]:cuts[r + 1]].sum() for r in range(W)])
+
+
+def balance_cuts(w, W):
+    """mdqt_engine.cpp:n3b_balance's cut points (tests/test_n3b_protocol.py restates the same)"""
+    pre = np.concatenate([[0.0], np.cumsum(np.asarray(w, dtype=float))])
+    NB, tot = len(w), pre[-1]
+    cut = [0] * (W + 1)
+    cut[W] = NB
+    for r in range(1, W):
+        t = tot * r / W
+        k = int(np.searchsorted(pre, t, side="left"))
+        if k > 0 and t - pre[k - 1] < pre[k] - t:
+            k -= 1
+        cut[r] = min(max(k, cut[r - 1] + 1), NB - (W - r))
+    return cut
 
 
 def main():
@@ -49,6 +66,8 @@ def main():
                 per = partition(w, W)
                 row[f"world{W}_max_over_mean"] = float(per.max() / per.mean())
                 row[f"world{W}_min_over_mean"] = float(per.min() / per.mean())
+                pw = partition(w, W, balance_cuts(w, W))      # force_balance 1 (the product default)
+                row[f"world{W}_weighted_max_over_mean"] = float(pw.max() / pw.mean())
             res[tag] = row
         sim.close()
         res["seconds"] = time.perf_counter() - t0

@@ -494,16 +494,17 @@ __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0
 #define MDQT_N3B_DBUF 0
 #endif
 // the block kernel's LDS, one object (k_pairs_n3b)
+constexpr int kN3BStageBufs = MDQT_N3B_DBUF ? 2 : 1;
 template <int W>
 struct N3BShared {
-    double pj[2][3][128];                           // J positions by sub-tiles twice over (n3b_lds), 2 buffers
+    double pj[kN3BStageBufs][3][128];               // J positions by sub-tiles twice over (n3b_lds), per buffer
     double accj[W][3][128];                         // per-wave j accumulators
     double mjs[2][128];                             // J validity weights: all ones / the ragged last tile's
     double etab[64];                                // 2^(k/64) (MDQT_EXP_TAB)
 #if MDQT_N3B_IRUN_LDS
     double irun[W][3][64];                          // the run's i accumulators
 #endif
-    uint2 pw[2][W];                                 // plan words (class, sub-tile groups), 2 buffers
+    uint2 pw[kN3BStageBufs][W];                     // plan words (class, sub-tile groups), per buffer
 };
 // AXP: the one-axis per-pair image (n3b_pack_class bits 28-29) in an instance of its own, launched
 // only where such tile pairs can lie inside the skip radius (launch_forces_n3b): compiled into the
@@ -666,7 +667,7 @@ void k_pairs_n3b(N3BArgs a) {
                     // this buffer's DMA was retired at the previous step's second barrier, or (the first
                     // step) it is retired here: everything but the 4 DMA loads just issued
                     if (ndb < d1) {
-                        dma_stage(buf ^ 1, ndb, nb);
+                        dma_stage(buf ^ (kN3BStageBufs - 1), ndb, nb);
                         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                     } else {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -814,7 +815,7 @@ void k_pairs_n3b(N3BArgs a) {
             }
             if (kDbuf && plan && q == kStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA retired
             __syncthreads();
-            if (kDbuf && plan) buf ^= 1;
+            if (kDbuf && plan) buf ^= kN3BStageBufs - 1;
             if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db
                 const int l = lane_opaque(l0);
                 const int li = n3b_lds(l);

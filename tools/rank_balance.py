@@ -43,21 +43,38 @@ def main(cfg="c5", W=8):
             s.get_state()
         for s in sims:
             s.allgather_positions()
-        ms, ev = [], []
+        ev = []
+        # each rank's call alone on the GPU, in rank order and then in reverse order (a drift of the
+        # clock over the sequence shows as a trend in rank order; the mean of both passes cancels it)
+        passes = []
+        for order in (list(range(W)), list(range(W - 1, -1, -1))):
+            t = [0.0] * W
+            for _ in range(3):
+                for r in order:
+                    s = sims[r]
+                    s.enable_timing(1, kinds=1)
+                    s.forces()
+                    s.synchronize()
+                    kt = s.kernel_times()
+                    s.enable_timing(0)
+                    t[r] += kt["block_ms"] / max(kt["n_block"], 1) / 3
+                for s in sims:                          # (the deferred reduce, then positions again)
+                    s.get_state()
+                for s in sims:
+                    s.allgather_positions()
+            passes.append(t)
+        ms = [(a + b) / 2 for a, b in zip(*passes)]
         for s in sims:
-            s.enable_timing(1, kinds=1)
             s.forces()
-            s.synchronize()
-            kt = s.kernel_times()
-            s.enable_timing(0)
-            ms.append(kt["block_ms"] / max(kt["n_block"], 1))
         worst = 0.0
         for s in sims:
             lo, hi = s.slab_bounds()
             worst = max(worst, np.abs(s.get_state()["F"][:, lo:hi] - G[:, lo:hi]).max() / np.abs(G).max())
+        cls = []
         for s in sims:
             c = s.force_census()
             ev.append(sum(v[0] for k, v in c.items() if not k.startswith("skip")))
+            cls.append({k: v[0] for k, v in c.items()})
         ranges = [(int(s.const("n3b_block_lo")), int(s.const("n3b_block_hi"))) for s in sims]
         ratio = sims[0].const("force_balance_ratio")
         for s in sims:
@@ -65,9 +82,11 @@ def main(cfg="c5", W=8):
         ms, ev = np.array(ms), np.array(ev)
         out["weighted" if bal else "equal"] = {
             "block_ranges": ranges, "block_kernel_ms": ms.round(4).tolist(),
+            "block_kernel_ms_forward": np.round(passes[0], 4).tolist(), "block_kernel_ms_reverse": np.round(passes[1], 4).tolist(),
             "kernel_max_over_mean": float(ms.max() / ms.mean()), "lane_steps_max_over_mean": float(ev.max() / ev.mean()),
-            "engine_census_ratio": ratio, "max_rel_err_vs_world1": worst}
-        print(cfg, "balance", bal, json.dumps(out["weighted" if bal else "equal"]), file=sys.stderr, flush=True)
+            "engine_census_ratio": ratio, "max_rel_err_vs_world1": worst, "census_lane_steps": cls}
+        brief = {k: v for k, v in out["weighted" if bal else "equal"].items() if k != "census_lane_steps"}
+        print(cfg, "world", W, "balance", bal, json.dumps(brief), file=sys.stderr, flush=True)
         assert worst < 1e-13
     print(json.dumps(out, indent=1))
 

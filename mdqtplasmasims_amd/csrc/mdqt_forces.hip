@@ -297,55 +297,111 @@ __device__ __forceinline__ float row_rol1f(float v) {   // lane 16 a + m <- lane
 }
 
 // An ultra-far tile pair (boxes >= r_ufar32 apart) with a uniform image, pair terms in f32
-// (MDQT_UFAR32; error analysis and bound in mdqt_internal.hpp kUfar32A/B): dx = fl32(xi - n L - xj)
-// from the f64 separation, v_rsq_f32, 2^t by v_exp_f32, the cutoff on the f32 r^2 (t = -inf).  Per
-// 16-step group the i side is summed in f32 registers and then added to the f64 partial; the j side
-// is a running sum rotated one lane down inside the lane's row of 16 each step (row_ror:15 folded
-// into the f32 add: lane m + 1's sum of the previous step is for lane m's current J ion) and ends in
-// one ds_add_f64 per component at the group's last index.  Off the diagonal only (a tile's pair with
-// itself is never ultra far); its separations take xi already shifted by n L.
+// (MDQT_UFAR32; error analysis and bound in mdqt_internal.hpp kUfar32A/B).  Round 5: the staging wave
+// also holds the J tile in f32 relative to its first ion c_J (pj32 = fl32(xj - c_J)), the wave takes
+// xi32 = fl32(xi - n L - c_J) once per tile pair and dx = fl32(xi32 - pj32) — no f64 subtraction and
+// f32 conversion per pair — and (MDQT_UF32_PK) runs two rotation steps t, t + 1 through each packed
+// instruction (v_pk_add_f32, v_pk_mul_f32, v_pk_fma_f32; v_rsq_f32, v_exp_f32 and the cutoff select
+// per step): 16.75 VALU instructions per pair instead of 29.  The cutoff on the f32 r^2 (t = -inf).  The
+// i side is summed in two f32 partials (even and odd steps), added, then added to the f64 partial; the j
+// side is a running sum rotated one lane down inside the lane's row of 16 each step (row_ror:15 folded
+// into the f32 add: lane m + 1's sum of the previous step is for lane m's current J ion; two steps at
+// once: row_ror:14 of the sum plus row_ror:15 of step t's term plus step t + 1's) and ends in one
+// ds_add_f64 per component at the group's last index.  Off the diagonal only (a tile's pair with
+// itself is never ultra far).
 static_assert(MDQT_SHIFT_I || !MDQT_UFAR32, "the f32 ultra-far form needs MDQT_SHIFT_I");
-__device__ __forceinline__ void n3b_group_uf32(int b0, double xi, double yi, double zi, const double (*pj)[128],
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float row_rol2f(float v) {   // lane 16 a + m <- lane 16 a + ((m + 2) & 15)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x12E, 0xF, 0xF, false));   // row_ror:14
+}
+// two rotation steps per v_pk_* instruction (MDQT_UF32_PK 1): gfx950 runs a packed f32 operation at half
+// the rate of a scalar one (tools/ubench_f64: the same VALU cycles per pair) but issues half the
+// instructions — A/B round 5 (tools/gpu/r05_uf32.sh): C4 force call 244.8 ms packed, 248.3 scalar,
+// 254.1 with the round-4 form (f64 separations); N = 1M 198.0 / 200.3 / 205.3.  0: one step at a time
+#ifndef MDQT_UF32_PK
+#define MDQT_UF32_PK 1
+#endif
+
+__device__ __forceinline__ void n3b_group_uf32(int b0, float xi, float yi, float zi, const float (*pj32)[128],
                                                double* ax, double* ay, double* az, double& fx, double& fy, double& fz,
                                                float cf, float invlf, float rc2f) {
-    int b_ = b0;
-    asm volatile("" : "+v"(b_));                    // immediate LDS offsets (N3B_REBASE)
-    const double (*pjb)[128] = (const double (*)[128])(&pj[0][0] + b_);
-    float ix = 0.f, iy = 0.f, iz = 0.f, jx = 0.f, jy = 0.f, jz = 0.f;
+    // one opaque LDS address per component, so the 16 steps read them at immediate offsets (N3B_REBASE;
+    // the array's own LDS offset and a shared base for the three components would not fit the
+    // ds_read2_b32 offset field)
+    typedef __attribute__((address_space(3))) const float* lds_f32p;
+    lds_f32p px0 = (lds_f32p)&pj32[0][b0], py0 = (lds_f32p)&pj32[1][b0], pz0 = (lds_f32p)&pj32[2][b0];
+    asm volatile("" : "+v"(px0), "+v"(py0), "+v"(pz0));
+    if constexpr (MDQT_UF32_PK) {
+        f32x2 ix = {0.f, 0.f}, iy = {0.f, 0.f}, iz = {0.f, 0.f};
+        float jx = 0.f, jy = 0.f, jz = 0.f;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        const float dx = (float)(xi - pjb[0][t]), dy = (float)(yi - pjb[1][t]), dz = (float)(zi - pjb[2][t]);
-        const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-        const float ri = __builtin_amdgcn_rsqf(r2);
-        const float e = __builtin_amdgcn_exp2f(r2 < rc2f ? (r2 * ri) * cf : -INFINITY);
-        const float ft = ((ri + invlf) * e) * (ri * ri);
-        const float px = dx * ft, py = dy * ft, pz = dz * ft;
-        if (t == 0) {
-            ix = px; iy = py; iz = pz;
-            jx = px; jy = py; jz = pz;
-        } else {
-            ix += px; iy += py; iz += pz;
-            jx = row_rol1f(jx) + px; jy = row_rol1f(jy) + py; jz = row_rol1f(jz) + pz;
+        for (int t = 0; t < 16; t += 2) {
+            const f32x2 dx = f32x2{xi, xi} - f32x2{px0[t], px0[t + 1]};
+            const f32x2 dy = f32x2{yi, yi} - f32x2{py0[t], py0[t + 1]};
+            const f32x2 dz = f32x2{zi, zi} - f32x2{pz0[t], pz0[t + 1]};
+            const f32x2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
+            const f32x2 ri = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
+            const f32x2 tt = (r2 * ri) * cf;
+            const f32x2 e = {__builtin_amdgcn_exp2f(r2.x < rc2f ? tt.x : -INFINITY),
+                             __builtin_amdgcn_exp2f(r2.y < rc2f ? tt.y : -INFINITY)};
+            const f32x2 ft = ((ri + invlf) * e) * (ri * ri);
+            const f32x2 px = dx * ft, py = dy * ft, pz = dz * ft;
+            // j side: S_t(m) = S_(t-1)(m + 1) + p_t(m); two steps: S_(t+1) = rol2(S_(t-1)) + (rol1(p_t) + p_(t+1))
+            const float ux = row_rol1f(px.x) + px.y, uy = row_rol1f(py.x) + py.y, uz = row_rol1f(pz.x) + pz.y;
+            if (t == 0) {
+                ix = px; iy = py; iz = pz;
+                jx = ux; jy = uy; jz = uz;
+            } else {
+                ix += px; iy += py; iz += pz;
+                jx = row_rol2f(jx) + ux; jy = row_rol2f(jy) + uy; jz = row_rol2f(jz) + uz;
+            }
+            // each step pair's sums formed in their step pair (without it: 79 VGPRs spilled instead of 50)
+            asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
         }
-        // each step's i and j sums formed in their step: without it the compiler sank the 45 DPP adds
-        // and the i-side adds after the last step and spilled the pending terms (64-VGPR budget)
-        asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
+        const int b_ = b0;
+        __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        fx += (double)(ix.x + ix.y); fy += (double)(iy.x + iy.y); fz += (double)(iz.x + iz.y);
+    } else {
+        float ix = 0.f, iy = 0.f, iz = 0.f, jx = 0.f, jy = 0.f, jz = 0.f;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const float dx = xi - px0[t], dy = yi - py0[t], dz = zi - pz0[t];
+            const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+            const float ri = __builtin_amdgcn_rsqf(r2);
+            const float e = __builtin_amdgcn_exp2f(r2 < rc2f ? (r2 * ri) * cf : -INFINITY);
+            const float ft = ((ri + invlf) * e) * (ri * ri);
+            const float px = dx * ft, py = dy * ft, pz = dz * ft;
+            if (t == 0) {
+                ix = px; iy = py; iz = pz;
+                jx = px; jy = py; jz = pz;
+            } else {
+                ix += px; iy += py; iz += pz;
+                jx = row_rol1f(jx) + px; jy = row_rol1f(jy) + py; jz = row_rol1f(jz) + pz;
+            }
+            // each step's i and j sums formed in their step: without it the compiler sank the DPP adds
+            // and the i-side adds after the last step and spilled the pending terms (80-VGPR budget)
+            asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
+        }
+        const int b_ = b0;
+        __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        fx += (double)ix; fy += (double)iy; fz += (double)iz;
     }
-    __hip_atomic_fetch_add(ax + b_ + 15, (double)jx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_add(ay + b_ + 15, (double)jy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_add(az + b_ + 15, (double)jz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    fx += (double)ix; fy += (double)iy; fz += (double)iz;
 }
 
-// the f32 ultra-far form over the groups of `groups` (off the diagonal)
-__device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, double xi, double yi, double zi,
-                                              const double (*pj)[128], double* ax, double* ay, double* az,
+// the f32 ultra-far form over the groups of `groups` (off the diagonal); xi, yi, zi: the lane's ion
+// relative to the J tile's raw box centre, in f32
+__device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, float xi, float yi, float zi,
+                                              const float (*pj32)[128], double* ax, double* ay, double* az,
                                               double& fx, double& fy, double& fz, float cf, float invlf, float rc2f) {
     l = lane_opaque(l);
     const int a = l >> 4, m = l & 15;
     for (int d = 0; d < 4; ++d) {
         if (!((groups >> d) & 1u)) continue;        // wave-uniform
-        n3b_group_uf32(32 * ((a + d) & 3) + m, xi, yi, zi, pj, ax, ay, az, fx, fy, fz, cf, invlf, rc2f);
+        n3b_group_uf32(32 * ((a + d) & 3) + m, xi, yi, zi, pj32, ax, ay, az, fx, fy, fz, cf, invlf, rc2f);
     }
 }
 
@@ -476,6 +532,18 @@ __device__ __forceinline__ int n3b_pack_class(double4 t4, int strad = 0) {
 }
 // real ions of 16-ion sub-tile s (0 for the padding of the ragged last tile)
 __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0, min(16, N - 16 * s)); }
+// tile J's raw box (the exact min / max of its coordinates, boxes [6, 12)): its squared half-diagonal —
+// the f32 ultra-far form (n3b_group_uf32) stages J relative to J's first ion and takes a sub-tile group
+// only where the box diagonal (twice this) is within the group's gap (kUfar32A/B's premise)
+__device__ __forceinline__ double raw_half2(const double* B, int T, int J) {
+    double h2 = 0.;
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) {
+        const double h = 0.5 * (B[(size_t)(9 + c3) * T + J] - B[(size_t)(6 + c3) * T + J]);
+        h2 = fma(h, h, h2);
+    }
+    return h2;
+}
 
 
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
@@ -493,11 +561,13 @@ __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0
 #ifndef MDQT_N3B_DBUF
 #define MDQT_N3B_DBUF 0
 #endif
+static_assert(!(MDQT_N3B_DBUF && MDQT_UFAR32), "the double-buffered staging has no f32 J copy: build it with MDQT_UFAR32 0");
 // the block kernel's LDS, one object (k_pairs_n3b)
 constexpr int kN3BStageBufs = MDQT_N3B_DBUF ? 2 : 1;
 template <int W>
 struct N3BShared {
     double pj[kN3BStageBufs][3][128];               // J positions by sub-tiles twice over (n3b_lds), per buffer
+    float pj32[3][128];                             // the same, fl32(xj - c_J), c_J = J's first ion (the f32 ultra-far form)
     double accj[W][3][128];                         // per-wave j accumulators
     double mjs[2][128];                             // J validity weights: all ones / the ragged last tile's
     double etab[64];                                // 2^(k/64) (MDQT_EXP_TAB)
@@ -684,6 +754,13 @@ void k_pairs_n3b(N3BArgs a) {
                     sh.pj[buf][0][li] = xj; sh.pj[buf][0][li + 16] = xj;
                     sh.pj[buf][1][li] = yj; sh.pj[buf][1][li + 16] = yj;
                     sh.pj[buf][2][li] = zj; sh.pj[buf][2][li + 16] = zj;
+                    if constexpr (FARF && MDQT_UFAR32) {   // relative to c_J = J's first ion (pj[.][0])
+                        const float x32 = (float)(xj - uniform_f64(xj)), y32 = (float)(yj - uniform_f64(yj)),
+                                    z32 = (float)(zj - uniform_f64(zj));
+                        sh.pj32[0][li] = x32; sh.pj32[0][li + 16] = x32;
+                        sh.pj32[1][li] = y32; sh.pj32[1][li + 16] = y32;
+                        sh.pj32[2][li] = z32; sh.pj32[2][li + 16] = z32;
+                    }
                     if (l < BW) {
                         if (plan) {                 // (P, db, b): one word per wave
                             sh.pw[buf][l] = plan[((size_t)(P - a.Plo) * a.nd + db) * (BW * BW) + b * BW + l];
@@ -746,7 +823,8 @@ void k_pairs_n3b(N3BArgs a) {
                             if (g0) n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(false, g0, l, sx, sy, sz, mi, pj, mj, ax,
                                                                                     ay, az, tx, ty, tz, c, nsh);
 #if !defined(MDQT_EXPT_UFAR_SKIP)                   // last: nothing after it keeps sx, nsh live (diagnostic build: skip it, wrong results)
-                            if (g5) n3b_pair_uf32(g5, l, sx, sy, sz, pj, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
+                            if (g5) n3b_pair_uf32(g5, l, (float)(sx - pj[0][0]), (float)(sy - pj[1][0]), (float)(sz - pj[2][0]),
+                                                  sh.pj32, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
 #endif
                         }
                     } else {
@@ -1015,6 +1093,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
             add(cls_of(0), 2560ull, (unsigned long long)(nI * (nI - 1) / 2));
         } else {
             const int T4 = 4 * a.T;
+            const double hj2 = raw_half2(a.boxes, a.T, J);
             unsigned act = 0, mm = 0, mf = 0, mv = 0, mu = 0, m32 = 0;
             double np[4] = {0., 0., 0., 0.};       // ion pairs per group
             for (int sa = 0; sa < 4; ++sa)
@@ -1026,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                     if (sg > rad.rf2) mf |= bit;
                     if (sg > rad.rv2) mv |= bit;
                     if (sg > rad.ru2) mu |= bit;
-                    if (sg > rad.ru32) m32 |= bit;
+                    if (sg > rad.ru32 && sg > 4. * hj2) m32 |= bit;   // (k_n3b_plan's level 5)
                     np[(sb - sa) & 3] += sub_count(a.N, 4 * I + sa) * sub_count(a.N, 4 * J + sb);
                 }
             const unsigned g = a.use_sort == 1 ? sub_groups_of(act) : 0xFu;   // (2: nothing skipped)
@@ -1090,11 +1169,13 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
 #pragma unroll
                 for (int sb = 0; sb < 4; ++sb) sg[sa][sb] = sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, invL);
             unsigned groups = 0u, lvm = 0u;
+            const double hj2 = raw_half2(a.boxes, a.T, J);
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 const double gm = fmin(fmin(sg[0][d & 3], sg[1][(1 + d) & 3]), fmin(sg[2][(2 + d) & 3], sg[3][(3 + d) & 3]));
                 if (a.use_sort != 1 || gm <= rad.rc2) {
-                    const int x = !FARF ? 0 : n3b_level(gm, rad);
+                    int x = !FARF ? 0 : n3b_level(gm, rad);
+                    if (x == 5 && !(gm > 4. * hj2)) x = 4;   // f32: J's raw box diagonal within the gap (kUfar32A/B)
                     groups |= 1u << d;
                     lvm |= 1u << (4 * x + d);
                 }

@@ -287,25 +287,29 @@ constexpr double kExp5RelErr = 1.1e-7;
 // kExp2fRelErr of itself (kExp2fRelErr: twice what tools/exp2f_precision measures, re-checked by a
 // GPU test).  f32's range holds 2^t down to t = -126: r <= 87 lDeb, beyond every L/2 it serves.
 constexpr double kExp2fRelErr = 0x1p-22;
-// The ultra-far tier in f32 (MDQT_UFAR32, round 3): a uniform-image tile pair whose boxes are
-// >= r_ufar32 apart evaluates its pair terms in f32 from the f64 separations: dx = fl32(xi - xj),
-// r^2 by f32 FMAs, v_rsq_f32 (<= kRsqF32RelErr = 1 ulp, measured by tools/rsq_precision and a GPU
-// test), t = (r^2 ri) cf with cf = fl32(-log2(e)/lDeb), v_exp_f32, then the force factor and the
-// three products in f32; the i side summed in f32 over 16 steps, then in f64; the j side rotated
-// along the wave over the same 16 steps (one ds_add_f64 per component).  Per term, to first order in
-// u = 2^-24: dx u, r^2 5u, ri 2u + 2.5u, r 10.5u, t 12.5u — so 2^t is within (r/lDeb) 12.5u +
-// kExp2fRelErr — the force factor 17.5u more, the product 2u; each 16-term f32 sum adds 15u: a term
-// is within (r/lDeb) 13u + 40u of itself (kUfar32A, kUfar32B, rounded up).  The cutoff is decided on
-// the f32 r^2 (<= 6u off): pairs within 3u Rcut of L/2 may land on either side, each at most
-// g(Rcut (1 - 2^-20)) — so far_radius_l's level 4 bounds every ion by (N - 1) g(r) err(r) +
-// (N - 1) g(Rcut (1 - 2^-20)), and the tier is off where that cannot meet 10^-k (C5: N g(L/2) is
-// ~1e-8; N = 1e6 at C2's parameters: ~5e-16).
+// The ultra-far tier in f32 (MDQT_UFAR32, round 3; round 5: relative to J's first ion, packed): a
+// uniform-image tile pair's sub-tile group whose sub-boxes are >= r_ufar32 apart — and whose gap g is
+// at least the J tile's raw box diagonal D (k_n3b_plan) — evaluates its pair terms in f32: the J tile
+// staged as fl32(xj - c_J), c_J its first ion, the lane's ion as fl32(xi - n L - c_J), dx their f32
+// difference; r^2 by f32 FMAs, v_rsq_f32 (<= kRsqF32RelErr = 1 ulp, measured by tools/rsq_precision
+// and a GPU test), t = (r^2 ri) cf with cf = fl32(-log2(e)/lDeb), v_exp_f32, then the force factor and
+// the three products in f32; the i side summed in two f32 partials of 8 steps, then in f64; the j side
+// rotated along the wave over the 16 steps (one ds_add_f64 per component).  With u = 2^-24, per axis
+// |ddx| <= u (|xi - n L - c_J| + |xj - c_J| + |dx|), and |xi - n L - c_J| <= r + D, |xj - c_J| <= D, so
+// |ddx| <= u (2 r + 2 D) <= 4 u r as a vector (D <= g <= r).  To first order: r^2 8u + 3u = 11u,
+// ri 5.5u + 2u = 7.5u, r 19.5u, t 21.5u — so 2^t is within (r/lDeb) 21.5u + kExp2fRelErr — the force
+// factor ((ri + invl) 9.5u, times 2^t 1u, ri^2 16u, product 1u) 27.5u more, the product with dx 5u;
+// each 16-term f32 sum adds 15u: a term is within (r/lDeb) 22u + 52u of itself (kUfar32A, kUfar32B,
+// rounded up).  The cutoff is decided on the f32 r^2 (<= 11u off): pairs within 6u Rcut of L/2 may
+// land on either side, each at most g(Rcut (1 - 2^-20)) — so far_radius_l's level 4 bounds every ion
+// by (N - 1) g(r) err(r) + (N - 1) g(Rcut (1 - 2^-20)), and the tier is off where that cannot meet
+// 10^-k (C5: N g(L/2) is ~1e-8; N = 1e6 at C2's parameters: ~5e-16).
 #ifndef MDQT_UFAR32
 #define MDQT_UFAR32 1
 #endif
 constexpr double kRsqF32RelErr = 0x1p-23;
-constexpr double kUfar32A = 13. * 0x1p-24;
-constexpr double kUfar32B = 40. * 0x1p-24;
+constexpr double kUfar32A = 22. * 0x1p-24;
+constexpr double kUfar32B = 52. * 0x1p-24;
 __device__ __forceinline__ double exp2_neg_cut5(double t, bool keep) {
     const double n = __builtin_rint(t);
     const double f = t - n;

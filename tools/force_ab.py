@@ -12,7 +12,8 @@ import sys
 ROOT = os.environ.get("MDQT_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)      # MDQT_ROOT: another tree's package (an older round's library and wrapper)
 
-CFG = {"C3": dict(N0=100000, Ge=1.0 / 12, qt_enabled=0), "C5": dict(N0=250000, detuningDP=1.0),
+CFG = {"C3": dict(N0=100000, Ge=1.0 / 12, qt_enabled=0), "C4": dict(N0=1000000, Ge=1.0 / 12, qt_enabled=0),
+       "C5": dict(N0=250000, detuningDP=1.0),
        "1M": dict(N0=1000000), "C2": dict(N0=3500)}
 DEFAULT = ("C3", "C5", "1M")
 

@@ -17,14 +17,17 @@ __device__ __forceinline__ double dppd(double v) {
 }
 
 // OP 0: fma f64; 1: add f64; 2: fma f32; 3: x = x + dpp_ror8(x) (2 movs + add); 4: rsq f64 + fma;
-// 5: mul f64
+// 5: mul f64; 6: packed fma f32 (v_pk_fma_f32); 7: packed mul f32 (v_pk_mul_f32); 8: exp f32 + fma f32;
+// 9: rsq f32 + fma f32
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int OP, int CH>
 __global__ __launch_bounds__(256) void k(double* out, long long* cyc, int iters, double a, double b) {
     const int gid = blockIdx.x * 256 + threadIdx.x;
     double x[CH];
     float xf[CH];
+    f32x2 xp[CH];
 #pragma unroll
-    for (int c = 0; c < CH; ++c) { x[c] = threadIdx.x * 1e-3 + c; xf[c] = (float)x[c]; }
+    for (int c = 0; c < CH; ++c) { x[c] = threadIdx.x * 1e-3 + c; xf[c] = (float)x[c]; xp[c] = f32x2{xf[c], xf[c] + 1.f}; }
     const float af = (float)a, bf = (float)b;
     __builtin_amdgcn_s_waitcnt(0);
     const long long t0 = __builtin_amdgcn_s_memtime();
@@ -38,6 +41,10 @@ __global__ __launch_bounds__(256) void k(double* out, long long* cyc, int iters,
                 else if (OP == 2) xf[c] = fmaf(xf[c], af, bf);
                 else if (OP == 3) x[c] = x[c] * a + dppd<0x128>(x[c]);
                 else if (OP == 4) x[c] = fma(__builtin_amdgcn_rsq(x[c]), a, b);
+                else if (OP == 6) xp[c] = __builtin_elementwise_fma(xp[c], f32x2{af, af}, f32x2{bf, bf});
+                else if (OP == 7) xp[c] = xp[c] * f32x2{af, bf};
+                else if (OP == 8) xf[c] = fmaf(__builtin_amdgcn_exp2f(xf[c]), af, -bf);
+                else if (OP == 9) xf[c] = fmaf(__builtin_amdgcn_rsqf(xf[c]), af, bf);
                 else x[c] = x[c] * a;
             }
         }
@@ -45,7 +52,7 @@ __global__ __launch_bounds__(256) void k(double* out, long long* cyc, int iters,
     const long long t1 = __builtin_amdgcn_s_memtime();
     double s = 0;
 #pragma unroll
-    for (int c = 0; c < CH; ++c) s += x[c] + xf[c];
+    for (int c = 0; c < CH; ++c) s += x[c] + xf[c] + xp[c].x + xp[c].y;
     out[gid] = s;
     cyc[gid] = t1 - t0;
 }
@@ -96,6 +103,14 @@ int main() {
         run<3, 4>("dpp+fma", wps, dout, dcyc, it);
         run<4, 1>("rsq+fma", wps, dout, dcyc, it / 4);
         run<4, 4>("rsq+fma", wps, dout, dcyc, it / 4);
+        run<2, 8>("fma_f32", wps, dout, dcyc, it);
+        run<6, 1>("pkfma_f32", wps, dout, dcyc, it);
+        run<6, 4>("pkfma_f32", wps, dout, dcyc, it);
+        run<6, 8>("pkfma_f32", wps, dout, dcyc, it);
+        run<7, 4>("pkmul_f32", wps, dout, dcyc, it);
+        run<7, 8>("pkmul_f32", wps, dout, dcyc, it);
+        run<8, 4>("exp+fma32", wps, dout, dcyc, it / 4);
+        run<9, 4>("rsq+fma32", wps, dout, dcyc, it / 4);
     }
     return 0;
 }

@@ -1169,13 +1169,19 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
 #pragma unroll
                 for (int sb = 0; sb < 4; ++sb) sg[sa][sb] = sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, invL);
             unsigned groups = 0u, lvm = 0u;
-            const double hj2 = raw_half2(a.boxes, a.T, J);
+            double gm[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+                gm[d] = fmin(fmin(sg[0][d & 3], sg[1][(1 + d) & 3]), fmin(sg[2][(2 + d) & 3], sg[3][(3 + d) & 3]));
+            // the f32 level needs J's raw box diagonal within the group's gap (kUfar32A/B): J's extents
+            // read only where a group is that far
+            const double gmax = fmax(fmax(gm[0], gm[1]), fmax(gm[2], gm[3]));
+            const double hj4 = FARF && gmax > rad.ru32 ? 4. * raw_half2(a.boxes, a.T, J) : 0.;
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
-                const double gm = fmin(fmin(sg[0][d & 3], sg[1][(1 + d) & 3]), fmin(sg[2][(2 + d) & 3], sg[3][(3 + d) & 3]));
-                if (a.use_sort != 1 || gm <= rad.rc2) {
-                    int x = !FARF ? 0 : n3b_level(gm, rad);
-                    if (x == 5 && !(gm > 4. * hj2)) x = 4;   // f32: J's raw box diagonal within the gap (kUfar32A/B)
+                if (a.use_sort != 1 || gm[d] <= rad.rc2) {
+                    int x = !FARF ? 0 : n3b_level(gm[d], rad);
+                    if (x == 5 && !(gm[d] > hj4)) x = 4;
                     groups |= 1u << d;
                     lvm |= 1u << (4 * x + d);
                 }

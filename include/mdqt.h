@@ -204,7 +204,13 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     j-slots the block kernel wrote (per-J-tile masks of the block distances whose J
  *                     step has work, from the plan), 0 = every j-slot (empty J steps write -0).  Bit
  *                     for bit the same forces (acc + -0 = acc)
- *   "force_tail_exp": block pairs in spatial order: tile pairs whose boxes are >= r_t apart are
+ *   "force_tile_split": Newton-3 tiles: 1 (default) = the whole tile pairs of the kernel's last round of
+ *                     workgroups (after the diagonal ones) run as two half workgroups each, their second
+ *                     halves' rows in one extra slot (C2 on 256 CUs: 4 of 1,596; "force_tile_split_pairs"
+ *                     reports the count, "device_cus" the device's compute units); 0 = whole tile pairs
+ *                     only.  Forces agree to rounding (another summation order on the split tiles); the
+ *                     options overlap / fused_step take the plain table
+ *   "force_tail_exp":block pairs in spatial order: tile pairs whose boxes are >= r_t apart are
  *                     skipped with every ion's force kept within eps = 10^-k of the exact sum to
  *                     L/2 (g(r) = one pair's |F| at distance r, SpeedUp:224); k = 12 default, 0 =
  *                     exact (r_t = L/2); a no-op where the a-priori radius below is >= L/2 (every

@@ -193,7 +193,10 @@ struct mdqt_ctx {
     bool rs_pending = false;       // in-process group: F = sum of the ranks' dFr chunks, not formed yet
     const double** dPeerParts = nullptr;   // device array of the group's dFr pointers
     int nslots = 0, npairs = 0, capPairs = 0;
-    int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel
+    int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel; after the
+                                   // npairs entries, the split table (nsplit > 0: ensure_aux)
+    int nsplit = 0;                // tile pairs the split table runs as two half workgroups
+    int split_opt = 1;             // option force_tile_split
     // rng_mode 0: the reference's drand48 stream, consumed in ion order on the device
     unsigned long long* dX48 = nullptr;   // [1] stream state + [48] jA + [48] jC
     int* dFlags = nullptr;         // [0] set by the substep kernels when a position leaves [-L/8, 9L/8]
@@ -679,8 +682,28 @@ static void choose_segments(mdqt_ctx* s) {
 }
 
 // partial-sum buffer (row segments or Newton-3 slots) and the tile-pair table
+// The tile kernel's last round of workgroups (C2: 1,596 on 256 CUs, 6 per CU and 60 more) decides
+// its end: the 56 diagonal tile pairs (half the steps) go last already (the table below), and the
+// split table also runs the 4 full tile pairs that remain in that round as two half workgroups each
+// (the first / second 8 of every wave's 16 rotation steps) — 64 half-work workgroups in the last
+// round instead of 56 + 4 whole ones, so no CU runs 7 whole tile pairs.  The second halves write
+// their rows into one extra slot (ntiles; the split pairs have disjoint tiles, (0, 1), (2, 3), ...,
+// and every other row of that slot stays 0), so F = the sum of ntiles + 1 slots.  The overlapped and
+// fused MD steps (tile arrival counts) keep the plain table.
+static int tile_split_count(const mdqt_ctx* s, int nt) {
+    if (!s->split_opt || nt < 2) return 0;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->dev) != hipSuccess || ncu <= 0) return 0;
+    const long w0 = (long)nt * (nt + 1) / 2;
+    if (w0 <= ncu || w0 > 8L * ncu) return 0;    // one round (nothing to balance) / many (dispatched as CUs free up)
+    const int k = (int)(w0 % ncu) - nt;          // whole tile pairs in the last round
+    return (k > 0 && nt + 2 * k <= ncu && 2 * k <= nt) ? k : 0;
+}
+
 static int ensure_aux(mdqt_ctx* s) {
-    const int need = std::max(std::max(s->nseg, s->nslots), 2);
+    const int nt_split = (s->N + 63) / 64;
+    s->nsplit = s->use_n3 && s->npairs > 0 ? tile_split_count(s, nt_split) : 0;
+    const int need = std::max(std::max(s->nseg, s->nslots + (s->nsplit > 0 ? 1 : 0)), 2);
     if (need > s->capNseg) {
         if (s->dFpart) HIPCHK(hipFree(s->dFpart));
         s->dFpart = nullptr;
@@ -725,11 +748,12 @@ static int ensure_aux(mdqt_ctx* s) {
         }
     }
     if (s->use_n3 && s->npairs > 0) {
-        if (s->npairs > s->capPairs) {
+        const int tot = s->npairs + (s->nsplit > 0 ? s->npairs + s->nsplit : 0);
+        if (tot > s->capPairs) {
             if (s->dPairs) HIPCHK(hipFree(s->dPairs));
             s->dPairs = nullptr;
-            HIPCHK(hipMalloc(&s->dPairs, (size_t)s->npairs * sizeof(int2)));
-            s->capPairs = s->npairs;
+            HIPCHK(hipMalloc(&s->dPairs, (size_t)tot * sizeof(int2)));
+            s->capPairs = tot;
         }
         const int nt = (s->N + 63) / 64;
         std::vector<int2> h;
@@ -742,6 +766,19 @@ static int ensure_aux(mdqt_ctx* s) {
             for (int J = I + 1; J < nt; ++J) h.push_back(make_int2(I, J));
         for (int I = 0; I < nt; ++I) h.push_back(make_int2(I, I));
         if ((int)h.size() != s->npairs) return fail("tile-pair table size mismatch");
+        if (s->nsplit > 0) {                         // the split table (tile_split_count)
+            const int k = s->nsplit;
+            auto split = [&](int I, int J) { return J == I + 1 && (I & 1) == 0 && I < 2 * k; };
+            for (int I = 0; I < nt; ++I)
+                for (int J = I + 1; J < nt; ++J)
+                    if (!split(I, J)) h.push_back(make_int2(I, J));
+            for (int m = 0; m < k; ++m) h.push_back(make_int2((1 << 30) | (2 * m), 2 * m + 1));
+            for (int I = 0; I < nt; ++I) h.push_back(make_int2(I, I));
+            for (int m = 0; m < k; ++m) h.push_back(make_int2((2 << 30) | (2 * m), 2 * m + 1));
+            if ((int)h.size() != 2 * s->npairs + k) return fail("split tile-pair table size mismatch");
+            // the extra slot: only the split pairs' second halves write it (their rows), every other row 0
+            HIPCHK(hipMemsetAsync(s->dFpart + (size_t)nt * 3 * s->S, 0, (size_t)3 * s->S * sizeof(double), s->stream));
+        }
         HIPCHK(hipMemcpyAsync(s->dPairs, h.data(), h.size() * sizeof(int2), hipMemcpyHostToDevice, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
     }
@@ -931,6 +968,12 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_sort")) return s->use_n3b ? s->sort_mode : 0;
     if (!strcmp(n, "force_ax1")) return s->ax1_mode;
     if (!strcmp(n, "force_reduce_mask")) return s->tmask_mode;
+    if (!strcmp(n, "force_tile_split")) return s->split_opt;
+    if (!strcmp(n, "force_tile_split_pairs")) return s->nsplit;
+    if (!strcmp(n, "device_cus")) {                    // compute units of the context's device
+        int ncu = 0;
+        return hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->dev) == hipSuccess ? ncu : -1;
+    }
     if (!strcmp(n, "force_balance")) return s->balance_opt;
     if (!strcmp(n, "force_balance_ratio")) return s->balance_ratio;           // max / mean rank work (NaN: not sharded yet)
     if (!strcmp(n, "force_balance_ratio_equal")) return s->balance_ratio_eq;  // the same for equal block counts
@@ -1654,8 +1697,11 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         // one tile (N <= 64): its one slot has F's [3][S] layout, so the kernel writes F itself and
         // nothing is pending (the substep kernels read F when nseg == 1)
         const bool one_slot = s->nslots == 1;
-        a.R = s->dR; a.P = one_slot ? s->dF : s->dFpart; a.pairs = s->dPairs;
-        a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs;
+        // the split table (ensure_aux) unless the MD steps count tile arrivals (options overlap, fused_step:
+        // then every force call of the context takes the plain table)
+        const bool split = s->nsplit > 0 && !s->force_arrive && !one_slot && !s->overlap_opt && !s->fused_opt;
+        a.R = s->dR; a.P = one_slot ? s->dF : s->dFpart; a.pairs = split ? s->dPairs + s->npairs : s->dPairs;
+        a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs + (split ? s->nsplit : 0);
         ForceArgs c = force_args(s, nullptr);
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
         a.micGuard = c.micGuard;
@@ -1665,7 +1711,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         a.arrive = s->force_arrive;                // overlapped MD step: count finished workgroups
         HIPCHK(launch_forces_n3(a, s->force_variant, s->stream, e0, e1));
         s->f_pending = !one_slot;  // slots summed by the next substep launch (or settle_forces)
-        s->pend_nseg = s->nslots;
+        s->pend_nseg = s->nslots + (split ? 1 : 0);
     } else if (s->use_n3b) {
         if (n3b_balance(s)) return -1;
         N3BArgs a;
@@ -2880,6 +2926,12 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
             }
         }
         return 0;
+    }
+    if (!strcmp(name, "force_tile_split")) {           // Newton-3 tiles: the last round's whole tile pairs as halves
+        if (value < 0 || value > 1) return fail("force_tile_split must be 0 (off) or 1 (on)");
+        if (settle_forces(s)) return -1;
+        s->split_opt = value;
+        return ensure_aux(s);
     }
     if (!strcmp(name, "force_reduce_mask")) {          // Newton-3 blocks: the reduction reads only written j-slots
         if (value < 0 || value > 1) return fail("force_reduce_mask must be 0 (every j-slot) or 1 (the written ones)");

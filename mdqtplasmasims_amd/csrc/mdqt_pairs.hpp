@@ -353,6 +353,8 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
                                         double (*ia)[3][64]) {
     constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;   // pair_ft_cut
+    const int half = (int)((unsigned)I >> 30);      // 0 whole; 1 / 2 the first / second 8 of each wave's 16 steps
+    I &= 0x3FFFFFFF;
     const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int S = a.S, N = a.N;
     const double* X = a.R;
@@ -399,7 +401,11 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
             else if (t == 3 * n / 4) __builtin_amdgcn_s_setprio(0);
         }
     };
-    if (!diag) {
+    if (!diag && half) {                            // (MDQT_N3_WAVES 4: 16 steps per wave)
+        const int b = l + (64 / N3W) * q + (half - 1) * (32 / N3W);
+#pragma unroll
+        for (int t = 0; t < 32 / N3W; ++t) step(b + t, 1.);
+    } else if (!diag) {
         const int b = l + (64 / N3W) * q;
 #pragma unroll
         for (int t = 0; t < 64 / N3W; ++t) {
@@ -420,8 +426,8 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     __syncthreads();
     const size_t slab3 = POT ? (size_t)S : (size_t)3 * S;   // potential: [ntiles][S], one plane per slot
     constexpr int NK = POT ? 1 : 3;                 // potential: component 0 only, j side not negated
-    if (q == 0) {                                   // rows of I -> slot J (diagonal: I)
-        double* Pi = a.P + (size_t)J * slab3;
+    if (q == 0) {                                   // rows of I -> slot J (diagonal: I; a second half: ntiles)
+        double* Pi = a.P + (size_t)(half == 2 ? a.ntiles : J) * slab3;
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             double v = ia[0][k][l];
@@ -430,8 +436,8 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
             if (diag) v = POT ? v + n3_jsum(accj, k, l) : v - n3_jsum(accj, k, l);
             if (i < S) slot_store<SIG>(&Pi[(size_t)k * S + i], v);
         }
-    } else if (q == 1 && !diag) {                   // rows of J -> slot I
-        double* Pj = a.P + (size_t)I * slab3;
+    } else if (q == 1 && !diag) {                   // rows of J -> slot I (a second half: ntiles)
+        double* Pj = a.P + (size_t)(half == 2 ? a.ntiles : I) * slab3;
         const int j = J * 64 + l;
 #pragma unroll
         for (int k = 0; k < NK; ++k) {

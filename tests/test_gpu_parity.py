@@ -276,8 +276,9 @@ def test_c2_headline_qt_instance_matches_oracle(eng, orc):
     k_substeps_lanes_im<true, true, true> (FAST + IM01 + EDZ, no renormalisation: the reference's
     reNormalizewvFns = false) summing all 56 Newton-3 tile slots in its
     lane-distributed prologue (lane k: slots k, k + 16, k + 32, k + 48 — all 16 lanes busy only
-    at >= 49 slots), so a slot-sum bug shared with the thread-per-ion kernel cannot hide behind
-    a self-comparison.  SpeedUp:438-717 (qstep), :1369-1377 (the MD step's cadence)."""
+    at >= 49 slots) — 57 with the split tile pairs' extra slot (force_tile_split, on 256 CUs) — so
+    a slot-sum bug shared with the thread-per-ion kernel cannot hide behind a self-comparison.
+    SpeedUp:438-717 (qstep), :1369-1377 (the MD step's cadence)."""
     kw = dict(N0=3500, seed=12346, job=1, rng_mode=1)
     s = eng.Simulation(**kw).init()
     o = orc.OracleSim(nthreads=8, **kw).init()
@@ -287,7 +288,7 @@ def test_c2_headline_qt_instance_matches_oracle(eng, orc):
     s.md_steps(2); o.md_steps(2)
     assert s.const("force_scheme") == 2 and s.const("force_slots") == 56
     assert s.const("qt_kernel") == QTK_LANES_IM_EDZ, s.const("qt_kernel")
-    assert s.const("qt_kernel_nseg") == 56
+    assert s.const("qt_kernel_nseg") == 56 + (s.const("force_tile_split_pairs") > 0)
     a, b = s.get_state(), o.get_state()
     assert a["t"] == b["t"] and s.qstep_index == o.qstep_index == 75
     jumped_a = a["tPart"] < 3 * 25 * 8e-5 - 1e-12
@@ -728,6 +729,7 @@ def test_fused_md_step_bit_identical(eng, N0):
     out = []
     for fu in (0, 1):
         s = eng.Simulation(N0=N0, seed=73).init()
+        s.set_option("force_tile_split", 0)            # (the fused launch takes the plain tile-pair table)
         s.set_option("fused_step", fu)
         assert s.const("fused_step") == fu
         s.md_steps(30)
@@ -769,6 +771,7 @@ def test_fused_md_step_run_files_identical(eng, tmp_path):
     dirs = []
     for fu in (0, 1):
         s = eng.Simulation(saveDirectory=str(tmp_path / f"f{fu}") + "/", **kw)
+        s.set_option("force_tile_split", 0)
         s.set_option("fused_step", fu)
         s.run()
         dirs.append(s.save_directory)
@@ -787,6 +790,7 @@ def test_overlapped_md_step_bit_identical(eng, N0):
     out = []
     for ov in (0, 1):
         s = eng.Simulation(N0=N0, seed=71).init()
+        s.set_option("force_tile_split", 0)            # (the overlapped steps take the plain tile-pair table)
         s.set_option("overlap", ov)
         s.md_steps(30)
         s.synchronize()
@@ -796,3 +800,26 @@ def test_overlapped_md_step_bit_identical(eng, N0):
     for k in ("R", "V", "F", "psi", "tPart"):
         assert np.array_equal(a[k], b[k]), k
     assert (a["tPart"] < 30 * 0.002 - 1e-9).sum() > 0          # jumps happened
+
+def test_tile_split_of_the_last_round(eng):
+    """the tile kernel's last round of workgroups: the whole tile pairs left in it run as two half
+    workgroups (mdqt_engine.cpp tile_split_count; C2 on 256 CUs: 1,596 workgroups, 60 in the last
+    round, 56 of them diagonal — 4 split), the second halves' rows in one extra slot: the same pair
+    terms, summed in another order — within rounding of the plain table, and only on the split tiles"""
+    s = eng.Simulation(N0=3500, seed=12346, job=1).init()     # bench.py's C2: N = 3,573, 56 tiles
+    assert s.const("force_tile_split") == 1 and s.N == 3573
+    k = int(s.const("force_tile_split_pairs"))
+    if s.const("device_cus") == 256:                  # MI355X
+        assert k == 4
+    out = {}
+    for sp in (1, 0):
+        s.set_option("force_tile_split", sp)
+        s.forces()
+        out[sp] = s.get_state()["F"]
+    assert s.const("force_tile_split_pairs") == 0
+    s.close()
+    d = np.abs(out[1] - out[0])
+    print(f"C2 split tile pairs {k}: max|dF|/max|F| = {d.max() / np.abs(out[0]).max():.3e}")
+    assert d.max() <= 1e-13 * np.abs(out[0]).max()
+    assert not d[:, 2 * k * 64:].any()                 # only the split pairs' tiles 0 .. 2k - 1 differ
+    assert k == 0 or d.max() > 0                       # (the split ran: another summation order)

@@ -195,8 +195,9 @@ struct mdqt_ctx {
     int nslots = 0, npairs = 0, capPairs = 0;
     int2* dPairs = nullptr;        // (I, J) tile pair of every wave of the Newton-3 kernel; after the
                                    // npairs entries, the split table (nsplit > 0: ensure_aux)
-    int nsplit = 0;                // tile pairs the split table runs as two half workgroups
-    int split_opt = 1;             // option force_tile_split
+    int nsplit = 0;                // tile pairs the split table runs in parts (halves / quarters)
+    int nsplit_wg = 0;             // workgroups of the split table
+    int split_opt = 1;             // option force_tile_split: 0 off, 1 halves, 2 quarters (+ diagonal halves)
     // rng_mode 0: the reference's drand48 stream, consumed in ion order on the device
     unsigned long long* dX48 = nullptr;   // [1] stream state + [48] jA + [48] jC
     int* dFlags = nullptr;         // [0] set by the substep kernels when a position leaves [-L/8, 9L/8]
@@ -690,6 +691,10 @@ static void choose_segments(mdqt_ctx* s) {
 // their rows into one extra slot (ntiles; the split pairs have disjoint tiles, (0, 1), (2, 3), ...,
 // and every other row of that slot stays 0), so F = the sum of ntiles + 1 slots.  The overlapped and
 // fused MD steps (tile arrival counts) keep the plain table.
+// Option 2 (quarters) runs those tile pairs in four parts and every diagonal tile in two: the last
+// round is then 4 k + 2 nt quarter-size workgroups (C2: 128), so its CUs carry 6.25 tile pairs of work
+// instead of 6.5.  Extra slots ntiles + 0 .. 3 (the diagonal tiles' second halves: + 0).
+constexpr int kSplitSlots = 4;
 static int tile_split_count(const mdqt_ctx* s, int nt) {
     if (!s->split_opt || nt < 2) return 0;
     int ncu = 0;
@@ -697,13 +702,14 @@ static int tile_split_count(const mdqt_ctx* s, int nt) {
     const long w0 = (long)nt * (nt + 1) / 2;
     if (w0 <= ncu || w0 > 8L * ncu) return 0;    // one round (nothing to balance) / many (dispatched as CUs free up)
     const int k = (int)(w0 % ncu) - nt;          // whole tile pairs in the last round
-    return (k > 0 && nt + 2 * k <= ncu && 2 * k <= nt) ? k : 0;
+    const int last = s->split_opt == 2 ? 4 * k + 2 * nt : 2 * k + nt;   // workgroups of the last round
+    return (k > 0 && last <= ncu && 2 * k <= nt) ? k : 0;
 }
 
 static int ensure_aux(mdqt_ctx* s) {
     const int nt_split = (s->N + 63) / 64;
     s->nsplit = s->use_n3 && s->npairs > 0 ? tile_split_count(s, nt_split) : 0;
-    const int need = std::max(std::max(s->nseg, s->nslots + (s->nsplit > 0 ? 1 : 0)), 2);
+    const int need = std::max(std::max(s->nseg, s->nslots + (s->nsplit > 0 ? kSplitSlots : 0)), 2);
     if (need > s->capNseg) {
         if (s->dFpart) HIPCHK(hipFree(s->dFpart));
         s->dFpart = nullptr;
@@ -748,7 +754,7 @@ static int ensure_aux(mdqt_ctx* s) {
         }
     }
     if (s->use_n3 && s->npairs > 0) {
-        const int tot = s->npairs + (s->nsplit > 0 ? s->npairs + s->nsplit : 0);
+        const int tot = s->npairs + (s->nsplit > 0 ? s->npairs + 3 * s->nsplit + s->npairs : 0);   // (bound)
         if (tot > s->capPairs) {
             if (s->dPairs) HIPCHK(hipFree(s->dPairs));
             s->dPairs = nullptr;
@@ -769,15 +775,25 @@ static int ensure_aux(mdqt_ctx* s) {
         if (s->nsplit > 0) {                         // the split table (tile_split_count)
             const int k = s->nsplit;
             auto split = [&](int I, int J) { return J == I + 1 && (I & 1) == 0 && I < 2 * k; };
+            auto part = [](int I, int pl, int p) { return (int)(((unsigned)pl << 30) | ((unsigned)p << 28) | (unsigned)I); };
             for (int I = 0; I < nt; ++I)
                 for (int J = I + 1; J < nt; ++J)
                     if (!split(I, J)) h.push_back(make_int2(I, J));
-            for (int m = 0; m < k; ++m) h.push_back(make_int2((1 << 30) | (2 * m), 2 * m + 1));
-            for (int I = 0; I < nt; ++I) h.push_back(make_int2(I, I));
-            for (int m = 0; m < k; ++m) h.push_back(make_int2((2 << 30) | (2 * m), 2 * m + 1));
-            if ((int)h.size() != 2 * s->npairs + k) return fail("split tile-pair table size mismatch");
-            // the extra slot: only the split pairs' second halves write it (their rows), every other row 0
-            HIPCHK(hipMemsetAsync(s->dFpart + (size_t)nt * 3 * s->S, 0, (size_t)3 * s->S * sizeof(double), s->stream));
+            if (s->split_opt == 2) {                 // quarters of the split pairs, halves of the diagonal tiles
+                for (int p = 0; p < 4; ++p)
+                    for (int m = 0; m < k; ++m) h.push_back(make_int2(part(2 * m, 2, p), 2 * m + 1));
+                for (int p = 0; p < 2; ++p)
+                    for (int I = 0; I < nt; ++I) h.push_back(make_int2(part(I, 1, p), I));
+            } else {                                 // halves of the split pairs around the diagonal tiles
+                for (int m = 0; m < k; ++m) h.push_back(make_int2(part(2 * m, 1, 0), 2 * m + 1));
+                for (int I = 0; I < nt; ++I) h.push_back(make_int2(I, I));
+                for (int m = 0; m < k; ++m) h.push_back(make_int2(part(2 * m, 1, 1), 2 * m + 1));
+            }
+            s->nsplit_wg = (int)h.size() - s->npairs;
+            if (s->nsplit_wg != s->npairs + (s->split_opt == 2 ? 3 * k + nt : k)) return fail("split tile-pair table size mismatch");
+            // the extra slots: only later parts of split tile pairs write them (their rows), every other row 0
+            HIPCHK(hipMemsetAsync(s->dFpart + (size_t)nt * 3 * s->S, 0, (size_t)kSplitSlots * 3 * s->S * sizeof(double),
+                                  s->stream));
         }
         HIPCHK(hipMemcpyAsync(s->dPairs, h.data(), h.size() * sizeof(int2), hipMemcpyHostToDevice, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
@@ -1701,7 +1717,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         // then every force call of the context takes the plain table)
         const bool split = s->nsplit > 0 && !s->force_arrive && !one_slot && !s->overlap_opt && !s->fused_opt;
         a.R = s->dR; a.P = one_slot ? s->dF : s->dFpart; a.pairs = split ? s->dPairs + s->npairs : s->dPairs;
-        a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = s->npairs + (split ? s->nsplit : 0);
+        a.N = s->N; a.S = s->S; a.ntiles = (s->N + 63) / 64; a.npairs = split ? s->nsplit_wg : s->npairs;
         ForceArgs c = force_args(s, nullptr);
         a.L = c.L; a.lDeb = c.lDeb; a.Rcut = c.Rcut; a.invlDeb = c.invlDeb; a.micT = c.micT;
         a.micGuard = c.micGuard;
@@ -1711,7 +1727,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         a.arrive = s->force_arrive;                // overlapped MD step: count finished workgroups
         HIPCHK(launch_forces_n3(a, s->force_variant, s->stream, e0, e1));
         s->f_pending = !one_slot;  // slots summed by the next substep launch (or settle_forces)
-        s->pend_nseg = s->nslots + (split ? 1 : 0);
+        s->pend_nseg = s->nslots + (split ? kSplitSlots : 0);
     } else if (s->use_n3b) {
         if (n3b_balance(s)) return -1;
         N3BArgs a;
@@ -2928,7 +2944,7 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         return 0;
     }
     if (!strcmp(name, "force_tile_split")) {           // Newton-3 tiles: the last round's whole tile pairs as halves
-        if (value < 0 || value > 1) return fail("force_tile_split must be 0 (off) or 1 (on)");
+        if (value < 0 || value > 2) return fail("force_tile_split must be 0 (off), 1 (halves) or 2 (quarters)");
         if (settle_forces(s)) return -1;
         s->split_opt = value;
         return ensure_aux(s);

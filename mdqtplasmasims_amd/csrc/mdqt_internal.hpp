@@ -399,8 +399,8 @@ __device__ __forceinline__ double slot_sum16(const double* __restrict__ p, size_
 struct N3Args {
     const double* R;    // [3][S] (world_size 1)
     double* P;          // [ntiles][3][S]
-    const int2* pairs;  // (I, J) of every workgroup; I's bits 30-31: 0 the whole tile pair, 1 / 2 its first /
-                        // second half of the rotation steps (the second half's rows go to slot ntiles)
+    const int2* pairs;  // (I, J) of every workgroup; I's bits 28-31: a part of the tile pair's rotation
+                        // steps (mdqt_pairs.hpp n3_tile; later parts write the extra slots ntiles + 0..3)
     int N, S, ntiles, npairs;
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;          // as ForceArgs::guard (exact variant only; the fast one needs no guard)

@@ -353,8 +353,13 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
                                         double (*pj)[128], double (*accj)[3][128], double* mj,
                                         double (*ia)[3][64]) {
     constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;   // pair_ft_cut
-    const int half = (int)((unsigned)I >> 30);      // 0 whole; 1 / 2 the first / second 8 of each wave's 16 steps
-    I &= 0x3FFFFFFF;
+    // a part of the tile pair (the split table, mdqt_engine.cpp tile_split_count): I's bits 30-31 = log2 of
+    // the parts (0 whole, 1 halves, 2 quarters), bits 28-29 = which part — each wave's rotation steps in
+    // that many consecutive runs; part p > 0 writes its rows into the extra slot ntiles + p (a diagonal
+    // tile's second half: ntiles)
+    const int pl = (int)((unsigned)I >> 30), part = (I >> 28) & 3;
+    I &= 0x0FFFFFFF;
+    static_assert(N3W == 4, "the split table assumes 16 rotation steps per wave");
     const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int S = a.S, N = a.N;
     const double* X = a.R;
@@ -401,10 +406,20 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
             else if (t == 3 * n / 4) __builtin_amdgcn_s_setprio(0);
         }
     };
-    if (!diag && half) {                            // (MDQT_N3_WAVES 4: 16 steps per wave)
-        const int b = l + (64 / N3W) * q + (half - 1) * (32 / N3W);
+    if (!diag && pl) {                              // steps [part 16 / 2^pl, (part + 1) 16 / 2^pl)
+        const int b = l + (64 / N3W) * q + part * ((64 / N3W) >> pl);
+        if (pl == 1) {
 #pragma unroll
-        for (int t = 0; t < 32 / N3W; ++t) step(b + t, 1.);
+            for (int t = 0; t < 8; ++t) step(b + t, 1.);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) step(b + t, 1.);
+        }
+    } else if (diag && pl) {                        // a diagonal tile's 8 steps per wave in two halves
+        const int b = l + 1 + (32 / N3W) * q + 4 * part;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) step(b + t, 1.);
+        step(b + 3, (part == 1 && q == N3W - 1 && l >= 32) ? 0. : 1.);   // lane distance 32: once per pair
     } else if (!diag) {
         const int b = l + (64 / N3W) * q;
 #pragma unroll
@@ -426,8 +441,9 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     __syncthreads();
     const size_t slab3 = POT ? (size_t)S : (size_t)3 * S;   // potential: [ntiles][S], one plane per slot
     constexpr int NK = POT ? 1 : 3;                 // potential: component 0 only, j side not negated
-    if (q == 0) {                                   // rows of I -> slot J (diagonal: I; a second half: ntiles)
-        double* Pi = a.P + (size_t)(half == 2 ? a.ntiles : J) * slab3;
+    const int xs = part == 0 ? -1 : diag ? a.ntiles : a.ntiles + part;   // a later part's extra slot
+    if (q == 0) {                                   // rows of I -> slot J (diagonal: I; a later part: xs)
+        double* Pi = a.P + (size_t)(xs >= 0 ? xs : J) * slab3;
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             double v = ia[0][k][l];
@@ -436,8 +452,8 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
             if (diag) v = POT ? v + n3_jsum(accj, k, l) : v - n3_jsum(accj, k, l);
             if (i < S) slot_store<SIG>(&Pi[(size_t)k * S + i], v);
         }
-    } else if (q == 1 && !diag) {                   // rows of J -> slot I (a second half: ntiles)
-        double* Pj = a.P + (size_t)(half == 2 ? a.ntiles : I) * slab3;
+    } else if (q == 1 && !diag) {                   // rows of J -> slot I (a later part: xs)
+        double* Pj = a.P + (size_t)(xs >= 0 ? xs : I) * slab3;
         const int j = J * 64 + l;
 #pragma unroll
         for (int k = 0; k < NK; ++k) {

@@ -288,7 +288,7 @@ def test_c2_headline_qt_instance_matches_oracle(eng, orc):
     s.md_steps(2); o.md_steps(2)
     assert s.const("force_scheme") == 2 and s.const("force_slots") == 56
     assert s.const("qt_kernel") == QTK_LANES_IM_EDZ, s.const("qt_kernel")
-    assert s.const("qt_kernel_nseg") == 56 + (s.const("force_tile_split_pairs") > 0)
+    assert s.const("qt_kernel_nseg") == 56 + 4 * (s.const("force_tile_split_pairs") > 0)   # + the split's slots
     a, b = s.get_state(), o.get_state()
     assert a["t"] == b["t"] and s.qstep_index == o.qstep_index == 75
     jumped_a = a["tPart"] < 3 * 25 * 8e-5 - 1e-12
@@ -802,24 +802,28 @@ def test_overlapped_md_step_bit_identical(eng, N0):
     assert (a["tPart"] < 30 * 0.002 - 1e-9).sum() > 0          # jumps happened
 
 def test_tile_split_of_the_last_round(eng):
-    """the tile kernel's last round of workgroups: the whole tile pairs left in it run as two half
-    workgroups (mdqt_engine.cpp tile_split_count; C2 on 256 CUs: 1,596 workgroups, 60 in the last
-    round, 56 of them diagonal — 4 split), the second halves' rows in one extra slot: the same pair
-    terms, summed in another order — within rounding of the plain table, and only on the split tiles"""
+    """the tile kernel's last round of workgroups: the whole tile pairs left in it run in parts
+    (mdqt_engine.cpp tile_split_count; C2 on 256 CUs: 1,596 workgroups, 60 in the last round, 56 of
+    them diagonal — 4 split), later parts' rows in extra slots: the same pair terms, summed in another
+    order — within rounding of the plain table; halves (option 1) change only the split pairs' tiles,
+    quarters (option 2) halve every diagonal tile as well"""
     s = eng.Simulation(N0=3500, seed=12346, job=1).init()     # bench.py's C2: N = 3,573, 56 tiles
-    assert s.const("force_tile_split") == 1 and s.N == 3573
-    k = int(s.const("force_tile_split_pairs"))
-    if s.const("device_cus") == 256:                  # MI355X
-        assert k == 4
-    out = {}
-    for sp in (1, 0):
+    assert s.N == 3573
+    out, ks = {}, {}
+    for sp in (2, 1, 0):
         s.set_option("force_tile_split", sp)
+        ks[sp] = int(s.const("force_tile_split_pairs"))
         s.forces()
         out[sp] = s.get_state()["F"]
-    assert s.const("force_tile_split_pairs") == 0
+    cus = s.const("device_cus")
     s.close()
-    d = np.abs(out[1] - out[0])
-    print(f"C2 split tile pairs {k}: max|dF|/max|F| = {d.max() / np.abs(out[0]).max():.3e}")
-    assert d.max() <= 1e-13 * np.abs(out[0]).max()
-    assert not d[:, 2 * k * 64:].any()                 # only the split pairs' tiles 0 .. 2k - 1 differ
-    assert k == 0 or d.max() > 0                       # (the split ran: another summation order)
+    if cus == 256:                                    # MI355X
+        assert ks[1] == 4 and ks[2] == 4
+    assert ks[0] == 0
+    scale = np.abs(out[0]).max()
+    for sp in (1, 2):
+        d = np.abs(out[sp] - out[0])
+        print(f"C2 split {sp} ({ks[sp]} tile pairs): max|dF|/max|F| = {d.max() / scale:.3e}")
+        assert d.max() <= 1e-13 * scale
+        assert ks[sp] == 0 or d.max() > 0              # (the split ran: another summation order)
+    assert not np.abs(out[1] - out[0])[:, 2 * ks[1] * 64:].any()   # halves: only the split pairs' tiles

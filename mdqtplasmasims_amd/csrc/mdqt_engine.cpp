@@ -693,8 +693,9 @@ static void choose_segments(mdqt_ctx* s) {
 // fused MD steps (tile arrival counts) keep the plain table.
 // Option 2 (quarters) runs those tile pairs in four parts and every diagonal tile in two: the last
 // round is then 4 k + 2 nt quarter-size workgroups (C2: 128), so its CUs carry 6.25 tile pairs of work
-// instead of 6.5.  Extra slots ntiles + 0 .. 3 (the diagonal tiles' second halves: + 0).
-constexpr int kSplitSlots = 4;
+// instead of 6.5 (measured: the same launch time as halves, profiles/r05n_tile_split_quarters_ab.txt).
+// Extra slots: halves ntiles; quarters ntiles + 0 .. 2 (parts 1-3) and ntiles + 3 (diagonal halves).
+static int split_slots(const mdqt_ctx* s) { return s->nsplit > 0 ? (s->split_opt == 2 ? 4 : 1) : 0; }
 static int tile_split_count(const mdqt_ctx* s, int nt) {
     if (!s->split_opt || nt < 2) return 0;
     int ncu = 0;
@@ -709,7 +710,7 @@ static int tile_split_count(const mdqt_ctx* s, int nt) {
 static int ensure_aux(mdqt_ctx* s) {
     const int nt_split = (s->N + 63) / 64;
     s->nsplit = s->use_n3 && s->npairs > 0 ? tile_split_count(s, nt_split) : 0;
-    const int need = std::max(std::max(s->nseg, s->nslots + (s->nsplit > 0 ? kSplitSlots : 0)), 2);
+    const int need = std::max(std::max(s->nseg, s->nslots + split_slots(s)), 2);
     if (need > s->capNseg) {
         if (s->dFpart) HIPCHK(hipFree(s->dFpart));
         s->dFpart = nullptr;
@@ -792,7 +793,7 @@ static int ensure_aux(mdqt_ctx* s) {
             s->nsplit_wg = (int)h.size() - s->npairs;
             if (s->nsplit_wg != s->npairs + (s->split_opt == 2 ? 3 * k + nt : k)) return fail("split tile-pair table size mismatch");
             // the extra slots: only later parts of split tile pairs write them (their rows), every other row 0
-            HIPCHK(hipMemsetAsync(s->dFpart + (size_t)nt * 3 * s->S, 0, (size_t)kSplitSlots * 3 * s->S * sizeof(double),
+            HIPCHK(hipMemsetAsync(s->dFpart + (size_t)nt * 3 * s->S, 0, (size_t)split_slots(s) * 3 * s->S * sizeof(double),
                                   s->stream));
         }
         HIPCHK(hipMemcpyAsync(s->dPairs, h.data(), h.size() * sizeof(int2), hipMemcpyHostToDevice, s->stream));
@@ -1727,7 +1728,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         a.arrive = s->force_arrive;                // overlapped MD step: count finished workgroups
         HIPCHK(launch_forces_n3(a, s->force_variant, s->stream, e0, e1));
         s->f_pending = !one_slot;  // slots summed by the next substep launch (or settle_forces)
-        s->pend_nseg = s->nslots + (split ? kSplitSlots : 0);
+        s->pend_nseg = s->nslots + (split ? split_slots(s) : 0);
     } else if (s->use_n3b) {
         if (n3b_balance(s)) return -1;
         N3BArgs a;

@@ -400,7 +400,7 @@ struct N3Args {
     const double* R;    // [3][S] (world_size 1)
     double* P;          // [ntiles][3][S]
     const int2* pairs;  // (I, J) of every workgroup; I's bits 28-31: a part of the tile pair's rotation
-                        // steps (mdqt_pairs.hpp n3_tile; later parts write the extra slots ntiles + 0..3)
+                        // steps (mdqt_pairs.hpp n3_tile; later parts write the extra slots from ntiles on)
     int N, S, ntiles, npairs;
     double L, lDeb, Rcut, invlDeb, micT, micGuard;
     int guard;          // as ForceArgs::guard (exact variant only; the fast one needs no guard)

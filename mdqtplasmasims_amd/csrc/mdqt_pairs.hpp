@@ -355,8 +355,8 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;   // pair_ft_cut
     // a part of the tile pair (the split table, mdqt_engine.cpp tile_split_count): I's bits 30-31 = log2 of
     // the parts (0 whole, 1 halves, 2 quarters), bits 28-29 = which part — each wave's rotation steps in
-    // that many consecutive runs; part p > 0 writes its rows into the extra slot ntiles + p (a diagonal
-    // tile's second half: ntiles)
+    // that many consecutive runs; part p > 0 writes its rows into the extra slot ntiles + p - 1 (a diagonal
+    // tile's second half: ntiles + 3)
     const int pl = (int)((unsigned)I >> 30), part = (I >> 28) & 3;
     I &= 0x0FFFFFFF;
     static_assert(N3W == 4, "the split table assumes 16 rotation steps per wave");
@@ -441,7 +441,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     __syncthreads();
     const size_t slab3 = POT ? (size_t)S : (size_t)3 * S;   // potential: [ntiles][S], one plane per slot
     constexpr int NK = POT ? 1 : 3;                 // potential: component 0 only, j side not negated
-    const int xs = part == 0 ? -1 : diag ? a.ntiles : a.ntiles + part;   // a later part's extra slot
+    const int xs = part == 0 ? -1 : diag ? a.ntiles + 3 : a.ntiles + part - 1;   // a later part's extra slot
     if (q == 0) {                                   // rows of I -> slot J (diagonal: I; a later part: xs)
         double* Pi = a.P + (size_t)(xs >= 0 ? xs : J) * slab3;
 #pragma unroll

@@ -288,7 +288,7 @@ def test_c2_headline_qt_instance_matches_oracle(eng, orc):
     s.md_steps(2); o.md_steps(2)
     assert s.const("force_scheme") == 2 and s.const("force_slots") == 56
     assert s.const("qt_kernel") == QTK_LANES_IM_EDZ, s.const("qt_kernel")
-    assert s.const("qt_kernel_nseg") == 56 + 4 * (s.const("force_tile_split_pairs") > 0)   # + the split's slots
+    assert s.const("qt_kernel_nseg") == 56 + (s.const("force_tile_split_pairs") > 0)   # + the split's slot
     a, b = s.get_state(), o.get_state()
     assert a["t"] == b["t"] and s.qstep_index == o.qstep_index == 75
     jumped_a = a["tPart"] < 3 * 25 * 8e-5 - 1e-12

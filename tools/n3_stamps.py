@@ -16,9 +16,9 @@ for _ in range(3):
 s.synchronize()
 s.forces()
 s.synchronize()
-n = s.counters and 1596
 ntiles = (s.N + 63) // 64
-n = ntiles * (ntiles + 1) // 2
+k = int(s.const("force_tile_split_pairs"))         # the split table's extra workgroups (halves)
+n = ntiles * (ntiles + 1) // 2 + (k if s.const("force_tile_split") == 1 else 0)
 buf = (C.c_ulonglong * (6 * n))()
 assert lib().mdqt_expt_n3_stamps(buf, n) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 6).astype(np.int64)

@@ -31,6 +31,8 @@ FP64_PEAK_TFS = 78.6       # MI355X fp64 vector (spec), SURVEY §8d
 B_Q_PER_ION = 520.0        # algorithmic bytes per ion per fused-substep launch
 F_Q_PER_QSTEP = 1750.0     # fp64 flop per particle-qstep
 W_F_PER_PAIR = 30.0        # fp64 flop per distinct pair
+FP32_PEAK_TFS = 157.3      # MI355X fp32 vector (spec): the roof of the block kernel's f32 ultra-far form
+F32_TIERS = ("ufar32_uniform",)   # census classes whose pair terms run in f32 (mdqt_forces.hip n3b_group_uf32)
 
 METRIC = "particle-steps/sec (MD+QT) at N=3.5k and N=1M; 1/2/4/8-GPU scaling"
 LINE_MAX_BYTES = 8192      # the driver parses the last stdout line; VERDICT r04 item 1
@@ -65,6 +67,9 @@ def parse():
     ap.add_argument("--no-e2e-line", action="store_true",
                     help="skip the end-to-end line (reference cadence: output() every sampleFreq MD steps)")
     ap.add_argument("--e2e-md-steps", type=int, default=400)
+    ap.add_argument("--e2e-large", default="c5,c1m",
+                    help="comma-separated large configs with an end-to-end line (mdqt_run, output every 40 MD "
+                         "steps: 40 more MD steps and one output), or none")
     ap.add_argument("--no-replicas-line", action="store_true",
                     help="skip the jobs-per-GPU line (k independent C2 jobs sharing one GPU)")
     ap.add_argument("--secondary-deadline", type=float, default=420.0,
@@ -520,6 +525,10 @@ def main():
         dog.run("jobs_per_gpu", lambda: replicas_line(local, args.config))
     if world == 1 and not args.no_e2e_line:
         dog.run("end_to_end", lambda: end_to_end_line(local, args.config, args.e2e_md_steps))
+    if world == 1 and not args.no_e2e_line and args.e2e_large != "none":
+        for cfg in args.e2e_large.split(","):
+            name = "end_to_end_" + ("1m" if cfg == "c1m" else cfg)
+            dog.run(name, lambda cfg=cfg: end_to_end_line(local, cfg, 40, base=40, warm=False))
     # one large system sharded over all ranks (RCCL all-gather / reduce-scatter per MD step)
     in_child = args.sharded_in_child == 1 or (args.sharded_in_child == -1 and world > 1)
 
@@ -675,13 +684,24 @@ HEAD_CONFIG_KEYS = ("workload", "N", "md_steps", "qsteps_per_md_step", "particle
 HEAD_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "avg_launch_us",
                   "hbm_frac_8d", "traffic_frac", "compulsory_hbm_frac")
 HEAD_CPU_KEYS = ("value", "unit", "cores", "kind", "sample")
-LINE_KEYS = ("value", "unit", "N", "n_gpus", "ms_per_md_step")
-LINE_ROOF_KEYS = ("bound", "frac", "algorithmic_equivalent_frac", "pairs_evaluated_frac", "block_kernel_ms",
-                  "load_imbalance")
+LINE_KEYS = ("value", "unit", "N", "n_gpus", "ms_per_md_step", "force_breakdown_ms")
+LINE_ROOF_KEYS = ("bound", "frac", "fp64_frac", "f32_frac", "algorithmic_equivalent_frac", "pairs_evaluated_frac",
+                  "block_kernel_ms", "load_imbalance")
 
 
 def _pick(d, keys):
     return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _sig(x, n=5):
+    """floats of a secondary line in brief to n significant digits (the detail line keeps them whole)"""
+    if isinstance(x, float):
+        return float(f"{x:.{n}g}")
+    if isinstance(x, dict):
+        return {k: _sig(v, n) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_sig(v, n) for v in x]
+    return x
 
 
 def compact_secondary(name, v):
@@ -714,6 +734,9 @@ def compact_secondary(name, v):
     ft = v.get("force_tail")
     if isinstance(ft, dict) and "bound_met" in ft:
         c["force_tail_bound_met"] = ft["bound_met"]
+    ep = v.get("epotential")
+    if isinstance(ep, dict):
+        c["epot_ms"] = ep.get("wall_ms")
     return c
 
 
@@ -727,7 +750,7 @@ def compact_line(out):
     h["cpu_baseline"] = _pick(cb, HEAD_CPU_KEYS) if isinstance(cb, dict) else None
     if isinstance(cb, dict) and isinstance(cb.get("single_thread"), dict):
         h["cpu_baseline"]["single_thread_value"] = cb["single_thread"].get("value")
-    sec = {k: compact_secondary(k, v) for k, v in out.items() if k not in HEAD_KEYS and k not in
+    sec = {k: _sig(compact_secondary(k, v)) for k, v in out.items() if k not in HEAD_KEYS and k not in
            ("config", "roofline", "cpu_baseline", "secondary_errors", "run_s")}
     h["lines"] = sec
     if out.get("secondary_errors"):
@@ -825,11 +848,14 @@ def replicas_line(local, cfg, counts=(2, 4, 8), steps=100):
             "lines": res}
 
 
-def end_to_end_line(local, cfg, md_steps):
+def end_to_end_line(local, cfg, md_steps, base=40, warm=True):
     """mdqt_run() (SpeedUp main() loop :1248-1383) with the reference cadence: output() every
     sampleFreq = 40 MD steps (energies, KDE velocity distributions, state populations files),
     writeConditions at the end, files written.  mdqt_run() starts with init() (newRun = 1), so the
-    rate is differential: two runs to different tmax, value = extra particle-qsteps / extra wall."""
+    rate is differential: two runs to different tmax (base and base + md_steps MD steps), value = extra
+    particle-qsteps (particle-MD-steps without QT) / extra wall: init() and the final writeConditions
+    cancel, the MD steps and the outputs between remain.  Large configs (C5, N = 1M):
+    md_steps = 40, one output() — its Epotential() on the force call's plan — per 40 MD steps."""
     import tempfile
     import mdqtplasmasims_amd as M
     params, qt, desc = CONFIGS[cfg]
@@ -847,14 +873,21 @@ def end_to_end_line(local, cfg, md_steps):
             sim.close()
         return res
 
-    one(40)                                              # warm-up (module load, first allocations)
-    a, b = one(40), one(40 + md_steps)
+    if warm:
+        one(base)                                        # warm-up (module load, first allocations)
+    a, b = one(base), one(base + md_steps)
     el, dq = b["wall"] - a["wall"], b["q"] - a["q"]
-    return {"workload": desc + f", mdqt_run() with output() every 40 MD steps (files written): "
-                               f"run to {b['c0']} MD steps minus run to {a['c0']}",
-            "N": b["N"], "md_steps": b["c0"] - a["c0"], "qsteps": dq, "outputs": b["c0"] // 40 - a["c0"] // 40,
-            "files_long_run": b["files"], "wall_s": el, "wall_s_long_run_incl_init": b["wall"],
-            "value": b["N"] * dq / el, "unit": "particle-qsteps/s"}
+    dmd = b["c0"] - a["c0"]
+    res = {"workload": desc + f", mdqt_run() with output() every 40 MD steps (files written): "
+                              f"run to {b['c0']} MD steps minus run to {a['c0']}",
+           "N": b["N"], "md_steps": dmd, "qsteps": dq, "outputs": (b["c0"] + 1) // 40 - (a["c0"] + 1) // 40,
+           "files_long_run": b["files"], "wall_s": el, "wall_s_long_run_incl_init": b["wall"],
+           "ms_per_md_step": el / dmd * 1e3 if dmd else None}
+    if qt:
+        res.update(value=b["N"] * dq / el, unit="particle-qsteps/s")
+    else:
+        res.update(value=b["N"] * dmd / el, unit="particle-MD-steps/s")
+    return res
 
 
 # the large-N dominant kernel: its plain instance, or (C3, C5: the skip radius reaches the image
@@ -872,11 +905,13 @@ def latest_large_pmc(cfg):
 
 
 def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None):
-    """Roofline of a large line's dominant kernel, k_pairs_n3b.  FP64 VALU is the roof (30
-    flop per distinct pair, ~0 B per pair after staging).  `frac` is the block kernel's own rate on the
-    pairs it evaluates: 30 flop x the census's evaluated lane-steps (skipped tile
-    pairs and sub-tile groups excluded, every pair form counted) / the kernel's average duration from
-    its own HIP dispatch timestamps (k_avg, the timed force calls) / (world x 78.6 TF).  Beside it:
+    """Roofline of a large line's dominant kernel, k_pairs_n3b.  VALU is the roof (30 flop per
+    distinct pair, ~0 B per pair after staging).  `frac` is the block kernel's own rate on the pairs it
+    evaluates, time-weighted over its two precisions: 30 flop x
+    the census's f64 lane-steps / (world x 78.6 TF) plus 30 flop x its f32 lane-steps (the ultra-far f32
+    form, ufar32_uniform) / (world x 157.3 TF) — the time at the roofs — over the kernel's average
+    duration from its own HIP dispatch timestamps (k_avg, the timed force calls); skipped tile pairs and
+    sub-tile groups excluded.  fp64_frac / f32_frac are the two terms.  Beside it:
     algorithmic_equivalent_frac — all N(N-1)/2 pairs in the same time, what 8(d) defines — and
     pairs_evaluated_frac, the evaluated share; force_call_frac — all pairs over the whole forces() call
     (sort, plan, kernel, reduction, tail pass, collectives).  With a PMC summary of the same config
@@ -884,13 +919,26 @@ def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None):
     pair, the VALU issue-slot fraction, and the kernel's duration from the kernel trace."""
     tot = N * (N - 1) / 2.0
     ev = sum(v[0] for k, v in census.items() if not k.startswith("skip"))
-    peak = FP64_PEAK_TFS * world
+    ev32 = sum(v[0] for k, v in census.items() if k in F32_TIERS)     # lane-steps in f32 (packed) pair forms
+    ev64 = ev - ev32
+    # mixed precision (VERDICT r05 item 3): the f64 lane-steps against the fp64 roof, the f32 ones against
+    # the fp32 roof; frac = the time both would take at their roofs / the kernel's time (time-weighted),
+    # `peak` the matching mixed roof, so that achieved / peak = frac
+    t64 = W_F_PER_PAIR * ev64 / (FP64_PEAK_TFS * world * 1e12)
+    t32 = W_F_PER_PAIR * ev32 / (FP32_PEAK_TFS * world * 1e12)
+    peak = W_F_PER_PAIR * ev / (t64 + t32) / 1e12 if ev else FP64_PEAK_TFS * world
+    peak64 = FP64_PEAK_TFS * world
     t = k_avg if k_avg else f_avg
-    roof = {"bound": "fp64", "kernel": N3B_KERNEL, "unit": "TFLOP/s", "peak": peak,
-            "achieved": W_F_PER_PAIR * ev / t / 1e12, "frac": W_F_PER_PAIR * ev / t / 1e12 / peak,
-            "algorithmic_equivalent_frac": W_F_PER_PAIR * tot / t / 1e12 / peak,
+    roof = {"bound": "fp64+fp32" if ev32 else "fp64", "kernel": N3B_KERNEL, "unit": "TFLOP/s", "peak": peak,
+            "achieved": W_F_PER_PAIR * ev / t / 1e12, "frac": (t64 + t32) / t,
+            "fp64_pairs_frac": ev64 / ev if ev else None, "f32_pairs_frac": ev32 / ev if ev else None,
+            "fp64_frac": t64 / t, "f32_frac": t32 / t,
+            "roofs": {"fp64": peak64, "fp32": FP32_PEAK_TFS * world,
+                      "note": "frac = fp64_frac + f32_frac: 30 flop x the f64 lane-steps / fp64 roof + 30 flop x the "
+                              "f32 lane-steps (ufar32_uniform) / fp32 roof, over the kernel's time"},
+            "algorithmic_equivalent_frac": W_F_PER_PAIR * tot / t / 1e12 / peak64,
             "pairs_evaluated_frac": ev / tot,
-            "force_call_frac": W_F_PER_PAIR * tot / f_avg / 1e12 / peak,
+            "force_call_frac": W_F_PER_PAIR * tot / f_avg / 1e12 / peak64,
             "block_kernel_ms": k_avg * 1e3 if k_avg else None, "force_call_ms": f_avg * 1e3,
             "evaluated_lane_steps": ev,
             "time": "k_pairs_n3b's own dispatch timestamps (HIP events, every timed force call; max over ranks)"
@@ -923,8 +971,8 @@ def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None):
     if e.get("duration_us"):
         ks = e["duration_us"] * 1e-6
         p.update(kernel_us=e["duration_us"], clock_ghz=cyc / ks / 1e9 if cyc else None,
-                 fp64_frac_algorithmic_kernel=W_F_PER_PAIR * tot / ks / 1e12 / peak,
-                 fp64_frac_evaluated_kernel=W_F_PER_PAIR * ev / ks / 1e12 / peak)
+                 algorithmic_equivalent_frac_pmc=W_F_PER_PAIR * tot / ks / 1e12 / peak64,
+                 evaluated_frac_pmc=(t64 + t32) / ks)
     if "FETCH_SIZE" in e and "WRITE_SIZE" in e:    # kB; FETCH x 2 per MI355X_MICROARCH.md (gfx950)
         roof["traffic"] = (2.0 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
     roof["pmc"] = p
@@ -957,20 +1005,34 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
         F0 = sim.get_state()["F"]
     sim.md_steps(1)
     barrier()
-    sim.enable_timing(1)
+    # kinds: force calls, fused substeps, and the force-call breakdown (bit 3: events between the stages)
+    sim.enable_timing(1, kinds=1 | 2 | 8)
     t0 = time.perf_counter()
     sim.md_steps(steps)
     sim.synchronize()
     barrier()
     el = time.perf_counter() - t0
     kt = sim.kernel_times()
+    bd = sim.force_breakdown()
     f_ms, nf, s_ms, ns = kt["force_ms"], kt["n_force"], kt["substep_ms"], kt["n_substep"]
     k_avg = kt["block_ms"] / kt["n_block"] * 1e-3 if kt["n_block"] else 0.0
+    # Epotential() (SpeedUp:244-281; output() calls it every sampleFreq MD steps, :948) after the window:
+    # two calls, wall and (world 1, blocks) the potential calls' block kernel — VERDICT r05 item 2
+    sim.enable_timing(1, kinds=4)
+    t1 = time.perf_counter()
+    for _ in range(2):
+        epot = sim.Epotential()
+    sim.synchronize()
+    epot_ms = (time.perf_counter() - t1) / 2 * 1e3
+    pk = sim.kernel_times()
+    pot_k_ms = pk["pot_block_ms"] / pk["n_pot_block"] if pk["n_pot_block"] else 0.0
     sim.enable_timing(False)
-    tt = torch.tensor([el, k_avg], dtype=torch.float64, device="cuda")
+    bkeys = list(sim.BREAKDOWN_KEYS)
+    tt = torch.tensor([el, k_avg, epot_ms, pot_k_ms] + [bd[k] for k in bkeys], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    el, k_avg = float(tt[0]), float(tt[1])
+    el, k_avg, epot_ms, pot_k_ms = float(tt[0]), float(tt[1]), float(tt[2]), float(tt[3])
+    breakdown = {k: float(tt[4 + i]) for i, k in enumerate(bkeys)} if bd["calls"] else None
     N = sim.N
     L = sim.const("L")
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
@@ -1037,13 +1099,31 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     force = {"avg_ms": f_avg * 1e3, "launches": nf, "pairs_per_s": pairs / f_avg if f_avg else None,
              "fp64_tflops": W_F_PER_PAIR * pairs / f_avg / 1e12 if f_avg else None,
              "fp64_frac": W_F_PER_PAIR * pairs / f_avg / 1e12 / FP64_PEAK_TFS if f_avg else None,
-             "note": "this rank's forces() incl. all-gather/reduce-scatter; flops = 30 x N(N-1)/2 (SURVEY 8d)"}
+             "note": "this rank's forces() (sort, plan, block kernel, slot reduction, tail pass, reduce-scatter; "
+                     "the position all-gather runs just before it, force_breakdown_ms.allgather); flops = 30 x "
+                     "N(N-1)/2 (SURVEY 8d)"}
+    if breakdown is not None:
+        # the stages of the timed force calls (events between them on the context stream,
+        # max over ranks per stage); stages_sum = sort_boxes + ... + reduce_scatter, against force.avg_ms
+        st = sum(breakdown[k] for k in bkeys[1:7])
+        breakdown["stages_sum"] = st
+        breakdown["stages_sum_vs_force_call"] = st / (f_avg * 1e3) if f_avg else None
+        force["breakdown_note"] = ("force_breakdown_ms: allgather = the ncclAllGather before each timed call; "
+                                   "sort_boxes (Hilbert sort, tile/sub-tile boxes; the first sharded call's balance "
+                                   "census), plan, block_kernel, slot_reduce, tail_pass (ncclAllReduce of the tail "
+                                   "sums, k_tail_max, k_tail_fix), reduce_scatter: consecutive intervals of forces()")
+    epotential = {"Epot": epot, "wall_ms": epot_ms, "block_kernel_ms": pot_k_ms or None,
+                  "vs_force_call": epot_ms / (f_avg * 1e3) if f_avg else None,
+                  "mode": ("the force call's plan (potential_plan 1): skips, sub-tile groups, error-bounded forms, "
+                           "the enforced tail" if world == 1 and pot_k_ms else
+                           "owner-computes rows, every pair to L/2" if world > 1 else "exact, every pair to L/2")}
     return {"workload": desc + ", one system sharded over all ranks (RCCL position all-gather; "
                            "Newton-3 block-pair forces reduce-scattered)",
             "N": N, "n_gpus": world, "comm_size": comm_size, "md_steps": steps, "ms_per_md_step": el / steps * 1e3,
             "value": N * unit_steps * steps / el,
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
-            "scaling": "strong", "init_s": t_init, "force": force,
+            "scaling": "strong", "init_s": t_init, "force": force, "force_breakdown_ms": breakdown,
+            "epotential": epotential,
             "roofline": large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance) if census and f_avg else None,
             "parity": parity if check else {"note": "world 1: this line is the reference the sharded runs are checked against"},
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail, "bound_met": bound_met,

@@ -150,6 +150,9 @@ int         mdqt_potentials_raw(int N, double L, double lDeb, const double* R, s
  * part of the reference's seam: the benchmark's roofline bookkeeping (VALU per evaluated pair). */
 int         mdqt_force_census(mdqt_ctx* c, double* out, int n);
 int         mdqt_epotential(mdqt_ctx* c, double* Epot);      /* Epotential(), SpeedUp:244-281   */
+/* the per-ion pair-potential row sums U_i that Epotential() adds up (Epot = sum U_i / 2N), by ion index,
+ * world 1 — the same device path as mdqt_epotential (tests of its error-bounded block forms) */
+int         mdqt_potential_rows(mdqt_ctx* c, double* U, int n);
 /* observables of output(), SpeedUp:917-1032: out7 = t, EkinX, EkinY, EkinZ, Epot,
  * Etot-Epot0, <vx>; Pvel [3][2001] (may be NULL); pops [N][3] = S,P,D (may be NULL). */
 int         mdqt_observables(mdqt_ctx* c, double out7[7], double* Pvel, double* pops);
@@ -209,7 +212,10 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     halves' rows in one extra slot (C2 on 256 CUs: 4 of 1,596; "force_tile_split_pairs"
  *                     reports the count, "device_cus" the device's compute units); 0 = whole tile pairs
  *                     only.  Forces agree to rounding (another summation order on the split tiles); the
- *                     options overlap / fused_step take the plain table
+ *                     options overlap / fused_step take the plain table.  The table follows the device's
+ *                     CU count, so F's last bits (and trajectories) can differ between devices with
+ *                     different counts: "force_split_cus" = n cuts it for n CUs on any device (0 default:
+ *                     the device's), or force_tile_split 0 for results independent of the device
  *   "force_tail_exp":block pairs in spatial order: tile pairs whose boxes are >= r_t apart are
  *                     skipped with every ion's force kept within eps = 10^-k of the exact sum to
  *                     L/2 (g(r) = one pair's |F| at distance r, SpeedUp:224); k = 12 default, 0 =
@@ -316,6 +322,15 @@ int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, 
  * timed force call (its dispatch timestamps: the plan, the slot reduction, the tail pass and the
  * collectives excluded): out[6] = force_ms, n_force, substep_ms, n_substep, block_ms, n_block */
 int         mdqt_kernel_times(mdqt_ctx* c, double* out, int n);
+/* with n >= 8, out[6..7] = the block kernel of the timed potential calls (Epotential on the Newton-3
+ * blocks; timing kinds bit 2): ms, calls */
+/* the force-call breakdown (timing kinds bit 3 with bit 0; block scheme, N > 65,536): since the last call,
+ * the average ms per timed force call of out[0] the position all-gather just before it (0 at world 1),
+ * [1] the spatial sort and boxes, [2] the plan, [3] the block kernel, [4] the slot reduction, [5] the tail
+ * pass (all-reduce of the per-sub-tile sums, list, exact fix), [6] the reduce-scatter, [7] forces() from
+ * start to end (= [1] + ... + [6]); out[8] = the timed calls.  Events between the stages on the context
+ * stream; resets.  Replaces no reference function (measurement) */
+int         mdqt_force_breakdown(mdqt_ctx* c, double* out, int n);
 
 #ifdef __cplusplus
 }

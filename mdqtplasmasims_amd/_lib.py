@@ -144,6 +144,8 @@ SIGNATURES = [
     ("mdqt_force_census", C.c_int, [C.c_void_p, _dp, C.c_int]),
     ("mdqt_kernel_time_totals", C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int), _dp, C.POINTER(C.c_int)]),
     ("mdqt_kernel_times", C.c_int, [C.c_void_p, _dp, C.c_int]),
+    ("mdqt_force_breakdown", C.c_int, [C.c_void_p, _dp, C.c_int]),
+    ("mdqt_potential_rows", C.c_int, [C.c_void_p, _dp, C.c_int]),
     ("mdqt_force_block_work", C.c_int, [C.c_void_p, _dp, C.c_int, C.POINTER(C.c_int)]),
     ("mdqt_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_enable_timing_kinds", C.c_int, [C.c_void_p, C.c_int, C.c_int]),

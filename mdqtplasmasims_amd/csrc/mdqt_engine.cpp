@@ -90,6 +90,8 @@ struct mdqt_ctx {
            *dTp = nullptr, *dScr = nullptr, *dKde = nullptr, *dUrow = nullptr;
     double* dUpart = nullptr;      // potential-row partials of its own (small systems, world 1)
     int n3_potential = 1;          // option "potential_n3": 1 = Newton-3 tiles where the forces use them
+    int pot_plan = 1;              // option "potential_plan": 1 = Epotential on the blocks takes the force call's
+                                   // plan (skips, sub-tile groups, error-bounded forms); 0 = every pair to L/2 exactly
     size_t capUpart = 0;
     double* dPack = nullptr;       // output()'s per-ion columns [4][S] (world 1)
     int kdeChunks = 0;
@@ -198,6 +200,7 @@ struct mdqt_ctx {
     int nsplit = 0;                // tile pairs the split table runs in parts (halves / quarters)
     int nsplit_wg = 0;             // workgroups of the split table
     int split_opt = 1;             // option force_tile_split: 0 off, 1 halves, 2 quarters (+ diagonal halves)
+    int split_cus = 0;             // option force_split_cus: the CU count the split table is cut for (0: the device's)
     // rng_mode 0: the reference's drand48 stream, consumed in ion order on the device
     unsigned long long* dX48 = nullptr;   // [1] stream state + [48] jA + [48] jC
     int* dFlags = nullptr;         // [0] set by the substep kernels when a position leaves [-L/8, 9L/8]
@@ -226,8 +229,16 @@ struct mdqt_ctx {
     unsigned tperiod = 1, tcount[2] = {0, 0};   // bracket launches k = toffset mod tperiod of each kind
     unsigned toffset = 0;                        // tperiod / 2 unless mdqt_enable_timing_at
                                                 // (mid-period: not the first launch after a sync)
-    std::vector<hipEvent_t> evpool[3];          // 2: the Newton-3 block kernel's own timestamps (a timed force call)
-    int evused[3] = {0, 0, 0};
+    std::vector<hipEvent_t> evpool[4];          // 2: the Newton-3 block kernel's own timestamps (a timed force call)
+    int evused[4] = {0, 0, 0, 0};               // 3: the block kernel of the potential calls (Epotential on the blocks)
+    // force-call breakdown (timing kind bit 3): per timed block-scheme force call the
+    // events between its stages on the context stream — the preceding position all-gather (ag), then
+    // m[0] start | sort + boxes | m[1] | plan | m[2] | block kernel | m[3] | slot reduction | m[4] |
+    // tail pass (all-reduce, list, exact fix) | m[5] | reduce-scatter | m[6]
+    struct BdCall { hipEvent_t ag0 = nullptr, ag1 = nullptr; hipEvent_t m[7] = {}; };
+    std::vector<BdCall> bdcalls;
+    std::vector<hipEvent_t> bdfree;
+    hipEvent_t bd_ag[2] = {nullptr, nullptr};   // the all-gather just before the next timed force call
 };
 
 static int settle_forces(mdqt_ctx* s);
@@ -243,7 +254,7 @@ static int tail_reset(mdqt_ctx* s, bool keep_scale = false) {
     if (!keep_scale) s->tail_scale = 1.;
     s->tail_seen = 0;
     s->tail_pending = false;
-    if (s->dTailSt) HIPCHK(hipMemsetAsync(s->dTailSt, 0, 8 * sizeof(unsigned long long), s->stream));
+    if (s->dTailSt) HIPCHK(hipMemsetAsync(s->dTailSt, 0, 16 * sizeof(unsigned long long), s->stream));
     return 0;
 }
 
@@ -698,8 +709,11 @@ static void choose_segments(mdqt_ctx* s) {
 static int split_slots(const mdqt_ctx* s) { return s->nsplit > 0 ? (s->split_opt == 2 ? 4 : 1) : 0; }
 static int tile_split_count(const mdqt_ctx* s, int nt) {
     if (!s->split_opt || nt < 2) return 0;
-    int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->dev) != hipSuccess || ncu <= 0) return 0;
+    // the table (hence the summation order of the split tiles' forces, F's last bits) follows the CU count:
+    // force_split_cus fixes it, so that devices with different counts give the same bits
+    int ncu = s->split_cus;
+    if (ncu <= 0 && (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->dev) != hipSuccess || ncu <= 0))
+        return 0;
     const long w0 = (long)nt * (nt + 1) / 2;
     if (w0 <= ncu || w0 > 8L * ncu) return 0;    // one round (nothing to balance) / many (dispatched as CUs free up)
     const int k = (int)(w0 % ncu) - nt;          // whole tile pairs in the last round
@@ -749,7 +763,10 @@ static int ensure_aux(mdqt_ctx* s) {
             HIPCHK(hipMalloc(&s->dTail, (size_t)4 * Tc * sizeof(double)));
             HIPCHK(hipMemset(s->dTail, 0, (size_t)4 * Tc * sizeof(double)));
             HIPCHK(hipMalloc(&s->dTailList, (size_t)Tc * sizeof(int)));
-            if (!s->dTailSt) HIPCHK(hipMalloc(&s->dTailSt, 8 * sizeof(unsigned long long)));
+            if (!s->dTailSt) {                       // [0, 8) the force calls', [8, 16) the potential calls'
+                HIPCHK(hipMalloc(&s->dTailSt, 16 * sizeof(unsigned long long)));
+                HIPCHK(hipMemset(s->dTailSt, 0, 16 * sizeof(unsigned long long)));
+            }
             s->capSortN = Nc;
             if (tail_reset(s)) return -1;                // a new size: nothing measured yet
         }
@@ -959,6 +976,13 @@ extern "C" void mdqt_destroy(mdqt_ctx* s) {
     if (s->comm) (void)ncclCommDestroy(s->comm);
     for (auto& pool : s->evpool)
         for (hipEvent_t ev : pool) (void)hipEventDestroy(ev);
+    for (auto& c : s->bdcalls) {
+        for (hipEvent_t ev : c.m) if (ev) (void)hipEventDestroy(ev);
+        if (c.ag0) (void)hipEventDestroy(c.ag0);
+        if (c.ag1) (void)hipEventDestroy(c.ag1);
+    }
+    for (hipEvent_t ev : s->bdfree) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : s->bd_ag) if (ev) (void)hipEventDestroy(ev);
     if (s->own) (void)hipStreamDestroy(s->own);
     delete s;
 }
@@ -986,6 +1010,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "force_ax1")) return s->ax1_mode;
     if (!strcmp(n, "force_reduce_mask")) return s->tmask_mode;
     if (!strcmp(n, "force_tile_split")) return s->split_opt;
+    if (!strcmp(n, "force_split_cus")) return s->split_cus;
     if (!strcmp(n, "force_tile_split_pairs")) return s->nsplit;
     if (!strcmp(n, "device_cus")) {                    // compute units of the context's device
         int ncu = 0;
@@ -1063,6 +1088,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "fused_step")) return s->fused_opt;
     if (!strcmp(n, "qt_im01")) return s->qc.im01;
     if (!strcmp(n, "potential_n3")) return s->n3_potential;
+    if (!strcmp(n, "potential_plan")) return s->pot_plan;
     if (!strcmp(n, "md_step_fused")) return s->last_fused;     // 1: the last MD step was one k_md_step launch
     if (!strcmp(n, "qt_kernel")) return s->last_qt_kernel;     // instance of the last substep launch (QTKernel)
     if (!strcmp(n, "qt_kernel_nseg")) return s->last_qt_nseg;  // force partials its prologue summed
@@ -1514,8 +1540,10 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
             s->capPlan = need;
         }
         a.plan = s->dPlan;
-        a.tmw = s->tmask_mode ? tmw : 0;
-        a.tmask = s->tmask_mode ? (unsigned long long*)(s->dPlan + nplan) : nullptr;
+        // (no masks for a rank without blocks: nothing would clear or fill them — ADVICE r05)
+        const bool masks = s->tmask_mode && a.Phi > a.Plo;
+        a.tmw = masks ? tmw : 0;
+        a.tmask = masks ? (unsigned long long*)(s->dPlan + nplan) : nullptr;
     }
     return 0;
 }
@@ -1593,6 +1621,19 @@ static int take_events(mdqt_ctx* s, int k, hipEvent_t* e0, hipEvent_t* e1) {
     *e0 = pool[s->evused[k]++];
     *e1 = pool[s->evused[k]++];
     return 0;
+}
+
+// force-call breakdown (timing kind bit 3): one event recorded now on the context stream, from the free list
+static hipEvent_t bd_event(mdqt_ctx* s) {
+    hipEvent_t e = nullptr;
+    if (!s->bdfree.empty()) { e = s->bdfree.back(); s->bdfree.pop_back(); }
+    else if (hipEventCreateWithFlags(&e, kTimingEventFlags) != hipSuccess) return nullptr;
+    if (hipEventRecord(e, s->stream) != hipSuccess) { s->bdfree.push_back(e); return nullptr; }
+    return e;
+}
+// will the next force call be timed (its tcount not yet advanced)?
+static bool force_timed_next(const mdqt_ctx* s) {
+    return s->timing && (s->tkinds & 1u) && (s->tkinds & 8u) && (s->tcount[0] % s->tperiod == s->toffset);
 }
 
 // the block kernel's work by tile-pair class for the current positions (k_n3b_census): out[0, 12)
@@ -1730,9 +1771,17 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         s->f_pending = !one_slot;  // slots summed by the next substep launch (or settle_forces)
         s->pend_nseg = s->nslots + (split ? split_slots(s) : 0);
     } else if (s->use_n3b) {
+        const bool bd = tm && (s->tkinds & 8u);    // the breakdown of this call
+        mdqt_ctx::BdCall bc;
+        if (bd) {
+            bc.ag0 = s->bd_ag[0]; bc.ag1 = s->bd_ag[1];
+            bc.m[0] = bd_event(s);
+        }
+        s->bd_ag[0] = s->bd_ag[1] = nullptr;
         if (n3b_balance(s)) return -1;
         N3BArgs a;
         if (n3b_args(s, a)) return -1;
+        if (bd) bc.m[1] = bd_event(s);
         const int W = s->p.world_size;
         if (a.tailb) {
             HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)4 * a.T * sizeof(double), s->stream));
@@ -1740,7 +1789,14 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
         }
         hipEvent_t e0 = nullptr, e1 = nullptr;     // timed call: the block kernel alone as well
         if (tm && take_events(s, 2, &e0, &e1)) return -1;
-        HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream, e0, e1));
+        hipEvent_t pm[3] = {nullptr, nullptr, nullptr};   // after the plan, the kernel, the reduction
+        if (bd)
+            for (auto& e : pm) {
+                if (!s->bdfree.empty()) { e = s->bdfree.back(); s->bdfree.pop_back(); }
+                else HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
+            }
+        HIPCHK(launch_forces_n3b(a, s->force_variant, W == 1 ? s->dF : s->dFr, s->stream, e0, e1, bd ? pm : nullptr));
+        if (bd) { bc.m[2] = pm[0]; bc.m[3] = pm[1]; bc.m[4] = pm[2]; }
         if (a.tailb) {                  // measured tail: complete the per-tile sums, then enforce eps
             if (W > 1 && s->comm) {
                 NCCLCHK(ncclAllReduce(a.tailb, a.tailb, (size_t)4 * a.T, ncclDouble, ncclSum, s->comm, s->stream));
@@ -1752,6 +1808,7 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
                 s->tail_args = a;
             }
         }
+        if (bd) bc.m[5] = bd_event(s);
         if (W > 1) {
             if (s->comm) {
                 NCCLCHK(ncclReduceScatter(s->dFr, s->dF, (size_t)3 * s->S, ncclDouble, ncclSum, s->comm, s->stream));
@@ -1760,6 +1817,10 @@ extern "C" int mdqt_forces(mdqt_ctx* s) {                 // forces(), SpeedUp:1
             } else {
                 return fail("mdqt_forces: sharded Newton-3 blocks need a communicator (mdqt_comm_init)");
             }
+        }
+        if (bd) {
+            bc.m[6] = bd_event(s);
+            s->bdcalls.push_back(bc);
         }
         s->f_pending = false;
     } else if (s->nseg == 1) {
@@ -2129,11 +2190,32 @@ static int potential_rows(mdqt_ctx* s, double* urow_dev) {
     }
     // world 1 with Newton-3 blocks (N > 65,536): the block kernel's POT mode, per-ion row sums by
     // k_n3b_reduce (the block slots are free between force calls: the force path reduces at once)
+    // Round 6 (option potential_plan): on the force call's plan — the same skip radius,
+    // sub-tile groups and error-bounded forms (pair_u_cut, the f32 ultra-far form), the same measured and
+    // enforced tail (tiles whose sub-tile force sums exceed eps get their U_i recomputed exactly).  Since
+    // u(r) < lDeb g(r) and each form's relative error on u is at most its error on the force, every U_i is
+    // within lDeb x (the force call's per-ion bound: tail eps + the tiers') of its sum to L/2, and Epot =
+    // sum U_i / 2N within half that (C4, N = 1M: ~1e-12 absolute on Epot ~ 5; north_star asks 1e-6
+    // relative).  Tests: tests/test_gpu_large.py test_epotential_on_the_plan.
     if (s->use_n3b && s->p.world_size == 1 && s->local.empty() && s->force_variant <= 1 && s->n3_potential) {
         if (settle_forces(s)) return -1;
         N3BArgs a;
         if (n3b_args(s, a)) return -1;
-        HIPCHK(launch_potential_n3b(a, s->force_variant, urow_dev, s->stream));
+        const bool planned = s->pot_plan && a.plan && s->force_variant == 1 && !a.guard;
+        if (!planned) {
+            a.plan = nullptr; a.tmask = nullptr; a.tmw = 0; a.tailb = nullptr;
+            a.Rskip = a.Rcut;                       // (the no-plan kernel skips only beyond L/2 for potentials)
+        } else if (a.tailb) {
+            HIPCHK(hipMemsetAsync(a.tailb, 0, (size_t)4 * a.T * sizeof(double), s->stream));
+            HIPCHK(hipMemsetAsync(s->dTailSt + 8 + 3, 0, sizeof(unsigned long long), s->stream));
+        }
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (s->timing && (s->tkinds & 4u) && take_events(s, 3, &e0, &e1)) return -1;
+        HIPCHK(launch_potential_n3b(a, s->force_variant, urow_dev, s->stream, e0, e1));
+        if (a.tailb) {                              // the enforcement (its own counters: dTailSt[8, 16))
+            HIPCHK(launch_tail_max(a.tailb, a.T, pow(10., -s->tail_exp), s->dTailSt + 8, s->dTailList, s->stream));
+            HIPCHK(launch_tail_fix(a, s->dTailSt + 8, s->dTailList, urow_dev, s->stream, true));
+        }
         return 0;
     }
     double* buf = s->dFpart;
@@ -2176,6 +2258,19 @@ extern "C" int mdqt_partial_observables(mdqt_ctx* s, double vxAvg, double out5[5
     out5[1] = s->nloc ? h[16] : 0.; out5[2] = s->nloc ? h[17] : 0.; out5[3] = s->nloc ? h[18] : 0.;
     out5[4] = s->nloc ? h[19] : 0.;
     if (Pvel) memcpy(Pvel, h + 64, 3 * NBINS * sizeof(double));
+    return 0;
+}
+
+// the per-ion pair-potential row sums U_i that Epotential() adds up (world 1; by ion index): the same path as
+// Epotential() (Newton-3 tiles or blocks — on the force call's plan unless potential_plan 0 — or rows)
+extern "C" int mdqt_potential_rows(mdqt_ctx* s, double* U, int n) {
+    if (!s || !U) return fail("mdqt_potential_rows: NULL argument");
+    if (s->p.world_size != 1 || !s->local.empty()) return fail("mdqt_potential_rows: world 1 only");
+    if (n < s->N) return fail("mdqt_potential_rows: need %d doubles", s->N);
+    HIPCHK(hipSetDevice(s->dev));
+    if (potential_rows(s, s->dUrow)) return -1;
+    HIPCHK(hipMemcpyAsync(U, s->dUrow, (size_t)s->N * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
     return 0;
 }
 
@@ -2877,6 +2972,11 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         s->n3_potential = value;
         return 0;
     }
+    if (!strcmp(name, "potential_plan")) {             // Epotential on the blocks: the force call's plan (1) or exact (0)
+        if (value < 0 || value > 1) return fail("potential_plan must be 0 (every pair to L/2) or 1 (the plan)");
+        s->pot_plan = value;
+        return 0;
+    }
     if (!strcmp(name, "qt_im01")) {                    // 0: the general FAST lane instance (tests)
         if (value < 0 || value > 1) return fail("qt_im01 must be 0 or 1");
         if (value) {                                   // only where the table allows it
@@ -2948,6 +3048,12 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (value < 0 || value > 2) return fail("force_tile_split must be 0 (off), 1 (halves) or 2 (quarters)");
         if (settle_forces(s)) return -1;
         s->split_opt = value;
+        return ensure_aux(s);
+    }
+    if (!strcmp(name, "force_split_cus")) {            // the CU count the split table is cut for (0: the device's)
+        if (value < 0 || value > 65536) return fail("force_split_cus must be 0 (the device's CU count) or a CU count");
+        if (settle_forces(s)) return -1;
+        s->split_cus = value;
         return ensure_aux(s);
     }
     if (!strcmp(name, "force_reduce_mask")) {          // Newton-3 blocks: the reduction reads only written j-slots
@@ -3022,7 +3128,13 @@ extern "C" int mdqt_enable_timing_at(mdqt_ctx* s, int on, int kinds, int offset)
     s->toffset = on > 0 ? (unsigned)offset : 0u;
     s->tkinds = (unsigned)kinds;
     s->tcount[0] = s->tcount[1] = 0;
-    s->evused[0] = s->evused[1] = s->evused[2] = 0;
+    s->evused[0] = s->evused[1] = s->evused[2] = s->evused[3] = 0;
+    for (auto& c : s->bdcalls) {                    // (the breakdown restarts with the timing)
+        for (hipEvent_t e : c.m) if (e) s->bdfree.push_back(e);
+        if (c.ag0) s->bdfree.push_back(c.ag0);
+        if (c.ag1) s->bdfree.push_back(c.ag1);
+    }
+    s->bdcalls.clear();
     return 0;
 }
 extern "C" int mdqt_enable_timing_kinds(mdqt_ctx* s, int on, int kinds) {
@@ -3035,7 +3147,8 @@ extern "C" int mdqt_kernel_times(mdqt_ctx* s, double* out, int n) {
     if (n < 6) return fail("mdqt_kernel_times: need 6 doubles");
     HIPCHK(hipSetDevice(s->dev));
     HIPCHK(hipStreamSynchronize(s->stream));
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
+        if (2 * k + 1 >= n) { s->evused[k] = 0; continue; }
         double tot = 0.;
         for (int i = 0; i + 1 < s->evused[k]; i += 2) {
             float ms = 0.f;
@@ -3128,7 +3241,42 @@ extern "C" int mdqt_allgather_positions(mdqt_ctx* s) {
     }
     if (!s->comm) return fail("mdqt_allgather_positions: no communicator (mdqt_comm_init)");
     HIPCHK(hipSetDevice(s->dev));
+    const bool bd = force_timed_next(s) && s->use_n3b;   // (the breakdown's first stage)
+    for (hipEvent_t& e : s->bd_ag)
+        if (e) { s->bdfree.push_back(e); e = nullptr; }
+    if (bd) s->bd_ag[0] = bd_event(s);
     NCCLCHK(ncclAllGather(s->dR + (size_t)s->p.rank * cnt, s->dR, cnt, ncclDouble, s->comm, s->stream));
+    if (bd) s->bd_ag[1] = bd_event(s);
+    return 0;
+}
+
+// the force-call breakdown (timing kind bit 3) since the last call: average ms per timed block-scheme force
+// call of out[0] the preceding position all-gather (0 at world 1), [1] sort and boxes (with the first sharded
+// call's balance census), [2] plan, [3] block kernel (launch to end, incl. its dispatch gap), [4] slot reduction,
+// [5] tail pass (all-reduce of the per-sub-tile sums, list, exact fix), [6] reduce-scatter, [7] forces() start to
+// end (= [1] + ... + [6]), out[8] the calls; resets
+extern "C" int mdqt_force_breakdown(mdqt_ctx* s, double* out, int n) {
+    if (!s || !out) return fail("mdqt_force_breakdown: NULL argument");
+    if (n < 9) return fail("mdqt_force_breakdown: need 9 doubles");
+    HIPCHK(hipSetDevice(s->dev));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    double acc[8] = {0., 0., 0., 0., 0., 0., 0., 0.};
+    auto ms = [](hipEvent_t a, hipEvent_t b) -> double {
+        float t = 0.f;
+        return (a && b && hipEventElapsedTime(&t, a, b) == hipSuccess) ? (double)t : 0.;
+    };
+    for (auto& c : s->bdcalls) {
+        acc[0] += ms(c.ag0, c.ag1);
+        for (int k = 0; k < 6; ++k) acc[1 + k] += ms(c.m[k], c.m[k + 1]);
+        acc[7] += ms(c.m[0], c.m[6]);
+        for (hipEvent_t e : c.m) if (e) s->bdfree.push_back(e);
+        if (c.ag0) s->bdfree.push_back(c.ag0);
+        if (c.ag1) s->bdfree.push_back(c.ag1);
+    }
+    const double nc = (double)s->bdcalls.size();
+    for (int k = 0; k < 8; ++k) out[k] = nc > 0 ? acc[k] / nc : 0.;
+    out[8] = nc;
+    s->bdcalls.clear();
     return 0;
 }
 

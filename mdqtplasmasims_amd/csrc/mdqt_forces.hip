@@ -322,6 +322,9 @@ __device__ __forceinline__ float row_rol2f(float v) {   // lane 16 a + m <- lane
 #define MDQT_UF32_PK 1
 #endif
 
+// POT (Epotential on the plan, round 6): u = 2^t ri in the same f32 operations, one component (i side in
+// fx, j side in ax); its relative error is within the force form's (one factor ri instead of three)
+template <bool POT = false>
 __device__ __forceinline__ void n3b_group_uf32(int b0, float xi, float yi, float zi, const float (*pj32)[128],
                                                double* ax, double* ay, double* az, double& fx, double& fy, double& fz,
                                                float cf, float invlf, float rc2f) {
@@ -331,7 +334,29 @@ __device__ __forceinline__ void n3b_group_uf32(int b0, float xi, float yi, float
     typedef __attribute__((address_space(3))) const float* lds_f32p;
     lds_f32p px0 = (lds_f32p)&pj32[0][b0], py0 = (lds_f32p)&pj32[1][b0], pz0 = (lds_f32p)&pj32[2][b0];
     asm volatile("" : "+v"(px0), "+v"(py0), "+v"(pz0));
-    if constexpr (MDQT_UF32_PK) {
+    if constexpr (POT) {
+        f32x2 iu = {0.f, 0.f};
+        float ju = 0.f;
+#pragma unroll
+        for (int t = 0; t < 16; t += 2) {
+            const f32x2 dx = f32x2{xi, xi} - f32x2{px0[t], px0[t + 1]};
+            const f32x2 dy = f32x2{yi, yi} - f32x2{py0[t], py0[t + 1]};
+            const f32x2 dz = f32x2{zi, zi} - f32x2{pz0[t], pz0[t + 1]};
+            const f32x2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
+            const f32x2 ri = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
+            const f32x2 tt = (r2 * ri) * cf;
+            const f32x2 e = {__builtin_amdgcn_exp2f(r2.x < rc2f ? tt.x : -INFINITY),
+                             __builtin_amdgcn_exp2f(r2.y < rc2f ? tt.y : -INFINITY)};
+            const f32x2 u = e * ri;
+            const float uu = row_rol1f(u.x) + u.y;   // (the j side's rotation, as the forces')
+            if (t == 0) { iu = u; ju = uu; }
+            else { iu += u; ju = row_rol2f(ju) + uu; }
+            asm volatile("" : "+v"(iu));
+        }
+        __hip_atomic_fetch_add(ax + b0 + 15, (double)ju, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        fx += (double)(iu.x + iu.y);
+        (void)ay; (void)az; (void)fy; (void)fz; (void)invlf;
+    } else if constexpr (MDQT_UF32_PK) {
         f32x2 ix = {0.f, 0.f}, iy = {0.f, 0.f}, iz = {0.f, 0.f};
         float jx = 0.f, jy = 0.f, jz = 0.f;
 #pragma unroll
@@ -394,6 +419,7 @@ __device__ __forceinline__ void n3b_group_uf32(int b0, float xi, float yi, float
 
 // the f32 ultra-far form over the groups of `groups` (off the diagonal); xi, yi, zi: the lane's ion
 // relative to the J tile's raw box centre, in f32
+template <bool POT = false>
 __device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, float xi, float yi, float zi,
                                               const float (*pj32)[128], double* ax, double* ay, double* az,
                                               double& fx, double& fy, double& fz, float cf, float invlf, float rc2f) {
@@ -401,7 +427,7 @@ __device__ __forceinline__ void n3b_pair_uf32(unsigned groups, int l, float xi, 
     const int a = l >> 4, m = l & 15;
     for (int d = 0; d < 4; ++d) {
         if (!((groups >> d) & 1u)) continue;        // wave-uniform
-        n3b_group_uf32(32 * ((a + d) & 3) + m, xi, yi, zi, pj32, ax, ay, az, fx, fy, fz, cf, invlf, rc2f);
+        n3b_group_uf32<POT>(32 * ((a + d) & 3) + m, xi, yi, zi, pj32, ax, ay, az, fx, fy, fz, cf, invlf, rc2f);
     }
 }
 
@@ -634,7 +660,7 @@ void k_pairs_n3b(N3BArgs a) {
     // 8-byte word per tile pair, loaded by lanes 0..15); without a plan (potentials, unsorted order)
     // the staging lanes classify the tile pairs themselves and every group runs in the exact form.
     constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
-    constexpr bool FARF = VARIANT == 1 && !POT && !GUARD && CUT;   // the error-bounded pair forms
+    constexpr bool FARF = VARIANT == 1 && !GUARD && CUT;   // the error-bounded pair forms (potentials: on a plan)
     const N3BRadii rad = n3b_radii<VARIANT, POT>(a);
     // the f32 form's constants as wave-uniform SGPR values (in VGPRs they were spilled and reloaded
     // inside the pair loop at the kernel's 64-VGPR budget)
@@ -652,7 +678,7 @@ void k_pairs_n3b(N3BArgs a) {
     const size_t FS = a.Npad;
 #endif
     bool fi_first = true;
-    const uint2* plan = POT ? nullptr : a.plan;
+    const uint2* plan = a.plan;                     // (potentials: the plan of launch_potential_n3b, or none)
     // every J step: the staging wave (the last; not one of the combining waves 0..2) loads J, one
     // barrier, the pair work, one barrier, then waves 0..2 combine the 16 j accumulators of one
     // component each into the j-slot and zero them for the next step — while the staging wave
@@ -776,7 +802,9 @@ void k_pairs_n3b(N3BArgs a) {
                         }
                     }
                 }
+#if !defined(MDQT_EXPT_NOBAR)                       // (diagnostic build: no J-step barriers, wrong results)
                 __syncthreads();
+#endif
             }
             const double (*pj)[128] = sh.pj[buf];
             const double* mj = sh.mjs[J == T - 1];
@@ -823,8 +851,9 @@ void k_pairs_n3b(N3BArgs a) {
                             if (g0) n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(false, g0, l, sx, sy, sz, mi, pj, mj, ax,
                                                                                     ay, az, tx, ty, tz, c, nsh);
 #if !defined(MDQT_EXPT_UFAR_SKIP)                   // last: nothing after it keeps sx, nsh live (diagnostic build: skip it, wrong results)
-                            if (g5) n3b_pair_uf32(g5, l, (float)(sx - pj[0][0]), (float)(sy - pj[1][0]), (float)(sz - pj[2][0]),
-                                                  sh.pj32, ax, ay, az, tx, ty, tz, cf32, invl32, rc2f);
+                            if (g5) n3b_pair_uf32<POT>(g5, l, (float)(sx - pj[0][0]), (float)(sy - pj[1][0]),
+                                                       (float)(sz - pj[2][0]), sh.pj32, ax, ay, az, tx, ty, tz, cf32,
+                                                       invl32, rc2f);
 #endif
                         }
                     } else {
@@ -892,7 +921,9 @@ void k_pairs_n3b(N3BArgs a) {
                 bx += tx; by += ty; bz += tz;
             }
             if (kDbuf && plan && q == kStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA retired
+#if !defined(MDQT_EXPT_NOBAR)
             __syncthreads();
+#endif
             if (kDbuf && plan) buf ^= kN3BStageBufs - 1;
             if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db
                 const int l = lane_opaque(l0);
@@ -975,6 +1006,9 @@ __global__ __launch_bounds__(256) void k_tail_max(const double* __restrict__ tai
 // ballot; the waves' sums combined in wave order: deterministic.  Each ion belongs to one tile, so
 // `out` has one writer per ion.  With an empty list (the normal case) every workgroup reads st[3]
 // and returns.
+// POT (Epotential on the plan): the listed tiles' U_i = sum of u over every pair inside L/2 (pair_u<1>),
+// component 0 of `out` (the per-ion potential rows)
+template <bool POT = false>
 __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long long* __restrict__ st,
                                                   const int* __restrict__ list, double* __restrict__ out) {
     __shared__ double part[4][3][64];
@@ -1021,8 +1055,12 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
                     };
                     double dx = xi - lane_t(xl), dy = yi - lane_t(yl), dz = zi - lane_t(zl);
                     mic_r(dx, dy, dz, c);
-                    const double ft = pair_ft<1>(dx, dy, dz, c);   // 0 beyond L/2 and for i = j
-                    px = fma(dx, ft, px); py = fma(dy, ft, py); pz = fma(dz, ft, pz);
+                    if constexpr (POT) {
+                        px += pair_u<1>(dx, dy, dz, c);            // 0 beyond L/2 and for i = j
+                    } else {
+                        const double ft = pair_ft<1>(dx, dy, dz, c);   // 0 beyond L/2 and for i = j
+                        px = fma(dx, ft, px); py = fma(dy, ft, py); pz = fma(dz, ft, pz);
+                    }
                 }
                 nadd(fx, ex, px); nadd(fy, ey, py); nadd(fz, ez, pz);
             }
@@ -1034,7 +1072,7 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
             const int w = ion / a.S;
             double* o = out + (size_t)w * 3 * a.S + (ion - w * a.S);
 #pragma unroll
-            for (int c3 = 0; c3 < 3; ++c3)
+            for (int c3 = 0; c3 < (POT ? 1 : 3); ++c3)
                 o[(size_t)c3 * a.S] = ((part[0][c3][l] + part[1][c3][l]) + part[2][c3][l]) + part[3][c3][l];
         }
         __syncthreads();
@@ -1372,8 +1410,8 @@ hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    const int nblk = (a.Phi - a.Plo) * a.R;
+// the plan (k_n3b_plan) of a force or potential call in spatial order, its per-J-tile masks zeroed first
+static hipError_t launch_n3b_plan(const N3BArgs& a, int variant, hipStream_t s) {
     const int nplan = (a.Phi - a.Plo) * a.nd;
     if (a.plan && nplan > 0) {
         if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // spatial order only
@@ -1389,14 +1427,27 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     } else if (a.tailb) {
         return hipErrorInvalidValue;                // the tail sums come from the plan
     }
+    return hipGetLastError();
+}
+
+// the AXP instance where tile pairs whose image varies on one axis can be evaluated: their pairs are >=
+// L/2 - (the two tiles' extents) apart on that axis, so only when the skip radius reaches within two tile
+// widths (L (64/N)^(1/3)) of L/2 (C3, C5: r_s = L/2; not N = 1M, r_s = 61 < 80.6 - 12.9).  A function of
+// the call's parameters alone: every rank of a sharded run, and every call of one configuration, takes
+// the same kernel.
+static bool n3b_axp(const N3BArgs& a) {
+    return a.ax1 && a.use_sort != 0 && a.Rskip > 0.5 * a.L - 2. * a.L * cbrt(64. / a.N);
+}
+
+hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                             hipEvent_t* marks) {
+    const int nblk = (a.Phi - a.Plo) * a.R;
+    const int nplan = (a.Phi - a.Plo) * a.nd;
+    if (hipError_t e = launch_n3b_plan(a, variant, s); e != hipSuccess) return e;
+    if (marks && hipEventRecord(marks[0], s) != hipSuccess) return hipGetLastError();
     if (nblk > 0) {
         if (variant == 1) {
-            // the AXP instance where tile pairs whose image varies on one axis can be evaluated: their
-            // pairs are >= L/2 - (the two tiles' extents) apart on that axis, so only when the skip
-            // radius reaches within two tile widths (L (64/N)^(1/3)) of L/2 (C3, C5: r_s = L/2; not
-            // N = 1M, r_s = 61 < 80.6 - 12.9).  A function of the call's parameters alone: every rank
-            // of a sharded run, and every call of one configuration, takes the same kernel.
-            const bool axp = a.ax1 && a.use_sort != 0 && a.Rskip > 0.5 * a.L - 2. * a.L * cbrt(64. / a.N);
+            const bool axp = n3b_axp(a);
             if (a.guard) launch_timed(k_pairs_n3b<1, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
             else if (axp) launch_timed(k_pairs_n3b<1, false, false, MDQT_N3B_AX1 != 0>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
             else launch_timed(k_pairs_n3b<1, false>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
@@ -1407,7 +1458,13 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     } else if (ev0) {                                   // (no block of this rank: an empty interval)
         if (hipEventRecord(ev0, s) != hipSuccess || hipEventRecord(ev1, s) != hipSuccess) return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, a, out);
+    // a rank without blocks (Phi == Plo, sharded with NB < W) has no plan and so no masks to follow:
+    // the unmasked reduction reads none of its (unwritten) slots and leaves its dense partial 0
+    N3BArgs r = a;
+    if (!(a.plan && nplan > 0)) r.tmask = nullptr;
+    if (marks && hipEventRecord(marks[1], s) != hipSuccess) return hipGetLastError();
+    hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 3), dim3(256), 0, s, r, out);
+    if (marks && hipEventRecord(marks[2], s) != hipSuccess) return hipGetLastError();
 #if defined(MDQT_EXPT_TMASK_DEBUG)
     if (a.plan && a.tmask) {                        // diagnostic build: the masks' bit counts
         (void)hipStreamSynchronize(s);
@@ -1442,9 +1499,10 @@ hipError_t launch_tail_max(const double* tailb, int T, double eps, unsigned long
 }
 
 hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const int* list, double* out,
-                           hipStream_t s) {
+                           hipStream_t s, bool pot) {
     if (a.T <= 0 || !a.Rs || !a.perm || !a.boxes) return hipErrorInvalidValue;   // spatial order only
-    hipLaunchKernelGGL(k_tail_fix, dim3(a.T < 512 ? a.T : 512), dim3(256), 0, s, a, st, list, out);
+    if (pot) hipLaunchKernelGGL(k_tail_fix<true>, dim3(a.T < 512 ? a.T : 512), dim3(256), 0, s, a, st, list, out);
+    else hipLaunchKernelGGL(k_tail_fix<false>, dim3(a.T < 512 ? a.T : 512), dim3(256), 0, s, a, st, list, out);
     return hipGetLastError();
 }
 
@@ -1458,20 +1516,33 @@ hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s) {
+// Epotential()'s pair sums on the blocks.  With a plan (a.plan, the fast variant in spatial order; round
+// 6): the force call's skip radius, sub-tile groups and error-bounded forms (pair_u_cut, the f32
+// ultra-far form), the tail sums in a.tailb for the caller's enforcement; without: every pair to L/2 in
+// the exact form (the staging lanes classify)
+hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0,
+                                hipEvent_t ev1) {
     if (variant < 0 || variant > 1) return hipErrorInvalidValue;
     const int nblk = (a.Phi - a.Plo) * a.R;
+    const int nplan = (a.Phi - a.Plo) * a.nd;
+    const bool planned = a.plan && nplan > 0;
+    if (planned && (variant != 1 || a.guard)) return hipErrorInvalidValue;   // (the far forms are the fast variant's)
+    if (hipError_t e = launch_n3b_plan(a, variant, s); e != hipSuccess) return e;
+    N3BArgs r = a;
+    if (!planned) { r.plan = nullptr; r.tmask = nullptr; }   // (no plan: every j-slot written, every one read)
     if (nblk > 0) {
         if (variant == 1) {
-            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<1, true, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
-            else hipLaunchKernelGGL((k_pairs_n3b<1, false, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            if (a.guard) launch_timed(k_pairs_n3b<1, true, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, r);
+            else if (planned && n3b_axp(a))
+                launch_timed(k_pairs_n3b<1, false, true, MDQT_N3B_AX1 != 0>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, r);
+            else launch_timed(k_pairs_n3b<1, false, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, r);
         } else {
-            if (a.guard) hipLaunchKernelGGL((k_pairs_n3b<0, true, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
-            else hipLaunchKernelGGL((k_pairs_n3b<0, false, true>), dim3(nblk), dim3(BW * 64), 0, s, a);
+            if (a.guard) launch_timed(k_pairs_n3b<0, true, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, r);
+            else launch_timed(k_pairs_n3b<0, false, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, r);
         }
+    } else if (ev0) {
+        if (hipEventRecord(ev0, s) != hipSuccess || hipEventRecord(ev1, s) != hipSuccess) return hipGetLastError();
     }
-    N3BArgs r = a;                                  // (no plan: every j-slot written, every one read)
-    r.tmask = nullptr;
     hipLaunchKernelGGL(k_n3b_reduce, dim3((a.N + 255) / 256, 1), dim3(256), 0, s, r, out);   // component 0
     return hipGetLastError();
 }

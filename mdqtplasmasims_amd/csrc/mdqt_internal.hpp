@@ -468,16 +468,18 @@ struct SortArgs {
 hipError_t launch_spatial_order(const SortArgs& a, hipStream_t s);
 size_t spatial_order_tmp_bytes(int N);
 // ev0/ev1: the block kernel's own dispatch timestamps (timing on; k_pairs_n3b alone, not the plan or
-// the reduction)
+// the reduction); marks (optional, the force-call breakdown): 3 events recorded after the plan, after the
+// block kernel and after the slot reduction
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0 = nullptr,
-                             hipEvent_t ev1 = nullptr);
+                             hipEvent_t ev1 = nullptr, hipEvent_t* marks = nullptr);
 // force_tail_mode 1 (mdqt_forces.hip): the per-sub-tile tail sums [4T] against eps — st[0] running
 // max of the tiles within eps, st[1] of all, st[2] tiles over eps (cumulative), st[3] this call's
 // list length, st[4] measured calls — and the exact recomputation of the listed tiles' forces,
-// written into `out` ([world][3][S], by ion) on the rank that owns the tile (0 on the others)
+// written into `out` ([world][3][S], by ion) on the rank that owns the tile (0 on the others); pot: their
+// potential rows U_i (component 0) instead
 hipError_t launch_tail_max(const double* tailb, int T, double eps, unsigned long long* st, int* list, hipStream_t s);
 hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const int* list, double* out,
-                           hipStream_t s);
+                           hipStream_t s, bool pot = false);
 // census of k_pairs_n3b's work by tile-pair class (mdqt_forces.hip k_n3b_census): out[2 kCensus]
 constexpr int kCensus = 14;
 // tiles per block of the Newton-3 block kernel (= its waves per workgroup): 8 (round 4, A/B vs 16:
@@ -572,8 +574,11 @@ hipError_t launch_forces_n3(const N3Args& a, int variant, hipStream_t s, hipEven
 // Epotential on the Newton-3 tiles (world 1): pair potentials into slot p of a.P, plane stride S
 // ([ntiles][S]: one component, a third of the force slots' memory)
 hipError_t launch_potential_n3(const N3Args& a, int variant, hipStream_t s);
-// Epotential on the Newton-3 blocks (world 1): per-ion row sums of u into out[S]
-hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s);
+// Epotential on the Newton-3 blocks (world 1): per-ion row sums of u into out[S]; with a.plan on the force
+// call's plan (skips, sub-tile groups, error-bounded forms; tail sums into a.tailb), else exact to L/2;
+// ev0/ev1 (optional) time the block kernel
+hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0 = nullptr,
+                                hipEvent_t ev1 = nullptr);
 // partial p of component c at Fpart + p * plane + c * S (plane 0: 3 S, the force layout)
 hipError_t launch_reduce_segments(const double* Fpart, double* F, int nseg, int nrows, int S, int ncomp,
                                   hipStream_t s, size_t plane = 0);

@@ -209,6 +209,38 @@ __device__ __forceinline__ double pair_ft_cut_ufar(double dx, double dy, double 
     return ((ri + c.invlDeb) * e) * (ri * ri);
 }
 
+// The pair potential u = e^(-r/lDeb) / r (SpeedUp:265) in the error-bounded forms of the Newton-3
+// blocks (Epotential() on the plan, round 6): level FAR's rsq and 2^t, the same cutoff, u = 2^t ri.  A
+// term's relative error is at most the force form's err(r) (one factor ri instead of three), and
+// u(r) = g(r) r lDeb / (r + lDeb) < lDeb g(r), so every ion's U_i is within lDeb x (the force tiers'
+// per-ion bound) of its exact-form sum (mdqt_engine.cpp potential_rows)
+template <int FAR>
+__device__ __forceinline__ double pair_u_cut(double dx, double dy, double dz, const PairC& c) {
+    static_assert(FAR >= 1 && FAR <= 4, "the exact form is pair_u");
+    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+    if constexpr (FAR == 1 || FAR == 2) {
+        const double ri = rsq1(r2);
+        const double dr = r2 * ri;
+        if constexpr (FAR == 1)
+            return exp2_neg_cut_tab4(dr * (c.invlDeb * (64. * kNegLog2e)), r2 < c.rc2, c.etab) * ri;
+        return exp2_neg_cut6(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut) * ri;
+    } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const double ri = __builtin_amdgcn_rsq(r2);
+#else
+        const double ri = 1. / sqrt(r2);
+#endif
+        const double dr = r2 * ri;
+        if constexpr (FAR == 3) return exp2_neg_cut5(dr * (c.invlDeb * kNegLog2e), r2 < c.rc2) * ri;
+        const float tf = r2 < c.rc2 ? (float)(dr * (c.invlDeb * kNegLog2e)) : -INFINITY;
+#if defined(__HIP_DEVICE_COMPILE__)
+        return (double)__builtin_amdgcn_exp2f(tf) * ri;
+#else
+        return (double)exp2f(tf) * ri;
+#endif
+    }
+}
+
 template <int VARIANT>
 __device__ __forceinline__ void accum(double& f, double d, double ft) {
     if (VARIANT == 0) f += d * ft;        // the reference's F[i] += dx*ftotal (:225-230)
@@ -264,7 +296,10 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
         mic_v<VARIANT, GUARD>(dx, dy, dz, c);
     }
     if constexpr (POT) {
-        double u = pair_u<VARIANT>(dx, dy, dz, c);
+        // FAR > 0: the error-bounded forms of a Newton-3 block plan (pair_u_cut); 0: the exact form
+        double u;
+        if constexpr (FAR > 0) u = pair_u_cut<FAR>(dx, dy, dz, c);
+        else u = pair_u<VARIANT>(dx, dy, dz, c);
         if (RAGGED) u *= mi * mj[idx];
         u *= m;
         fx += u;
@@ -272,7 +307,7 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
         (void)fy; (void)fz;
         return;
     }
-    static_assert(!FAR || (CUT && !POT), "the far pair form is the fast force variant's");
+    static_assert(!FAR || CUT, "the far pair forms are the fast variant's");
     static_assert(FAR != 1 || MDQT_EXP_TAB, "the mid tier's 2^t is the table's");
     // FAR: 0 exact form, 1 mid, 2 far, 3 very far, 4 ultra far (Newton-3 blocks, error-bounded)
     double ft = FAR == 4 ? pair_ft_cut_ufar(dx, dy, dz, c)

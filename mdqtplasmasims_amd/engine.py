@@ -232,6 +232,14 @@ class Simulation:
 
     epotential = Epotential
 
+    def potential_rows(self):
+        """U_i, the per-ion pair-potential row sums Epotential() adds up (world 1; include/mdqt.h
+        mdqt_potential_rows)"""
+        import numpy as np
+        U = np.zeros(self.N)
+        check(lib().mdqt_potential_rows(self.h, U.ctypes.data_as(C.POINTER(C.c_double)), self.N), "potential_rows")
+        return U
+
     def observables(self, kde: bool = True, pops: bool = True):
         o = np.zeros(7)
         P = np.zeros((3, NBINS)) if kde else None
@@ -323,8 +331,9 @@ class Simulation:
 
     def enable_timing(self, period: int = 1, kinds: int = 3, offset: int | None = None):
         """bracket every `period`-th hot-kernel launch with HIP events (0/False: off); kinds:
-        bit 0 force launches, bit 1 fused-substep launches; offset: which launch of each period
-        (default period // 2)"""
+        bit 0 force launches, bit 1 fused-substep launches, bit 2 the potential calls' block kernel, bit 3
+        the force-call breakdown (force_breakdown); offset: which launch of each period (default
+        period // 2)"""
         if offset is None:
             check(lib().mdqt_enable_timing_kinds(self.h, int(period), int(kinds)))
         else:
@@ -360,12 +369,25 @@ class Simulation:
         return a.value, na.value, b.value, nb.value
 
     def kernel_times(self):
-        """{force_ms, n_force, substep_ms, n_substep, block_ms, n_block} since the last call (block: the
-        Newton-3 block kernel alone inside the timed force calls; include/mdqt.h mdqt_kernel_times)"""
-        out = (C.c_double * 6)()
-        check(lib().mdqt_kernel_times(self.h, out, 6), "kernel_times")
-        keys = ("force_ms", "n_force", "substep_ms", "n_substep", "block_ms", "n_block")
+        """{force_ms, n_force, substep_ms, n_substep, block_ms, n_block, pot_block_ms, n_pot_block} since
+        the last call (block: the Newton-3 block kernel alone inside the timed force calls; pot_block: the
+        same kernel in the timed potential calls, timing kinds bit 2; include/mdqt.h mdqt_kernel_times)"""
+        out = (C.c_double * 8)()
+        check(lib().mdqt_kernel_times(self.h, out, 8), "kernel_times")
+        keys = ("force_ms", "n_force", "substep_ms", "n_substep", "block_ms", "n_block", "pot_block_ms", "n_pot_block")
         return {k: (int(out[i]) if k.startswith("n_") else out[i]) for i, k in enumerate(keys)}
+
+    BREAKDOWN_KEYS = ("allgather", "sort_boxes", "plan", "block_kernel", "slot_reduce", "tail_pass",
+                      "reduce_scatter", "forces_total")
+
+    def force_breakdown(self):
+        """the force-call breakdown (timing kinds bit 3, with bit 0): average ms per timed block-scheme
+        force call of each stage, and the number of calls (include/mdqt.h mdqt_force_breakdown)"""
+        out = (C.c_double * 9)()
+        check(lib().mdqt_force_breakdown(self.h, out, 9), "force_breakdown")
+        d = {k: out[i] for i, k in enumerate(self.BREAKDOWN_KEYS)}
+        d["calls"] = int(out[8])
+        return d
 
 
 __all__ = ["forces_raw", "potentials_raw", "Simulation", "MdqtError", "default_params", "device_count", "slab", "NBINS", "NUM_STATES"]

@@ -458,6 +458,40 @@ void orc_forces_index(int N, double L, double lDeb, const double* R, size_t ld, 
     (void)nthreads;
 }
 
+/* rows idx[0..nidx) of the pair potential exp(-r/lDeb)/r over all j inside L/2 (SpeedUp:256-266, the terms
+ * Epotential() sums), compensated (Neumaier) sum: U[k] = U_idx[k] (sampled-ion checks at large N) */
+void orc_potentials_index(int N, double L, double lDeb, const double* R, size_t ld, const int* idx, int nidx,
+                          double* U, int nthreads) {
+    const double Rcut = L / 2.;
+    const double* X = R; const double* Y = R + ld; const double* Z = R + 2 * ld;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int k = 0; k < nidx; k++) {
+        const int i = idx[k];
+        double S = 0., C = 0.;
+        double rx = X[i], ry = Y[i], rz = Z[i];
+        for (int j = 0; j < N; j++) {
+            if (j == i) continue;
+            double dx = rx - X[j];
+            double dy = ry - Y[j];
+            double dz = rz - Z[j];
+            dx -= L * round(dx / L);
+            dy -= L * round(dy / L);
+            dz -= L * round(dz / L);
+            double dr = sqrt(dx * dx + dy * dy + dz * dz);
+            if (dr > 0 && dr < Rcut) {
+                const double t = exp(-dr / lDeb) / (dr);                                  /* :265 */
+                const double u = S + t;
+                C += (fabs(S) >= fabs(t)) ? (S - u) + t : (t - u) + S;
+                S = u;
+            }
+        }
+        U[k] = S + C;
+    }
+    (void)nthreads;
+}
+
 void orc_set_ion_ids(orc_sim* s, const uint64_t* ids, int n) {
     free(s->ion_ids);
     s->ion_ids = NULL;

@@ -102,6 +102,10 @@ void   orc_forces_rows(int N, int lo, int hi, double L, double lDeb, const doubl
  * checks at large N) */
 void   orc_forces_index(int N, double L, double lDeb, const double* R, size_t ld, const int* idx, int nidx,
                         double* F, int nthreads);
+/* rows idx[0..nidx) of the pair potential (the terms of Epotential(), SpeedUp:256-266), compensated sum:
+ * U[k] = sum over j != idx[k] inside L/2 of exp(-r/lDeb)/r */
+void   orc_potentials_index(int N, double L, double lDeb, const double* R, size_t ld, const int* idx, int nidx,
+                            double* U, int nthreads);
 /* Philox ion key of local ion i = ids[i] (default i): a subset of a large system's ions run by the
  * oracle draws the same uniforms as the full system */
 void   orc_set_ion_ids(orc_sim* s, const uint64_t* ids, int n);

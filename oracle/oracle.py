@@ -78,6 +78,8 @@ def lib():
                                       C.c_size_t, _dp, C.c_int]
         L.orc_forces_index.argtypes = [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t,
                                        C.POINTER(C.c_int), C.c_int, _dp, C.c_int]
+        L.orc_potentials_index.argtypes = [C.c_int, C.c_double, C.c_double, _dp, C.c_size_t,
+                                           C.POINTER(C.c_int), C.c_int, _dp, C.c_int]
         L.orc_set_ion_ids.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
         L.orc_epotential.restype = C.c_double
         L.orc_epotential.argtypes = [C.c_void_p]
@@ -300,6 +302,17 @@ def forces_index(R, idx, L, lDeb, nthreads=1):
     F = np.zeros((3, len(ii)))
     lib().orc_forces_index(N, L, lDeb, _p(R), N, ii.ctypes.data_as(C.POINTER(C.c_int)), len(ii), _p(F), nthreads)
     return F
+
+
+def potentials_index(R, idx, L, lDeb, nthreads=1):
+    """U[len(idx)]: the pair-potential row sums (SpeedUp:256-266's terms) of the ions idx over all j,
+    compensated, for sampled-row checks of Epotential() at large N"""
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    N = R.shape[1]
+    ii = np.ascontiguousarray(idx, dtype=np.int32)
+    U = np.zeros(len(ii))
+    lib().orc_potentials_index(N, L, lDeb, _p(R), N, ii.ctypes.data_as(C.POINTER(C.c_int)), len(ii), _p(U), nthreads)
+    return U
 
 
 def epotential_raw(R, L, lDeb):

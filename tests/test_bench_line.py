@@ -45,7 +45,7 @@ def test_recorded_r04d_line_fits_and_parses():
     for k in ("md_only_c3", "sharded", "sharded_1m", "pump_models", "mcmd", "jobs_per_gpu", "end_to_end"):
         assert k in h["lines"], k
     assert h["lines"]["sharded_1m"]["roofline"]["bound"] == "fp64"
-    assert h["lines"]["md_only_c3"]["cpu_baseline"] == out["md_only_c3"]["cpu_baseline"]["value"]
+    assert h["lines"]["md_only_c3"]["cpu_baseline"] == bench._sig(out["md_only_c3"]["cpu_baseline"]["value"])
     assert '"tiers"' not in so and '"force_tail":' not in so and '"pmc"' not in so
     # the detail line keeps everything
     det = [l for l in se.splitlines() if l.startswith("BENCH_DETAIL ")]
@@ -79,3 +79,35 @@ def test_md_only_config_list():
     import pytest
     with pytest.raises(SystemExit):
         bench.md_only_configs("c5")                  # QT on: not an MD-only line
+
+
+def test_synthetic_world8_line_fits():
+    """a W = 8 line — every large line sharded over 8 ranks with its force-call
+    breakdown, load imbalance and Epotential timing, plus the large end-to-end lines — stays within the
+    8 KB budget with no secondary line dropped"""
+    with open(R04D) as f:
+        out = json.load(f)
+    out["n_gpus"] = out["comm_size"] = 8
+    bd = {k: 12.3456789 for k in ("allgather", "sort_boxes", "plan", "block_kernel", "slot_reduce", "tail_pass",
+                                  "reduce_scatter", "forces_total", "stages_sum")}
+    bd["stages_sum_vs_force_call"] = 0.99876543
+    for k in ("md_only_c3", "md_only_c4", "sharded", "sharded_1m"):
+        line = dict(out.get(k) or out["sharded_1m"])
+        line["n_gpus"] = 8
+        line["force_breakdown_ms"] = dict(bd)
+        line["epotential"] = {"wall_ms": 123.456789, "block_kernel_ms": 101.23456, "vs_force_call": 0.987654321}
+        roof = dict(line.get("roofline") or {})
+        roof.update(bound="fp64+fp32", frac=0.412345678, fp64_frac=0.31234567, f32_frac=0.1012345678,
+                    load_imbalance=1.0123456789)
+        line["roofline"] = roof
+        out[k] = line
+    for k in ("end_to_end_c5", "end_to_end_1m"):
+        out[k] = dict(out["end_to_end"], N=1000258, epot_ms=190.123456)
+    so, _ = _emit(out)
+    h = _check_head(so.strip().splitlines()[-1])
+    assert "lines_in_detail_only" not in h, h.get("lines_in_detail_only")
+    for k in ("md_only_c3", "md_only_c4", "sharded", "sharded_1m", "end_to_end_c5", "end_to_end_1m"):
+        assert k in h["lines"], k
+    assert h["lines"]["sharded_1m"]["force_breakdown_ms"]["reduce_scatter"] == 12.346
+    assert h["lines"]["sharded_1m"]["roofline"]["f32_frac"] == 0.10123
+    print(f"W = 8 headline line: {len(so.strip().splitlines()[-1])} bytes")

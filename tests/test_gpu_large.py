@@ -679,3 +679,44 @@ def test_weighted_block_ranges_local_group():
     assert worst < 1e-13
     for s in sims:
         s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["C5", "C4", "1M"])
+def test_epotential_on_the_plan(cfg, orc):
+    """Epotential() (SpeedUp:244-281) on the Newton-3 blocks with the force call's plan (round 6, VERDICT
+    r05 item 2; option potential_plan 1): skip radius, sub-tile groups, the error-bounded pair forms for
+    u = e^(-r/lDeb)/r and the enforced tail.  Since u(r) < lDeb g(r) and each form's relative error on u is
+    at most its error on the force, every U_i stays within lDeb x (the tail eps 1e-12 + the tiers' bounds)
+    of the sum to L/2 — checked on ~640 sampled ions against the oracle's compensated rows
+    (orc_potentials_index), beside the exact block path (potential_plan 0); Epot = sum U_i / 2N within
+    1e-12 relative of the exact path's (north_star asks 1e-6 relative for energies)"""
+    import mdqtplasmasims_amd as M
+    if M.device_count() < 1:
+        pytest.fail("no GPU visible to the gpu-marked tests")
+    kw = dict(CONFIGS[cfg])
+    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **kw).init()
+    N, L, lDeb = s.N, s.const("L"), s.const("lDeb")
+    assert s.const("force_scheme") == 3 and s.const("potential_plan") == 1
+    U1 = s.potential_rows()
+    e1 = s.Epotential()
+    s.set_option("potential_plan", 0)
+    U0 = s.potential_rows()
+    e0 = s.Epotential()
+    R = s.get_state()["R"]
+    bounds = sum(s.const(k) for k in ("force_mid_bound", "force_far_bound", "force_vfar_bound", "force_ufar_bound"))
+    s.close()
+    rng = np.random.default_rng(5)
+    idx = sample_ions(N, 640, rng)
+    G = orc.potentials_index(R, idx, L, lDeb, nthreads=threads())
+    d1, d0 = np.abs(U1[idx] - G).max(), np.abs(U0[idx] - G).max()
+    gate = lDeb * (1e-12 + bounds) + 1e-13 * np.abs(G).max()
+    rel = abs(e1 - e0) / abs(e0)
+    print(f"{cfg}: N={N} sampled {len(idx)}: plan max|dU| = {d1:.3e} (gate {gate:.3e}), exact max|dU| = {d0:.3e}; "
+          f"Epot plan {e1:.15g} exact {e0:.15g} rel {rel:.2e}; max|U_plan - U_exact| over all ions "
+          f"{np.abs(U1 - U0).max():.3e}")
+    assert d0 <= 1e-12 * np.abs(G).max()
+    assert d1 <= gate
+    assert np.abs(U1 - U0).max() <= gate + 1e-13 * np.abs(U0).max()
+    assert rel <= 1e-12
+    assert abs(e1 - U1.sum() / 2 / N) <= 1e-12 * abs(e1)

@@ -139,13 +139,15 @@ def test_newton3_blocks_sizes(eng, orc, N0):
     assert np.abs(s2.get_state()["V"] - o.get_state()["V"]).max() < 1e-10
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_newton3_blocks_local_group(eng, orc, world):
+@pytest.mark.parametrize("world,N0", [(2, 5000), (3, 5000), (2, 400), (3, 700)])
+def test_sharded_newton3_blocks_local_group(eng, orc, world, N0):
     """sharded Newton-3 block pairs: every rank computes its blocks' pairs for all ions, the dense
     partials are reduce-scattered (in-process group: summed in rank order) — forces within the
-    1e-13 gate of the oracle, trajectories within the short-horizon gate"""
+    1e-13 gate of the oracle, trajectories within the short-horizon gate.  N0 = 400 (one block) at
+    world 2 and N0 = 700 (two blocks) at world 3 leave a rank without blocks: its dense partial must
+    be 0, whatever its unused plan memory holds (the per-J-tile masks)"""
     from mdqtplasmasims_amd.engine import comm_init_local
-    kw = dict(N0=5000, seed=9)
+    kw = dict(N0=N0, seed=9)
     o = orc.OracleSim(nthreads=8, rng_mode=1, **kw).init()
     st = o.get_state()
     sims = [eng.Simulation(world_size=world, rank=r, **kw) for r in range(world)]
@@ -827,3 +829,25 @@ def test_tile_split_of_the_last_round(eng):
         assert d.max() <= 1e-13 * scale
         assert ks[sp] == 0 or d.max() > 0              # (the split ran: another summation order)
     assert not np.abs(out[1] - out[0])[:, 2 * ks[1] * 64:].any()   # halves: only the split pairs' tiles
+
+
+def test_tile_split_fixed_cu_count(eng):
+    """force_split_cus: the split table cut for a given CU count on any device — 256
+    gives the MI355X table bit for bit whatever the device, another count another table (a 304-CU
+    device's: C2's 1,596 workgroups leave 76 in the last round, 20 whole pairs) within rounding"""
+    s = eng.Simulation(N0=3500, seed=12346, job=1).init()
+    out, ks = {}, {}
+    for n in (0, 256, 304):
+        s.set_option("force_split_cus", n)
+        assert s.const("force_split_cus") == n
+        ks[n] = int(s.const("force_tile_split_pairs"))
+        s.forces()
+        out[n] = s.get_state()["F"]
+    cus = s.const("device_cus")
+    s.close()
+    assert ks[256] == 4
+    if cus == 256:
+        assert ks[0] == 4 and np.array_equal(out[0], out[256])
+    scale = np.abs(out[256]).max()
+    assert ks[304] != ks[256]
+    assert np.abs(out[304] - out[256]).max() <= 1e-13 * scale

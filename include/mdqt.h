@@ -264,6 +264,10 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     0 = the general instance (bit-identical up to the sign of zero)
  *   "potential_n3":   1 (default) = Epotential on the Newton-3 tiles / blocks (each distinct
  *                     pair once; world 1), 0 = the owner-computes potential rows (Epot within 1e-14 relative)
+ *   "potential_plan": Newton-3 blocks (N > 65,536, world 1): 1 (default, round 6) = Epotential on the
+ *                     force call's plan — its skip radius, sub-tile groups, error-bounded pair forms and
+ *                     enforced tail; u(r) < lDeb g(r), so every U_i is within lDeb x the force call's
+ *                     per-ion bound (~1e-12) of its sum to L/2; 0 = every pair to L/2 in the exact form
  *   "init_threads":   init() rejection sampling: 0 = auto, 1 = sequential, k = k host threads
  *                     (bit-identical positions, psi and drand48 state in every setting)
  *   "fused_step", "overlap": 1 = the one-launch MD step / the two-stream MD step (measured and
@@ -316,6 +320,10 @@ int         mdqt_enable_timing_at(mdqt_ctx* c, int period, int kinds, int offset
  * skipped ones) for the current positions: out[0 .. *nblocks) for blocks Plo .. Phi - 1; at world 1
  * every block, so the work of any partition of the blocks over ranks follows (load balance) */
 int         mdqt_force_block_work(mdqt_ctx* c, double* out, int n, int* nblocks);
+/* the block kernel's lock-step J loop for the current positions (diagnostic): out[0] the estimated VALU
+ * instructions of all its tile pairs (per-form counts), out[1] 8 x the sum over J steps of the busiest
+ * wave's, out[2] the J steps with work; out[1] / out[0] = the max-over-mean excess the J-step barriers cost */
+int         mdqt_force_jstep_balance(mdqt_ctx* c, double* out, int n);
 int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
                                     int* nsub);
 /* the same with the Newton-3 block kernel (k_pairs_n3b, N > 65,536) timed on its own inside every

@@ -1658,6 +1658,28 @@ extern "C" int mdqt_force_census(mdqt_ctx* s, double* out, int n) {
     return 0;
 }
 
+// the lock-step J loop's balance over a workgroup's 8 waves for the current positions (k_n3b_census, bal):
+// out[0] the estimated VALU instructions of all tile pairs, out[1] the sum over J steps of 8 x the busiest
+// wave's, out[2] the J steps with work — out[1] / out[0] is the excess of max over mean (diagnostic)
+extern "C" int mdqt_force_jstep_balance(mdqt_ctx* s, double* out, int n) {
+    if (!s || !out) return fail("mdqt_force_jstep_balance: NULL argument");
+    if (n < 3) return fail("mdqt_force_jstep_balance: need 3 doubles");
+    if (!s->use_n3b || !s->sort_mode) return fail("mdqt_force_jstep_balance: Newton-3 blocks in spatial order only");
+    HIPCHK(hipSetDevice(s->dev));
+    N3BArgs a;
+    if (n3b_args(s, a)) return -1;
+    unsigned long long* d = nullptr;
+    unsigned long long h[3];
+    HIPCHK(hipMalloc(&d, (2 * kCensus + 3) * sizeof(unsigned long long)));
+    hipError_t e = launch_n3b_census(a, d, s->stream, nullptr, d + 2 * kCensus);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d + 2 * kCensus, sizeof h, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail("mdqt_force_jstep_balance: %s", hipGetErrorString(e));
+    out[0] = (double)h[0]; out[1] = 8. * (double)h[1]; out[2] = (double)h[2];
+    return 0;
+}
+
 // the block kernel's evaluated lane-steps per block of this rank for the current positions (k_n3b_census's
 // per-block sums): out[P - Plo], P = Plo .. Phi - 1 (*nblocks = Phi - Plo) — what each block's workgroups
 // do; at world 1 every block, so the work of any rank partition follows

@@ -260,10 +260,19 @@ __device__ __forceinline__ void n3b_group(int b0, double w, double xi, double yi
                                           double* az, double& fx, double& fy, double& fz, const PairC& c,
                                           const double* nsh, double w_last = 1.) {
     N3B_REBASE(b0);
+    LdsPJ p = lds_pj(pjb, 0);
 #pragma unroll
-    for (int t = 0; t < NSTEP; ++t)
-        n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX>(t, t == NSTEP - 1 ? w * w_last : w, xi, yi, zi, mi,
-                                                                   pjb, mjb, axb, ayb, azb, fx, fy, fz, c, nsh);
+    for (int t = 0; t < NSTEP; ++t) {
+        if constexpr (MDQT_LDS_SPLIT) {             // (the LDS bases opaque per step: ds_read_b64, no read2)
+            lds_pj_opaque(p);
+            n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX, LdsPJ>(t, t == NSTEP - 1 ? w * w_last : w, xi, yi,
+                                                                              zi, mi, p, mjb, axb, ayb, azb, fx, fy, fz,
+                                                                              c, nsh);
+        } else {
+            n3_step<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX>(t, t == NSTEP - 1 ? w * w_last : w, xi, yi, zi,
+                                                                       mi, pjb, mjb, axb, ayb, azb, fx, fy, fz, c, nsh);
+        }
+    }
 }
 
 // a whole tile pair in one pair form: the groups of `groups` (off the diagonal) or the diagonal
@@ -1093,18 +1102,26 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
 // kernel's wave q at J-step b does.
 // bw (optional): the evaluated lane-steps (every class but the skipped ones) per block of this rank,
 // bw[P - Plo] — the work each block's workgroups do, for the ranks' load balance (mdqt_force_block_work)
+// bal (optional, round 6): the J steps' balance over the workgroup's 8 waves — each tile pair's VALU
+// instructions estimated from its groups' classes (kCensusValu: per wave-step of each form, from the ISA
+// counts in docs/FORCES.md) — bal[0] += sum over the waves, bal[1] += the busiest wave's, bal[2] += 1 per
+// J step with work: bal[1] / (bal[0] / 8) is the barrier-bound excess of the lock-step J loop
+__constant__ const unsigned kCensusValu[kCensus] = {0, 0, 52, 48, 39, 38, 31, 32, 27, 25, 9, 0, 44, 36};
 __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long long* __restrict__ out,
-                                                    unsigned long long* __restrict__ bw) {
+                                                    unsigned long long* __restrict__ bw,
+                                                    unsigned long long* __restrict__ bal) {
     __shared__ unsigned long long h[2 * kCensus];
     __shared__ unsigned long long hb;
     const int t = threadIdx.x;
     if (t < 2 * kCensus) h[t] = 0;
     if (t == 0) hb = 0;
     __syncthreads();
+    unsigned long long cost = 0;                    // this tile pair's estimated VALU (bal)
     auto add = [&](int k, unsigned long long steps, unsigned long long pairs) {
         atomicAdd(&h[k], steps);
         atomicAdd(&h[kCensus + k], pairs);
         if (k != 0 && k != 1 && k != 11) atomicAdd(&hb, steps);
+        cost += (steps / 64) * kCensusValu[k];
     };
     const int P = a.Plo + (int)blockIdx.x / a.nd, db = (int)blockIdx.x % a.nd;
     const int q = t & (BW - 1), b = t / BW;
@@ -1150,6 +1167,20 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
             const unsigned lv = sub_group_levels(mm, mf, mv, mu, m32);
             for (int d = 0; d < 4; ++d)
                 add((g >> d) & 1u ? cls_of((lv >> (4 * d)) & 15u) : 11, 1024ull, (unsigned long long)np[d]);
+        }
+    }
+    if (bal) {                                      // the 8 threads of J step b: lanes 8 (b mod 8) .. + 7
+        unsigned long long sm = cost, mx = cost;
+#pragma unroll
+        for (int off = 1; off < BW; off <<= 1) {
+            sm += __shfl_xor(sm, off);
+            const unsigned long long o = __shfl_xor(mx, off);
+            mx = o > mx ? o : mx;
+        }
+        if (q == 0 && sm) {
+            atomicAdd(bal, sm);
+            atomicAdd(bal + 1, mx);
+            atomicAdd(bal + 2, 1ull);
         }
     }
     __syncthreads();
@@ -1506,13 +1537,15 @@ hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const
     return hipGetLastError();
 }
 
-hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s, unsigned long long* bw) {
+hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s, unsigned long long* bw,
+                             unsigned long long* bal) {
     if (!a.use_sort || !a.boxes || !a.subboxes) return hipErrorInvalidValue;   // the classes need the boxes
     const int nblk = (a.Phi - a.Plo) * a.nd;
     if (hipMemsetAsync(out, 0, 2 * kCensus * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
     if (bw && a.Phi > a.Plo && hipMemsetAsync(bw, 0, (size_t)(a.Phi - a.Plo) * sizeof(unsigned long long), s) != hipSuccess)
         return hipGetLastError();
-    if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out, bw);
+    if (bal && hipMemsetAsync(bal, 0, 3 * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
+    if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out, bw, bal);
     return hipGetLastError();
 }
 

@@ -489,7 +489,8 @@ constexpr int kCensus = 14;
 #define MDQT_N3B_BW 8
 #endif
 constexpr int kN3BBlock = MDQT_N3B_BW;
-hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s, unsigned long long* bw = nullptr);
+hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStream_t s, unsigned long long* bw = nullptr,
+                             unsigned long long* bal = nullptr);
 hipError_t launch_sum_rank_chunks(const double* const* parts, int world, int rank, int S, double* F, hipStream_t s);
 
 // ---- Monte-Carlo + MD analytics program (mdmc_kernels.hip) ----

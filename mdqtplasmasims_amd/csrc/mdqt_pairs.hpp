@@ -275,13 +275,29 @@ __device__ __forceinline__ void accum(double& f, double d, double ft) {
 // MAX >= 0 (Newton-3 blocks, a tile pair whose image varies on one axis only): the caller passes the
 // i position shifted on the other two axes (as SHIFT), and the minimum image is taken per pair on axis
 // MAX alone — mic_r's operations on that axis, none on the others
+// J positions in LDS: the arrays pj[3][128] (generic pointer), or (MDQT_LDS_SPLIT) one LDS address per
+// component, made opaque at every rotation step by the caller — so that the compiler cannot merge two
+// steps' reads into one ds_read2_b64 (8 LDS cycles per wave for 2 x 512 B, where two ds_read_b64 take 2 + 2;
+// MI355X_MICROARCH.md §LDS) nor needs a v_add_u32 for a base beyond read2's 8-bit offset field
+#ifndef MDQT_LDS_SPLIT
+#define MDQT_LDS_SPLIT 0
+#endif
+typedef __attribute__((address_space(3))) const double* lds_dp;
+struct LdsPJ { lds_dp x, y, z; };
+__device__ __forceinline__ double pj_at(const double (*pj)[128], int c, int idx) { return pj[c][idx]; }
+__device__ __forceinline__ double pj_at(const LdsPJ& p, int c, int idx) { return (c == 0 ? p.x : c == 1 ? p.y : p.z)[idx]; }
+__device__ __forceinline__ LdsPJ lds_pj(const double (*pj)[128], int b) {   // component bases at index b
+    return LdsPJ{(lds_dp)&pj[0][b], (lds_dp)&pj[1][b], (lds_dp)&pj[2][b]};
+}
+__device__ __forceinline__ void lds_pj_opaque(LdsPJ& p) { asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z)); }
+
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          int FAR = 0, int MAX = -1>
+          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128]>
 __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi, double zi, double mi,
-                                         const double (*pj)[128], const double* mj, double& fx, double& fy,
+                                         PJ pj, const double* mj, double& fx, double& fy,
                                          double& fz, const PairC& c, const double* nsh, double& px, double& py,
                                          double& pz) {
-    double dx = xi - pj[0][idx], dy = yi - pj[1][idx], dz = zi - pj[2][idx];   // :213-215
+    double dx = xi - pj_at(pj, 0, idx), dy = yi - pj_at(pj, 1, idx), dz = zi - pj_at(pj, 2, idx);   // :213-215
     if constexpr (SHIFT) {
         if (!MDQT_SHIFT_I) {
             dx = fma(-nsh[0], c.L, dx);             // = mic_r's fma(-rint(dx / L), L, dx)
@@ -325,13 +341,13 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
 // (ds_add_f64 at index idx, no return; one wave's LDS operations run in order, so the
 // accumulation order is fixed)
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          int FAR = 0, int MAX = -1>
+          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128]>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
-                                        const double (*pj)[128], const double* mj, double* ax, double* ay,
+                                        PJ pj, const double* mj, double* ax, double* ay,
                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
                                         const double* nsh = nullptr) {
     double px, py, pz;
-    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh, px,
+    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX, PJ>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh, px,
                                                                 py, pz);
 #if defined(MDQT_EXPT_NOJACC)
     (void)ax; (void)ay; (void)az;
@@ -423,8 +439,20 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     double* ax = accj[q][0];
     double* ay = accj[q][1];
     double* az = accj[q][2];
+    LdsPJ pb{};                                     // MDQT_LDS_SPLIT: the bases at the loop's first index
+    int pbase = 0;
+    auto set_base = [&](int b) {
+        if constexpr (MDQT_LDS_SPLIT) { pb = lds_pj(pj, b); pbase = b; }
+    };
     auto step = [&](int idx, double m) {
-        n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+        if constexpr (MDQT_LDS_SPLIT) {             // (the LDS bases opaque per step: ds_read_b64, no read2)
+            lds_pj_opaque(pb);
+            n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT, 0, -1, LdsPJ>(idx - pbase, m, xi, yi, zi, mi, pb,
+                                                                          mj + pbase, ax + pbase, ay + pbase,
+                                                                          az + pbase, fx, fy, fz, c);
+        } else {
+            n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+        }
     };
     const bool diag = I == J;
     // progress priority (MDQT_N3_PRIO): a SIMD's VALU issue goes to the highest-priority wave, then
@@ -443,6 +471,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     };
     if (!diag && pl) {                              // steps [part 16 / 2^pl, (part + 1) 16 / 2^pl)
         const int b = l + (64 / N3W) * q + part * ((64 / N3W) >> pl);
+        set_base(b);
         if (pl == 1) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) step(b + t, 1.);
@@ -452,11 +481,13 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         }
     } else if (diag && pl) {                        // a diagonal tile's 8 steps per wave in two halves
         const int b = l + 1 + (32 / N3W) * q + 4 * part;
+        set_base(b);
 #pragma unroll
         for (int t = 0; t < 3; ++t) step(b + t, 1.);
         step(b + 3, (part == 1 && q == N3W - 1 && l >= 32) ? 0. : 1.);   // lane distance 32: once per pair
     } else if (!diag) {
         const int b = l + (64 / N3W) * q;
+        set_base(b);
 #pragma unroll
         for (int t = 0; t < 64 / N3W; ++t) {
             prio(t, 64 / N3W);
@@ -464,6 +495,7 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         }
     } else {
         const int b = l + 1 + (32 / N3W) * q;
+        set_base(b);
 #pragma unroll
         for (int t = 0; t < 32 / N3W - 1; ++t) {
             prio(t, 32 / N3W);

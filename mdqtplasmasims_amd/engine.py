@@ -362,6 +362,14 @@ class Simulation:
               "force_block_work")
         return out[:nb.value].copy()
 
+    def force_jstep_balance(self):
+        """the block kernel's J-step balance over a workgroup's 8 waves (diagnostic; include/mdqt.h
+        mdqt_force_jstep_balance): {valu, valu_lockstep, jsteps, excess}"""
+        out = (C.c_double * 3)()
+        check(lib().mdqt_force_jstep_balance(self.h, out, 3), "force_jstep_balance")
+        return {"valu": out[0], "valu_lockstep": out[1], "jsteps": int(out[2]),
+                "excess": out[1] / out[0] if out[0] else None}
+
     def kernel_time_totals(self):
         """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""
         a = C.c_double(); b = C.c_double(); na = C.c_int(); nb = C.c_int()

@@ -90,6 +90,10 @@ struct mdqt_ctx {
            *dTp = nullptr, *dScr = nullptr, *dKde = nullptr, *dUrow = nullptr;
     double* dUpart = nullptr;      // potential-row partials of its own (small systems, world 1)
     int n3_potential = 1;          // option "potential_n3": 1 = Newton-3 tiles where the forces use them
+#ifndef MDQT_N3B_PAIRS_DEFAULT
+#define MDQT_N3B_PAIRS_DEFAULT 0
+#endif
+    int n3b_pairs = MDQT_N3B_PAIRS_DEFAULT;   // option "force_n3b_pairs": the paired-wave block kernel (k_pairs_n3b_pw)
     int pot_plan = 1;              // option "potential_plan": 1 = Epotential on the blocks takes the force call's
                                    // plan (skips, sub-tile groups, error-bounded forms); 0 = every pair to L/2 exactly
     size_t capUpart = 0;
@@ -1089,6 +1093,7 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "qt_im01")) return s->qc.im01;
     if (!strcmp(n, "potential_n3")) return s->n3_potential;
     if (!strcmp(n, "potential_plan")) return s->pot_plan;
+    if (!strcmp(n, "force_n3b_pairs")) return s->n3b_pairs;
     if (!strcmp(n, "md_step_fused")) return s->last_fused;     // 1: the last MD step was one k_md_step launch
     if (!strcmp(n, "qt_kernel")) return s->last_qt_kernel;     // instance of the last substep launch (QTKernel)
     if (!strcmp(n, "qt_kernel_nseg")) return s->last_qt_nseg;  // force partials its prologue summed
@@ -1506,6 +1511,7 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     a.use_sort = 0; a.Rs = nullptr; a.perm = nullptr; a.boxes = nullptr; a.subboxes = nullptr; a.plan = nullptr;
     a.tmask = nullptr; a.tmw = 0;
     a.ax1 = s->ax1_mode;
+    a.pairs = s->n3b_pairs;
     double bound;
     a.Rskip = skip_radius(s, &bound);
     a.tailb = nullptr;
@@ -1664,19 +1670,25 @@ extern "C" int mdqt_force_census(mdqt_ctx* s, double* out, int n) {
 extern "C" int mdqt_force_jstep_balance(mdqt_ctx* s, double* out, int n) {
     if (!s || !out) return fail("mdqt_force_jstep_balance: NULL argument");
     if (n < 3) return fail("mdqt_force_jstep_balance: need 3 doubles");
+    // (out[3..5] when n >= 6: 8 x the J-step pairs' best two-sub-step schedule, 8 x the same pairs in
+    // lock-step, 8 x the per-(P, db) busiest wave's 8-step sum — see k_n3b_census)
     if (!s->use_n3b || !s->sort_mode) return fail("mdqt_force_jstep_balance: Newton-3 blocks in spatial order only");
     HIPCHK(hipSetDevice(s->dev));
     N3BArgs a;
     if (n3b_args(s, a)) return -1;
     unsigned long long* d = nullptr;
-    unsigned long long h[3];
-    HIPCHK(hipMalloc(&d, (2 * kCensus + 3) * sizeof(unsigned long long)));
+    unsigned long long h[9];
+    HIPCHK(hipMalloc(&d, (2 * kCensus + 9) * sizeof(unsigned long long)));
     hipError_t e = launch_n3b_census(a, d, s->stream, nullptr, d + 2 * kCensus);
     if (e == hipSuccess) e = hipMemcpyAsync(h, d + 2 * kCensus, sizeof h, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(d);
     if (e != hipSuccess) return fail("mdqt_force_jstep_balance: %s", hipGetErrorString(e));
     out[0] = (double)h[0]; out[1] = 8. * (double)h[1]; out[2] = (double)h[2];
+    if (n >= 6) { out[3] = 8. * (double)h[3]; out[4] = 8. * (double)h[4]; out[5] = 8. * (double)h[5]; }
+    // (out[6..8] when n >= 9: 4 waves on two I tiles each — heavy-light pairing, (q, 7 - q), (q, q + 4) —
+    // 4 x the sum over J steps of the busiest wave's pair)
+    if (n >= 9) { out[6] = 4. * (double)h[6]; out[7] = 4. * (double)h[7]; out[8] = 4. * (double)h[8]; }
     return 0;
 }
 
@@ -2994,6 +3006,12 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         s->n3_potential = value;
         return 0;
     }
+    if (!strcmp(name, "force_n3b_pairs")) {            // Newton-3 blocks: 4 waves on two I tiles each (1) or 8 waves (0)
+        if (value < 0 || value > 1) return fail("force_n3b_pairs must be 0 (8 waves, one I tile each) or 1 (4 waves, two each)");
+        if (settle_forces(s)) return -1;
+        s->n3b_pairs = value;
+        return 0;
+    }
     if (!strcmp(name, "potential_plan")) {             // Epotential on the blocks: the force call's plan (1) or exact (0)
         if (value < 0 || value > 1) return fail("potential_plan must be 0 (every pair to L/2) or 1 (the plan)");
         s->pot_plan = value;
@@ -3143,7 +3161,7 @@ extern "C" int mdqt_positions_device(mdqt_ctx* s, void** dptr, int* S) {
 }
 extern "C" int mdqt_enable_timing_at(mdqt_ctx* s, int on, int kinds, int offset) {
     if (!s) return fail("NULL context");
-    if (kinds < 1 || kinds > 3) return fail("mdqt_enable_timing_at: kinds must be 1, 2 or 3");
+    if (kinds < 1 || kinds > 15) return fail("mdqt_enable_timing_at: kinds must be 1 .. 15 (bits: force, substeps, potential block kernel, force breakdown)");
     if (on > 0 && (offset < 0 || offset >= on)) return fail("mdqt_enable_timing_at: offset must be in [0, period)");
     s->timing = on > 0;
     s->tperiod = on > 0 ? (unsigned)on : 1u;

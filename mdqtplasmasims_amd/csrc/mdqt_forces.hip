@@ -581,6 +581,118 @@ __device__ __forceinline__ double raw_half2(const double* B, int T, int J) {
 }
 
 
+// One tile pair (I, J) of the block kernels (k_pairs_n3b, k_pairs_n3b_pw): its sub-tile groups of `word`
+// (k_n3b_plan) in the pair forms of their levels, the image of the class word `tw` (n3b_pack_class); the i
+// side into tx, ty, tz (a fresh sum per tile pair), the j side into the wave's accumulators ax, ay, az.
+// rag: the ragged last tile is one of the two (exact form, validity weights)
+template <int VARIANT, bool GUARD, bool POT, bool AXP>
+__device__ __forceinline__ void n3b_tile_pair(const N3BArgs& a, const PairC& c, int l, bool diag, bool rag, int tw,
+                                              unsigned word, double xi, double yi, double zi, double mi,
+                                              const double (*pj)[128], const double* mj, const float (*pj32)[128],
+                                              double* ax, double* ay, double* az, double& tx, double& ty, double& tz,
+                                              float cf32, float invl32, float rc2f) {
+    constexpr bool CUT = VARIANT == 1 && MDQT_N3_CUT;
+    constexpr bool FARF = VARIANT == 1 && !GUARD && CUT;   // the error-bounded pair forms
+    const unsigned groups = word & 15u;
+    const int ci = (tw & 15) - 2;       // bit 0 uniform image (the tile pair's)
+    if (rag)
+        n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                        az, tx, ty, tz, c);
+    else if (VARIANT == 1 && (ci & 1)) {       // uniform image
+        const double nsh[3] = {(double)((tw << 20) >> 24), (double)((tw << 12) >> 24), (double)((tw << 4) >> 24)};
+        // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
+        const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
+        const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
+        const double sz = MDQT_SHIFT_I ? fma(-nsh[2], a.L, zi) : zi;
+        if constexpr (FARF) {
+            if (diag) {                 // (a tile with itself: the exact form)
+                n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(true, groups, l, sx, sy, sz, mi, pj, mj, ax, ay,
+                                                                az, tx, ty, tz, c, nsh);
+            } else {                    // each form over the groups at its level
+                const unsigned g5 = level_groups(word, 5), g4 = level_groups(word, 4),
+                               g3 = level_groups(word, 3), g2 = level_groups(word, 2),
+                               g1 = level_groups(word, 1), g0 = level_groups(word, 0);
+                if (g4) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 4>(false, g4, l, sx, sy, sz, mi, pj, mj,
+                                                                           ax, ay, az, tx, ty, tz, c, nsh);
+                if (g3) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(false, g3, l, sx, sy, sz, mi, pj, mj,
+                                                                           ax, ay, az, tx, ty, tz, c, nsh);
+                if (g2) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(false, g2, l, sx, sy, sz, mi, pj, mj,
+                                                                           ax, ay, az, tx, ty, tz, c, nsh);
+                if (MDQT_EXP_TAB && g1)
+                    n3b_pair<VARIANT, GUARD, false, true, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(
+                        false, g1, l, sx, sy, sz, mi, pj, mj, ax, ay, az, tx, ty, tz, c, nsh);
+                if (g0) n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(false, g0, l, sx, sy, sz, mi, pj, mj, ax,
+                                                                        ay, az, tx, ty, tz, c, nsh);
+#if !defined(MDQT_EXPT_UFAR_SKIP)                   // last: nothing after it keeps sx, nsh live (diagnostic build: skip it, wrong results)
+                if (g5) n3b_pair_uf32<POT>(g5, l, (float)(sx - pj[0][0]), (float)(sy - pj[1][0]),
+                                           (float)(sz - pj[2][0]), pj32, ax, ay, az, tx, ty, tz, cf32,
+                                           invl32, rc2f);
+#endif
+            }
+        } else {
+            n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, groups, l, sx, sy, sz, mi, pj, mj,
+                                                                    ax, ay, az, tx, ty, tz, c, nsh);
+        }
+    } else if constexpr (FARF) {       // per-pair image
+        const int ax1 = (tw >> 28) & 3;  // 1 + the one axis whose image varies (n3b_pack_class)
+        if (diag) {
+            n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(true, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                             az, tx, ty, tz, c);
+        } else if (AXP && ax1) {        // one axis: the other two shifted once (xi - n L)
+          if constexpr (AXP) {
+            const double sx = fma(-(double)((tw << 20) >> 24), a.L, xi);   // (0 on the varying axis:
+            const double sy = fma(-(double)((tw << 12) >> 24), a.L, yi);   //  fma(-0, L, x) = x)
+            const double sz = fma(-(double)((tw << 4) >> 24), a.L, zi);
+            const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
+                           g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
+            constexpr unsigned LV = MDQT_N3B_AX1_LEVELS;   // the levels that take it (bit x: level x)
+            auto one_axis = [&](auto axc) {
+                constexpr int AX = decltype(axc)::value;
+                if ((LV & 8u) && g3)
+                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3, AX>(false, g3, l, sx, sy, sz, mi, pj, mj,
+                                                                            ax, ay, az, tx, ty, tz, c);
+                if ((LV & 4u) && g2)
+                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2, AX>(false, g2, l, sx, sy, sz, mi, pj, mj,
+                                                                            ax, ay, az, tx, ty, tz, c);
+                if ((LV & 2u) && MDQT_EXP_TAB && g1)
+                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0, AX>(
+                        false, g1, l, sx, sy, sz, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
+            };
+            if (ax1 == 1) one_axis(std::integral_constant<int, 0>{});
+            else if (ax1 == 2) one_axis(std::integral_constant<int, 1>{});
+            else one_axis(std::integral_constant<int, 2>{});
+            // the other levels per pair (the exact level with a varying image: ~never, C3 1.6e-5
+            // of the pairs)
+            if (!(LV & 8u) && g3)
+                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3>(false, g3, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                    az, tx, ty, tz, c);
+            if (!(LV & 4u) && g2)
+                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                    az, tx, ty, tz, c);
+            if (!(LV & 2u) && MDQT_EXP_TAB && g1)
+                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(
+                    false, g1, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
+            if (g0) n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(false, g0, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                     ay, az, tx, ty, tz, c);
+          }
+        } else {                        // (ultra far with a per-pair image: rare, very-far form)
+            const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
+                           g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
+            if (g3) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3>(false, g3, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                        ay, az, tx, ty, tz, c);
+            if (g2) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax,
+                                                                        ay, az, tx, ty, tz, c);
+            if (MDQT_EXP_TAB && g1)
+                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(false, g1, l, xi, yi, zi, mi,
+                                                                                   pj, mj, ax, ay, az, tx, ty, tz, c);
+            if (g0) n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(false, g0, l, xi, yi, zi, mi, pj, mj, ax, ay,
+                                                                     az, tx, ty, tz, c);
+        }
+    } else
+        n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay, az,
+                                                         tx, ty, tz, c);
+}
+
 // POT: Epotential's pair potential (component 0 of the slots, both rows +u) instead of the force
 // the fast variant fits 80 VGPRs (6 waves per SIMD: three 8-wave workgroups per CU); the exact one (libm exp, divisions) gets 128
 #ifndef MDQT_N3B_IRUN_LDS
@@ -825,108 +937,14 @@ void k_pairs_n3b(N3BArgs a) {
             const unsigned word = __builtin_amdgcn_readfirstlane(sh.pw[buf][q].y);
             const unsigned groups = word & 15u;
             if (mine && cls >= 0 && groups) {
-                const int ci = cls;                 // bit 0 uniform image (the tile pair's)
                 // blocked i accumulation: the tile pair's steps into a fresh sum, those into the
                 // block distance's sum, those into the run's (a run is ~1e5 pair terms at N = 1e6;
                 // in spatial order they arrive in coherent groups, and one serial chain would
                 // carry their rounding: momentum |sum F| / mean |F| 1.8e-8 -> 1e-10 at C4)
                 double tx = 0., ty = 0., tz = 0.;
-                if (ragN && (I == T - 1 || J == T - 1))
-                    n3b_pair<VARIANT, GUARD, true, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
-                                                                    az, tx, ty, tz, c);
-                else if (VARIANT == 1 && (ci & 1)) {       // uniform image
-                    const double nsh[3] = {(double)((tw << 20) >> 24), (double)((tw << 12) >> 24), (double)((tw << 4) >> 24)};
-                    // xi - n L once per tile pair (n3_step SHIFT; MDQT_SHIFT_I)
-                    const double sx = MDQT_SHIFT_I ? fma(-nsh[0], a.L, xi) : xi;
-                    const double sy = MDQT_SHIFT_I ? fma(-nsh[1], a.L, yi) : yi;
-                    const double sz = MDQT_SHIFT_I ? fma(-nsh[2], a.L, zi) : zi;
-                    if constexpr (FARF) {
-                        if (diag) {                 // (a tile with itself: the exact form)
-                            n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(true, groups, l, sx, sy, sz, mi, pj, mj, ax, ay,
-                                                                            az, tx, ty, tz, c, nsh);
-                        } else {                    // each form over the groups at its level
-                            const unsigned g5 = level_groups(word, 5), g4 = level_groups(word, 4),
-                                           g3 = level_groups(word, 3), g2 = level_groups(word, 2),
-                                           g1 = level_groups(word, 1), g0 = level_groups(word, 0);
-                            if (g4) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 4>(false, g4, l, sx, sy, sz, mi, pj, mj,
-                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
-                            if (g3) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 3>(false, g3, l, sx, sy, sz, mi, pj, mj,
-                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
-                            if (g2) n3b_pair<VARIANT, GUARD, false, true, CUT, POT, 2>(false, g2, l, sx, sy, sz, mi, pj, mj,
-                                                                                       ax, ay, az, tx, ty, tz, c, nsh);
-                            if (MDQT_EXP_TAB && g1)
-                                n3b_pair<VARIANT, GUARD, false, true, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(
-                                    false, g1, l, sx, sy, sz, mi, pj, mj, ax, ay, az, tx, ty, tz, c, nsh);
-                            if (g0) n3b_pair<VARIANT, GUARD, false, true, CUT, POT>(false, g0, l, sx, sy, sz, mi, pj, mj, ax,
-                                                                                    ay, az, tx, ty, tz, c, nsh);
-#if !defined(MDQT_EXPT_UFAR_SKIP)                   // last: nothing after it keeps sx, nsh live (diagnostic build: skip it, wrong results)
-                            if (g5) n3b_pair_uf32<POT>(g5, l, (float)(sx - pj[0][0]), (float)(sy - pj[1][0]),
-                                                       (float)(sz - pj[2][0]), sh.pj32, ax, ay, az, tx, ty, tz, cf32,
-                                                       invl32, rc2f);
-#endif
-                        }
-                    } else {
-                        n3b_pair<VARIANT, GUARD, false, VARIANT == 1, CUT, POT>(diag, groups, l, sx, sy, sz, mi, pj, mj,
-                                                                                ax, ay, az, tx, ty, tz, c, nsh);
-                    }
-                } else if constexpr (FARF) {       // per-pair image
-                    const int ax1 = (tw >> 28) & 3;  // 1 + the one axis whose image varies (n3b_pack_class)
-                    if (diag) {
-                        n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(true, groups, l, xi, yi, zi, mi, pj, mj, ax, ay,
-                                                                         az, tx, ty, tz, c);
-                    } else if (AXP && ax1) {        // one axis: the other two shifted once (xi - n L)
-                      if constexpr (AXP) {
-                        const double sx = fma(-(double)((tw << 20) >> 24), a.L, xi);   // (0 on the varying axis:
-                        const double sy = fma(-(double)((tw << 12) >> 24), a.L, yi);   //  fma(-0, L, x) = x)
-                        const double sz = fma(-(double)((tw << 4) >> 24), a.L, zi);
-                        const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
-                                       g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
-                        constexpr unsigned LV = MDQT_N3B_AX1_LEVELS;   // the levels that take it (bit x: level x)
-                        auto one_axis = [&](auto axc) {
-                            constexpr int AX = decltype(axc)::value;
-                            if ((LV & 8u) && g3)
-                                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3, AX>(false, g3, l, sx, sy, sz, mi, pj, mj,
-                                                                                        ax, ay, az, tx, ty, tz, c);
-                            if ((LV & 4u) && g2)
-                                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2, AX>(false, g2, l, sx, sy, sz, mi, pj, mj,
-                                                                                        ax, ay, az, tx, ty, tz, c);
-                            if ((LV & 2u) && MDQT_EXP_TAB && g1)
-                                n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0, AX>(
-                                    false, g1, l, sx, sy, sz, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
-                        };
-                        if (ax1 == 1) one_axis(std::integral_constant<int, 0>{});
-                        else if (ax1 == 2) one_axis(std::integral_constant<int, 1>{});
-                        else one_axis(std::integral_constant<int, 2>{});
-                        // the other levels per pair (the exact level with a varying image: ~never, C3 1.6e-5
-                        // of the pairs)
-                        if (!(LV & 8u) && g3)
-                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3>(false, g3, l, xi, yi, zi, mi, pj, mj, ax, ay,
-                                                                                az, tx, ty, tz, c);
-                        if (!(LV & 4u) && g2)
-                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax, ay,
-                                                                                az, tx, ty, tz, c);
-                        if (!(LV & 2u) && MDQT_EXP_TAB && g1)
-                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(
-                                false, g1, l, xi, yi, zi, mi, pj, mj, ax, ay, az, tx, ty, tz, c);
-                        if (g0) n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(false, g0, l, xi, yi, zi, mi, pj, mj, ax,
-                                                                                 ay, az, tx, ty, tz, c);
-                      }
-                    } else {                        // (ultra far with a per-pair image: rare, very-far form)
-                        const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
-                                       g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
-                        if (g3) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3>(false, g3, l, xi, yi, zi, mi, pj, mj, ax,
-                                                                                    ay, az, tx, ty, tz, c);
-                        if (g2) n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 2>(false, g2, l, xi, yi, zi, mi, pj, mj, ax,
-                                                                                    ay, az, tx, ty, tz, c);
-                        if (MDQT_EXP_TAB && g1)
-                            n3b_pair<VARIANT, GUARD, false, false, CUT, POT, MDQT_EXP_TAB ? 1 : 0>(false, g1, l, xi, yi, zi, mi,
-                                                                                               pj, mj, ax, ay, az, tx, ty, tz, c);
-                        if (g0) n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(false, g0, l, xi, yi, zi, mi, pj, mj, ax, ay,
-                                                                                 az, tx, ty, tz, c);
-                    }
-                } else
-                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT>(diag, groups, l, xi, yi, zi, mi, pj, mj, ax, ay, az,
-                                                                     tx, ty, tz, c);
+                n3b_tile_pair<VARIANT, GUARD, POT, AXP>(a, c, l, diag, ragN && (I == T - 1 || J == T - 1), tw, word, xi, yi,
+                                                        zi, mi, pj, mj, sh.pj32, ax, ay, az, tx, ty, tz, cf32, invl32,
+                                                        rc2f);
                 bx += tx; by += ty; bz += tz;
             }
             if (kDbuf && plan && q == kStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA retired
@@ -969,6 +987,217 @@ void k_pairs_n3b(N3BArgs a) {
     }
 }
 
+
+// k_pairs_n3b_pw's tile pairing of a block distance: wave k runs I tiles (bits 6k..6k+2, 6k+3..6k+5);
+// without a plan the fixed pairing (k, 7 - k)
+constexpr unsigned kN3BPairsDefault = (0u | 7u << 3) | (1u | 6u << 3) << 6 | (2u | 5u << 3) << 12 | (3u | 4u << 3) << 18;
+static_assert(BW == 8, "the paired-wave pairing word holds 8 tiles");
+// a tile pair's estimated VALU instructions per lane (the pairing's weights: per wave-step of each pair
+// form — exact, mid, far, very far, ultra far, f32 ultra far — uniform / per-pair image; the ragged
+// tile's exact form) from its plan word (class, sub-tile groups by level)
+__device__ __forceinline__ unsigned n3b_word_cost(uint2 w, bool rag, bool diag) {
+    const int cls = (int)(w.x & 15u) - 2;
+    const unsigned groups = w.y & 15u;
+    if (cls < 0 || !groups) return 0u;
+    const bool uni = cls & 1;
+    if (rag) return 52u * (diag ? 40u : 16u * __builtin_popcount(groups));
+    if (diag) return (uni ? 39u : 48u) * 40u;
+    constexpr unsigned wu[6] = {39u, 36u, 31u, 27u, 25u, 9u}, wi[6] = {48u, 44u, 38u, 32u, 32u, 32u};
+    unsigned c = 0;
+#pragma unroll
+    for (int x = 0; x < 6; ++x) c += 16u * (uni ? wu[x] : wi[x]) * __builtin_popcount(level_groups(w.y, x));
+    return c;
+}
+
+// ------------------------------------------------------------------------------------------
+// Paired waves (round 6, option force_n3b_pairs): the blocks, plan, slots and reduction of k_pairs_n3b
+// with a workgroup of BW / 2 = 4 waves, each running TWO of block P's 8 I tiles against every J tile of
+// the block distance — tiles paired per block distance by k_n3b_plan, the one with the most estimated
+// work with the one with the least (n3b_pairing).  k_pairs_n3b's J-step barriers wait for the busiest of
+// its 8 waves, and within a block distance the same tiles are the busy ones (the I tiles nearest block Q):
+// the busiest wave of a J step carried 1.19-1.28 x the mean (k_n3b_census bal, tools/jstep_balance.py),
+// a no-barrier timing build ran 4-12 % faster.  A wave's two tile pairs of a J step add to one j
+// accumulator (the J tile is the same), and the combine sums 4 of them; the I positions of the wave's two
+// tiles are loaded once per block distance, the run's i sums are per tile in LDS.  LDS 31 KB: five
+// workgroups per CU.  Deterministic (the pairing is a function of the positions), not bit-identical to
+// k_pairs_n3b (another summation tree on the j side).
+// ------------------------------------------------------------------------------------------
+constexpr int NWP = BW / 2;                         // waves per workgroup
+template <int W>
+struct N3BSharedPW {
+    double pj[3][128];                              // J positions by sub-tiles twice over (n3b_lds)
+    float pj32[3][128];                             // fl32(xj - c_J) (the f32 ultra-far form)
+    double accj[W][3][128];                         // per-wave j accumulators
+    double mjs[2][128];                             // J validity weights: all ones / the ragged last tile's
+    double etab[64];                                // 2^(k/64) (MDQT_EXP_TAB)
+    double irun[BW][3][64];                         // the run's i sums, per I tile of the block
+    uint2 pw[BW];                                   // the J step's plan words, per I tile
+};
+#ifndef MDQT_N3B_PW_WPE
+#define MDQT_N3B_PW_WPE 5                           // waves per SIMD: five 4-wave workgroups per CU (LDS 31 KB)
+#endif
+template <int VARIANT, bool GUARD, bool POT = false, bool AXP = false>
+__global__ __launch_bounds__(NWP * 64) __attribute__((amdgpu_waves_per_eu(VARIANT == 1 ? MDQT_N3B_PW_WPE : 4, VARIANT == 1 ? MDQT_N3B_PW_WPE : 4)))
+void k_pairs_n3b_pw(N3BArgs a) {
+    __shared__ N3BSharedPW<NWP> sh;
+    double* const etab = sh.etab;
+    stage_exp_tab(etab);
+    const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;   // q: wave-uniform
+    const int l0 = l;
+    const int nP = a.Phi - a.Plo;
+    const int P = a.Plo + (MDQT_N3B_ORDER ? (int)blockIdx.x % nP : (int)blockIdx.x / a.R);
+    const int run = MDQT_N3B_ORDER ? (int)blockIdx.x / nP : (int)blockIdx.x % a.R;
+    const int d0 = run * a.runlen, d1 = min(a.nd, d0 + a.runlen);
+    const PairC c = {a.L, a.micT, a.micGuard, a.Rcut, a.lDeb, a.invlDeb, 1. / a.L, a.rc2, etab};
+    const int T = a.T, N = a.N, S = a.S;
+    const bool ragN = (N & 63) != 0;
+    const bool srt = a.use_sort != 0;
+    const int PS = srt ? a.Npad : S;
+    auto tile_ptr = [&](int tile) { return srt ? a.Rs + tile * 64 : tile_base(a.Rall, tile, S); };
+    const double pad = (double)(l + 1) * 0x1p-10;  // pad ions: distinct points (pair_ft_cut: r > 0)
+    constexpr bool FARF = VARIANT == 1 && !GUARD && VARIANT == 1 && MDQT_N3_CUT;
+    const N3BRadii rad = n3b_radii<VARIANT, POT>(a);
+    auto sgpr_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    const float cf32 = sgpr_f((float)(a.invlDeb * kNegLog2e)), invl32 = sgpr_f((float)a.invlDeb),
+                rc2f = sgpr_f((float)a.rc2);
+    const uint2* plan = a.plan;
+    constexpr int kStage = NWP - 1;                 // stages J; waves 0..2 combine the j sums
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        sh.accj[q][k][l] = 0.; sh.accj[q][k][l + 64] = 0.;
+        sh.irun[q][k][l] = 0.; sh.irun[q + NWP][k][l] = 0.;
+    }
+    double* ax = sh.accj[q][0];
+    double* ay = sh.accj[q][1];
+    double* az = sh.accj[q][2];
+    if (q == kStage) {
+        const int li = n3b_lds(l);
+        const double m1 = (T - 1) * 64 + l < N ? 1. : 0.;
+        sh.mjs[0][li] = 1.; sh.mjs[0][li + 16] = 1.;
+        sh.mjs[1][li] = m1; sh.mjs[1][li + 16] = m1;
+    }
+    const size_t plane = (size_t)3 * a.Npad;
+    const unsigned* jsteps = plan ? (const unsigned*)(plan + (size_t)(a.Phi - a.Plo) * a.nd * (BW * BW)) : nullptr;
+    auto half_db = [&](int db) { return !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2; };
+    for (int db = d0; db < d1; ++db) {
+        if (half_db(db)) continue;
+        const int Q = (P + db) % a.NB;
+        const size_t jw = 2 * ((size_t)(P - a.Plo) * a.nd + db);
+        const unsigned jmask = jsteps ? __builtin_amdgcn_readfirstlane(jsteps[jw]) : ~0u;
+        // the wave's two I tiles of this block distance (k_n3b_plan; without a plan: q and 7 - q)
+        const unsigned pr = jsteps ? __builtin_amdgcn_readfirstlane(jsteps[jw + 1]) : kN3BPairsDefault;
+        const int tA = (pr >> (6 * q)) & 7, tB = (pr >> (6 * q + 3)) & 7;
+        const int IA = P * BW + tA, IB = P * BW + tB;
+        const bool vA = IA < T, vB = IB < T;
+        double xA = pad, yA = pad, zA = pad, mA = 0., xB = pad, yB = pad, zB = pad, mB = 0.;
+        if (vA && IA * 64 + l < N) {
+            const double* p = tile_ptr(IA) + l;
+            xA = p[0]; yA = p[PS]; zA = p[2 * PS]; mA = 1.;
+        }
+        if (vB && IB * 64 + l < N) {
+            const double* p = tile_ptr(IB) + l;
+            xB = p[0]; yB = p[PS]; zB = p[2 * PS]; mB = 1.;
+        }
+        double bxA = 0., byA = 0., bzA = 0., bxB = 0., byB = 0., bzB = 0.;
+        bool work = false;
+        for (int b = 0; b < BW; ++b) {
+            const int J = Q * BW + b;
+            if (J >= T) break;
+            if (jsteps && !((jmask >> b) & 1u)) {   // every tile pair of this J step skipped (wave-uniform)
+                if (q < (POT ? 1 : 3) && !a.tmask)
+                    a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + lane_opaque(l0)] = POT ? 0. : -0.;
+                continue;
+            }
+            work = true;
+            if (q == kStage) {                      // stage J (by sub-tiles, twice over) and the step's plan words
+                const int j = J * 64 + l;
+                const bool vj = j < N;
+                const double* p = tile_ptr(J) + l;
+                const double xj = vj ? p[0] : pad, yj = vj ? p[PS] : pad, zj = vj ? p[2 * PS] : pad;
+                const int li = n3b_lds(l);
+                sh.pj[0][li] = xj; sh.pj[0][li + 16] = xj;
+                sh.pj[1][li] = yj; sh.pj[1][li + 16] = yj;
+                sh.pj[2][li] = zj; sh.pj[2][li + 16] = zj;
+                if constexpr (FARF && MDQT_UFAR32) {
+                    const float x32 = (float)(xj - uniform_f64(xj)), y32 = (float)(yj - uniform_f64(yj)),
+                                z32 = (float)(zj - uniform_f64(zj));
+                    sh.pj32[0][li] = x32; sh.pj32[0][li + 16] = x32;
+                    sh.pj32[1][li] = y32; sh.pj32[1][li + 16] = y32;
+                    sh.pj32[2][li] = z32; sh.pj32[2][li + 16] = z32;
+                }
+                if (l < BW) {
+                    if (plan) {
+                        sh.pw[l] = plan[((size_t)(P - a.Plo) * a.nd + db) * (BW * BW) + b * BW + l];
+                    } else {
+                        int w = 2;
+                        if (srt && P * BW + l < T) {
+                            double g2;
+                            int sm = 0;
+                            w = n3b_pack_class(n3b_classify<VARIANT == 1>(a, c.invL, rad, P * BW + l, J, g2,
+                                                                          AXP ? &sm : nullptr), sm);
+                        }
+                        sh.pw[l] = make_uint2((unsigned)w, 0xFFu);
+                    }
+                }
+            }
+            __syncthreads();
+            const double (*pj)[128] = sh.pj;
+            const double* mj = sh.mjs[J == T - 1];
+#pragma unroll 1
+            for (int u = 0; u < 2; ++u) {            // the wave's two tile pairs (I_A, J), (I_B, J)
+                const int tI = u ? tB : tA;
+                const int I = P * BW + tI;
+                const int tw = __builtin_amdgcn_readfirstlane((int)sh.pw[tI].x);
+                const unsigned word = __builtin_amdgcn_readfirstlane(sh.pw[tI].y);
+                const bool mine = (u ? vB : vA) && (db > 0 || J >= I);
+                if (mine && (tw & 15) >= 2 && (word & 15u)) {
+                    double tx = 0., ty = 0., tz = 0.;
+                    n3b_tile_pair<VARIANT, GUARD, POT, AXP>(a, c, l, db == 0 && J == I, ragN && (I == T - 1 || J == T - 1),
+                                                            tw, word, u ? xB : xA, u ? yB : yA, u ? zB : zA,
+                                                            u ? mB : mA, pj, mj, sh.pj32, ax, ay, az, tx, ty, tz, cf32,
+                                                            invl32, rc2f);
+                    if (u) { bxB += tx; byB += ty; bzB += tz; }
+                    else { bxA += tx; byA += ty; bzA += tz; }
+                }
+            }
+            __syncthreads();
+            if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db: the 4 waves' two copies
+                const int l = lane_opaque(l0);
+                const int li = n3b_lds(l);
+                double s4[NWP];
+#pragma unroll
+                for (int w = 0; w < NWP; ++w) {
+                    s4[w] = sh.accj[w][q][li] + sh.accj[w][q][li + 16];
+                    sh.accj[w][q][li] = 0.;
+                    sh.accj[w][q][li + 16] = 0.;
+                }
+#pragma unroll
+                for (int h = NWP / 2; h >= 1; h /= 2)
+#pragma unroll
+                    for (int w = 0; w < h; ++w) s4[w] = s4[2 * w] + s4[2 * w + 1];
+                a.slots[(size_t)db * plane + (size_t)q * a.Npad + J * 64 + l] = POT ? s4[0] : -s4[0];
+            }
+        }
+        if (work) {                                 // this block distance's i sums into the run's, per tile
+            const int lo = lane_opaque(l0);
+            double* fa = sh.irun[tA][0] + lo;
+            fa[0] += bxA; fa[64] += byA; fa[128] += bzA;
+            double* fb = sh.irun[tB][0] + lo;
+            fb[0] += bxB; fb[64] += byB; fb[128] += bzB;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {                   // i side -> i-slot nd + run: tiles q and q + 4
+        const int tI = q + u * NWP, I = P * BW + tI;
+        if (I < T) {
+            const int lo = lane_opaque(l0);
+            const double* f = sh.irun[tI][0] + lo;
+            double* o = a.slots + (size_t)(a.nd + run) * plane + I * 64 + lo;
+            o[0] = f[0]; o[a.Npad] = f[64]; o[2 * (size_t)a.Npad] = f[128];
+        }
+    }
+}
 
 // force_tail_mode 1, after the call's per-sub-tile tail sums are complete (all-reduced over the
 // ranks when sharded): every tile with a sub-tile sum that, with the sum's rounding (x (1 + 1e-12)),
@@ -1182,6 +1411,71 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
             atomicAdd(bal + 1, mx);
             atomicAdd(bal + 2, 1ull);
         }
+        // schedules that move no work between waves (what a J-order change could reach): bal[3] the pairs
+        // of J steps (b, b + 1) each run as two sub-steps with every wave on one of the two J tiles, the
+        // best of the 256 choices; bal[4] the same pairs in lock-step; bal[5] per (P, db) the busiest
+        // wave's sum over its 8 J steps (any J order's floor)
+        const int lane = t & 63, base = lane & ~15;     // the pair's 16 costs: lanes base .. base + 15
+        unsigned long long c16[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c16[k] = __shfl(cost, base + k);
+        if (lane == base) {
+            unsigned long long cur = 0, m0 = 0, m1 = 0, best = ~0ull;
+            for (int k = 0; k < 8; ++k) { m0 = c16[k] > m0 ? c16[k] : m0; m1 = c16[8 + k] > m1 ? c16[8 + k] : m1; }
+            cur = m0 + m1;
+            for (unsigned S = 0; S < 256; ++S) {        // wave k in S: J step b first, b + 1 second
+                unsigned long long a1 = 0, a2 = 0;
+                for (int k = 0; k < 8; ++k) {
+                    const unsigned long long x = c16[k], y = c16[8 + k];
+                    const bool in = (S >> k) & 1u;
+                    const unsigned long long f = in ? x : y, g = in ? y : x;
+                    a1 = f > a1 ? f : a1;
+                    a2 = g > a2 ? g : a2;
+                }
+                best = a1 + a2 < best ? a1 + a2 : best;
+            }
+            if (cur) { atomicAdd(bal + 3, best); atomicAdd(bal + 4, cur); }
+        }
+        unsigned long long rw = cost;                   // wave q's sum over the workgroup's 8 J steps
+#pragma unroll
+        for (int off = BW; off < 64; off <<= 1) rw += __shfl_xor(rw, off);
+        __shared__ unsigned long long rws[BW];
+        if (lane < BW) rws[lane] = 0;
+        __syncthreads();
+        if (lane < BW) atomicAdd(&rws[lane], rw);
+        __syncthreads();
+        if (t == 0) {
+            unsigned long long m = 0;
+            for (int k = 0; k < BW; ++k) m = rws[k] > m ? rws[k] : m;
+            if (m) atomicAdd(bal + 5, m);
+        }
+        // 4 waves, each on two I tiles per J step (the pair's costs add): bal[6] the pairing of the heaviest
+        // row with the lightest (per (P, db)), bal[7] the fixed pairing (q, 7 - q), bal[8] (q, q + 4) — each
+        // the sum over J steps of 2 x the busiest wave's pair, comparable with bal[1]
+        unsigned long long c64[BW * BW];
+#pragma unroll
+        for (int k = 0; k < BW * BW; ++k) c64[k] = __shfl(cost, k);   // c64[q + 8 b]
+        if (t == 0) {
+            unsigned long long row[BW];
+            int ord[BW];
+            for (int k = 0; k < BW; ++k) { row[k] = 0; ord[k] = k; }
+            for (int b = 0; b < BW; ++b)
+                for (int k = 0; k < BW; ++k) row[k] += c64[k + BW * b];
+            for (int i = 1; i < BW; ++i)                // rows by cost, descending
+                for (int j = i; j > 0 && row[ord[j]] > row[ord[j - 1]]; --j) { const int x = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = x; }
+            unsigned long long hl = 0, fx = 0, f4 = 0;
+            for (int b = 0; b < BW; ++b) {
+                unsigned long long m1 = 0, m2 = 0, m3 = 0;
+                for (int k = 0; k < BW / 2; ++k) {
+                    const unsigned long long p1 = c64[ord[k] + BW * b] + c64[ord[BW - 1 - k] + BW * b];
+                    const unsigned long long p2 = c64[k + BW * b] + c64[BW - 1 - k + BW * b];
+                    const unsigned long long p3 = c64[k + BW * b] + c64[k + BW / 2 + BW * b];
+                    m1 = p1 > m1 ? p1 : m1; m2 = p2 > m2 ? p2 : m2; m3 = p3 > m3 ? p3 : m3;
+                }
+                hl += m1; fx += m2; f4 += m3;
+            }
+            if (hl) { atomicAdd(bal + 6, hl); atomicAdd(bal + 7, fx); atomicAdd(bal + 8, f4); }
+        }
     }
     __syncthreads();
     if (t < 2 * kCensus && h[t]) atomicAdd(out + t, h[t]);
@@ -1298,8 +1592,25 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
         for (int k = 0; k < per; ++k) mw |= ((wk >> (BW * k)) & ((1ull << BW) - 1)) ? 1u << k : 0u;
         atomicOr(&jm, mw << (per * (t >> 6)));
     }
+    // k_pairs_n3b_pw's pairing (.y of the J-step word): the tiles' estimated work over the 8 J steps (threads
+    // q, q + 8, ... hold tile q's tile pairs), the busiest tile with the least busy, and so on
+    const bool runs = !half && I < a.T && J < a.T && (db > 0 || J >= I);   // (the tile pairs the kernel runs)
+    unsigned rc = runs ? n3b_word_cost(w, (a.N & 63) && (I == a.T - 1 || J == a.T - 1), db == 0 && J == I) : 0u;
+#pragma unroll
+    for (int off = BW; off < 64; off <<= 1) rc += __shfl_xor(rc, off);
+    unsigned row[BW];
+#pragma unroll
+    for (int k = 0; k < BW; ++k) row[k] = __shfl(rc, k);
     __syncthreads();
-    if (t == 0) plan[(size_t)(a.Phi - a.Plo) * a.nd * (BW * BW) + (size_t)Pl * a.nd + db] = make_uint2(jm, 0u);
+    if (t == 0) {
+        int ord[BW];
+        for (int k = 0; k < BW; ++k) ord[k] = k;
+        for (int u = 1; u < BW; ++u)                // descending by work, ties by tile (deterministic)
+            for (int v = u; v > 0 && row[ord[v]] > row[ord[v - 1]]; --v) { const int x = ord[v]; ord[v] = ord[v - 1]; ord[v - 1] = x; }
+        unsigned pr = 0;
+        for (int k = 0; k < BW / 2; ++k) pr |= ((unsigned)ord[k] | (unsigned)ord[BW - 1 - k] << 3) << (6 * k);
+        plan[(size_t)(a.Phi - a.Plo) * a.nd * (BW * BW) + (size_t)Pl * a.nd + db] = make_uint2(jm, pr);
+    }
     // the reduction's per-J-tile masks: J step b has work -> the block kernel writes J's j-slot db
     if (a.tmask && t < BW && ((jm >> t) & 1u))
         atomicOr(a.tmask + (size_t)(Q * BW + t) * a.tmw + (db >> 6), 1ull << (db & 63));
@@ -1477,7 +1788,10 @@ hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStre
     if (hipError_t e = launch_n3b_plan(a, variant, s); e != hipSuccess) return e;
     if (marks && hipEventRecord(marks[0], s) != hipSuccess) return hipGetLastError();
     if (nblk > 0) {
-        if (variant == 1) {
+        if (variant == 1 && !a.guard && a.pairs) {   // the paired-wave kernel (option force_n3b_pairs)
+            if (n3b_axp(a)) launch_timed(k_pairs_n3b_pw<1, false, false, MDQT_N3B_AX1 != 0>, dim3(nblk), dim3(NWP * 64), s, ev0, ev1, a);
+            else launch_timed(k_pairs_n3b_pw<1, false>, dim3(nblk), dim3(NWP * 64), s, ev0, ev1, a);
+        } else if (variant == 1) {
             const bool axp = n3b_axp(a);
             if (a.guard) launch_timed(k_pairs_n3b<1, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
             else if (axp) launch_timed(k_pairs_n3b<1, false, false, MDQT_N3B_AX1 != 0>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, a);
@@ -1544,7 +1858,7 @@ hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStrea
     if (hipMemsetAsync(out, 0, 2 * kCensus * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
     if (bw && a.Phi > a.Plo && hipMemsetAsync(bw, 0, (size_t)(a.Phi - a.Plo) * sizeof(unsigned long long), s) != hipSuccess)
         return hipGetLastError();
-    if (bal && hipMemsetAsync(bal, 0, 3 * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
+    if (bal && hipMemsetAsync(bal, 0, 9 * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
     if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out, bw, bal);
     return hipGetLastError();
 }
@@ -1564,7 +1878,11 @@ hipError_t launch_potential_n3b(const N3BArgs& a, int variant, double* out, hipS
     N3BArgs r = a;
     if (!planned) { r.plan = nullptr; r.tmask = nullptr; }   // (no plan: every j-slot written, every one read)
     if (nblk > 0) {
-        if (variant == 1) {
+        if (variant == 1 && !a.guard && a.pairs) {   // the paired-wave kernel (option force_n3b_pairs)
+            if (planned && n3b_axp(a))
+                launch_timed(k_pairs_n3b_pw<1, false, true, MDQT_N3B_AX1 != 0>, dim3(nblk), dim3(NWP * 64), s, ev0, ev1, r);
+            else launch_timed(k_pairs_n3b_pw<1, false, true>, dim3(nblk), dim3(NWP * 64), s, ev0, ev1, r);
+        } else if (variant == 1) {
             if (a.guard) launch_timed(k_pairs_n3b<1, true, true>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, r);
             else if (planned && n3b_axp(a))
                 launch_timed(k_pairs_n3b<1, false, true, MDQT_N3B_AX1 != 0>, dim3(nblk), dim3(BW * 64), s, ev0, ev1, r);

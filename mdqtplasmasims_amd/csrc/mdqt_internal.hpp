@@ -424,6 +424,7 @@ struct N3BArgs {
     // spatial order (mdqt_sort.hip): tiles are 64 consecutive ions of the Hilbert order
     int use_sort;       // 1: positions from Rs, slots by sorted index, tile pairs beyond L/2 skipped;
                         // 2: the same order, nothing skipped (tests: bit-identical to 1)
+    int pairs;          // 1: the paired-wave block kernel (k_pairs_n3b_pw; option "force_n3b_pairs"), 0: k_pairs_n3b
     int ax1;            // 1: the one-axis per-pair image instance where the skip radius reaches the image
                         // boundary (launch_forces_n3b; option "force_ax1"), 0: every per-pair image on all axes
     const double* Rs;   // [3][Npad] positions in sorted order

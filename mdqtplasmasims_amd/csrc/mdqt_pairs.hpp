@@ -11,6 +11,9 @@ struct PairC {
     double L, T, G, Rcut, lDeb, invlDeb, invL;
     double rc2;         // VARIANT 2: pair kept iff r2 < rc2 (= sqrt(r2) < Rcut exactly)
     const double* etab; // the Newton-3 kernels' 2^(j/64) table in LDS (pair_ft_cut, MDQT_EXP_TAB)
+    // the tile kernel's box-scaled form (MDQT_N3_SCALED, n3_tile): positions s = x / L, so the minimum
+    // image is ds - rint(ds); sA = 1/L^2, sB = 1/(lDeb L), sT = 64 (-log2 e) L / lDeb
+    double sA, sB, sT;
 };
 
 // 2^t of the Newton-3 kernels' exact pair form by a 64-entry table (round 3, MDQT_EXP_TAB):
@@ -291,13 +294,33 @@ __device__ __forceinline__ LdsPJ lds_pj(const double (*pj)[128], int b) {   // c
 }
 __device__ __forceinline__ void lds_pj_opaque(LdsPJ& p) { asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z)); }
 
+// SC (the tile kernel's box-scaled form, MDQT_N3_SCALED): xi and the J tile hold x / L (rounded once at
+// load: a position perturbation within 1 ulp of the box, ~2.7e-15 at C2 — the positions' own storage
+// rounding); the minimum image ds - rint(ds) (2 operations per axis instead of 3), r_s = r / L, and the
+// force of the physical pair from ds: F = ds (ri_s / L^2 + 1 / (lDeb L)) e^(-r/lDeb) ri_s^2 — the same
+// operation count as the unscaled form, 3 VALU fewer per pair
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128]>
+          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128], bool SC = false>
 __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi, double zi, double mi,
                                          PJ pj, const double* mj, double& fx, double& fy,
                                          double& fz, const PairC& c, const double* nsh, double& px, double& py,
                                          double& pz) {
     double dx = xi - pj_at(pj, 0, idx), dy = yi - pj_at(pj, 1, idx), dz = zi - pj_at(pj, 2, idx);   // :213-215
+    if constexpr (SC) {
+        static_assert(VARIANT == 1 && CUT && !POT && !FAR && MAX < 0 && !SHIFT && MDQT_EXP_TAB, "the scaled tile form");
+        dx -= __builtin_rint(dx);                   // minimum image in box units (SpeedUp:218-220)
+        dy -= __builtin_rint(dy);
+        dz -= __builtin_rint(dz);
+        const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+        const double ri = rsq3(r2);
+        const double dr = r2 * ri;                  // r / L; the cutoff r < L/2 as r / L < 1/2
+        double ft = (fma(ri, c.sA, c.sB) * exp2_neg_cut_tab(dr * c.sT, dr < 0.5, c.etab)) * (ri * ri);
+        if (RAGGED) ft *= mi * mj[idx];
+        ft *= m;
+        px = dx * ft; py = dy * ft; pz = dz * ft;
+        fx += px; fy += py; fz += pz;
+        return;
+    }
     if constexpr (SHIFT) {
         if (!MDQT_SHIFT_I) {
             dx = fma(-nsh[0], c.L, dx);             // = mic_r's fma(-rint(dx / L), L, dx)
@@ -341,13 +364,13 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
 // (ds_add_f64 at index idx, no return; one wave's LDS operations run in order, so the
 // accumulation order is fixed)
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128]>
+          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128], bool SC = false>
 __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi, double zi, double mi,
                                         PJ pj, const double* mj, double* ax, double* ay,
                                         double* az, double& fx, double& fy, double& fz, const PairC& c,
                                         const double* nsh = nullptr) {
     double px, py, pz;
-    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX, PJ>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh, px,
+    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX, PJ, SC>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh, px,
                                                                 py, pz);
 #if defined(MDQT_EXPT_NOJACC)
     (void)ax; (void)ay; (void)az;
@@ -396,6 +419,9 @@ __device__ __forceinline__ void slot_store(double* p, double v) {
 #ifndef MDQT_N3_CUT
 #define MDQT_N3_CUT 1
 #endif
+#ifndef MDQT_N3_SCALED
+#define MDQT_N3_SCALED 1                            // the tile kernel's box-scaled force form (n3_terms SC); A/B round 6: C2 force launch -4 %
+#endif
 #ifndef MDQT_N3_PRIO
 #define MDQT_N3_PRIO 0
 #endif
@@ -416,12 +442,22 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     const double* X = a.R;
     const double* Y = a.R + S;
     const double* Z = a.R + 2 * S;
+    // the box-scaled force form (MDQT_N3_SCALED): positions in box units from the load on
+    constexpr bool SC = MDQT_N3_SCALED && VARIANT == 1 && CUT && !POT && !GUARD && MDQT_EXP_TAB;
+    const double sc = SC ? c.invL : 1.;
+    PairC cs = c;
+    if constexpr (SC) {
+        cs.sA = c.invL * c.invL;
+        cs.sB = c.invlDeb * c.invL;
+        cs.sT = c.L * (c.invlDeb * (64. * kNegLog2e));
+    }
     if (q == 0) {                                   // stage the J tile (twice over)
         const int j = J * 64 + l;
         const bool vj = !RAGGED || j < N;
         // pad ions (ragged last tile): distinct points (pad-pad pairs must have r > 0), weight 0
         const double pad = (double)(l + 1) * 0x1p-10;
-        const double xj = vj ? X[j] : pad, yj = vj ? Y[j] : pad, zj = vj ? Z[j] : pad;
+        double xj = vj ? X[j] : pad, yj = vj ? Y[j] : pad, zj = vj ? Z[j] : pad;
+        if constexpr (SC) { xj *= sc; yj *= sc; zj *= sc; }
         pj[0][l] = xj; pj[0][l + 64] = xj;
         pj[1][l] = yj; pj[1][l + 64] = yj;
         pj[2][l] = zj; pj[2][l + 64] = zj;
@@ -432,7 +468,8 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     const int i = I * 64 + l;
     const bool vi = !RAGGED || i < N;
     const double padi = (double)(l + 1) * 0x1p-10;
-    const double xi = vi ? X[i] : padi, yi = vi ? Y[i] : padi, zi = vi ? Z[i] : padi;
+    double xi = vi ? X[i] : padi, yi = vi ? Y[i] : padi, zi = vi ? Z[i] : padi;
+    if constexpr (SC) { xi *= sc; yi *= sc; zi *= sc; }
     const double mi = vi ? 1. : 0.;
     __syncthreads();
     double fx = 0., fy = 0., fz = 0.;
@@ -447,11 +484,12 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     auto step = [&](int idx, double m) {
         if constexpr (MDQT_LDS_SPLIT) {             // (the LDS bases opaque per step: ds_read_b64, no read2)
             lds_pj_opaque(pb);
-            n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT, 0, -1, LdsPJ>(idx - pbase, m, xi, yi, zi, mi, pb,
-                                                                          mj + pbase, ax + pbase, ay + pbase,
-                                                                          az + pbase, fx, fy, fz, c);
+            n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT, 0, -1, LdsPJ, SC>(idx - pbase, m, xi, yi, zi, mi, pb,
+                                                                              mj + pbase, ax + pbase, ay + pbase,
+                                                                              az + pbase, fx, fy, fz, cs);
         } else {
-            n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT>(idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, c);
+            n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT, 0, -1, const double (*)[128], SC>(
+                idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, cs);
         }
     };
     const bool diag = I == J;

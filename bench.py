@@ -893,7 +893,10 @@ def end_to_end_line(local, cfg, md_steps, base=40, warm=True):
 # the large-N dominant kernel: its plain instance, or (C3, C5: the skip radius reaches the image
 # boundary) the one with the one-axis per-pair image (mdqt_forces.hip launch_forces_n3b)
 N3B_KERNELS = ("void mdqt::k_pairs_n3b<1, false, false, false>(mdqt::N3BArgs)",
-               "void mdqt::k_pairs_n3b<1, false, false, true>(mdqt::N3BArgs)")
+               "void mdqt::k_pairs_n3b<1, false, false, true>(mdqt::N3BArgs)",
+               # the paired-wave kernel (option force_n3b_pairs, round 6)
+               "void mdqt::k_pairs_n3b_pw<1, false, false, false>(mdqt::N3BArgs)",
+               "void mdqt::k_pairs_n3b_pw<1, false, false, true>(mdqt::N3BArgs)")
 N3B_KERNEL = N3B_KERNELS[0]
 
 
@@ -904,7 +907,7 @@ def latest_large_pmc(cfg):
     return os.path.join(d, fs[-1]) if fs else None
 
 
-def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None):
+def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None, pairs=0):
     """Roofline of a large line's dominant kernel, k_pairs_n3b.  VALU is the roof (30 flop per
     distinct pair, ~0 B per pair after staging).  `frac` is the block kernel's own rate on the pairs it
     evaluates, time-weighted over its two precisions: 30 flop x
@@ -929,7 +932,7 @@ def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None):
     peak = W_F_PER_PAIR * ev / (t64 + t32) / 1e12 if ev else FP64_PEAK_TFS * world
     peak64 = FP64_PEAK_TFS * world
     t = k_avg if k_avg else f_avg
-    roof = {"bound": "fp64+fp32" if ev32 else "fp64", "kernel": N3B_KERNEL, "unit": "TFLOP/s", "peak": peak,
+    roof = {"bound": "fp64+fp32" if ev32 else "fp64", "kernel": N3B_KERNELS[2 if pairs else 0], "unit": "TFLOP/s", "peak": peak,
             "achieved": W_F_PER_PAIR * ev / t / 1e12, "frac": (t64 + t32) / t,
             "fp64_pairs_frac": ev64 / ev if ev else None, "f32_pairs_frac": ev32 / ev if ev else None,
             "fp64_frac": t64 / t, "f32_frac": t32 / t,
@@ -1036,6 +1039,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     N = sim.N
     L = sim.const("L")
     rt, tail = sim.const("force_skip_radius"), sim.const("force_tail_bound")
+    n3b_pairs = int(sim.const("force_n3b_pairs"))   # the paired-wave block kernel (k_pairs_n3b_pw) or the 8-wave one
     tmode, tmodel = int(sim.const("force_tail_mode")), sim.const("force_tail_model_bound")
     fixed, raw = sim.const("force_tail_fixed_tiles"), sim.const("force_tail_raw_bound")
     rm, mid = sim.const("force_mid_radius"), sim.const("force_mid_bound")
@@ -1124,7 +1128,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "unit": "particle-qsteps/s" if qt else "particle-MD-steps/s",
             "scaling": "strong", "init_s": t_init, "force": force, "force_breakdown_ms": breakdown,
             "epotential": epotential,
-            "roofline": large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance) if census and f_avg else None,
+            "roofline": large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance, n3b_pairs) if census and f_avg else None,
             "parity": parity if check else {"note": "world 1: this line is the reference the sharded runs are checked against"},
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail, "bound_met": bound_met,
                            "tail_mode": "measured+enforced" if tmode == 1 else "a priori",

@@ -91,7 +91,7 @@ struct mdqt_ctx {
     double* dUpart = nullptr;      // potential-row partials of its own (small systems, world 1)
     int n3_potential = 1;          // option "potential_n3": 1 = Newton-3 tiles where the forces use them
 #ifndef MDQT_N3B_PAIRS_DEFAULT
-#define MDQT_N3B_PAIRS_DEFAULT 0
+#define MDQT_N3B_PAIRS_DEFAULT 1                  // A/B round 6 (r06e): N = 1M force call -4.3 %, C5 -2.3 %, C3 -2.3 %
 #endif
     int n3b_pairs = MDQT_N3B_PAIRS_DEFAULT;   // option "force_n3b_pairs": the paired-wave block kernel (k_pairs_n3b_pw)
     int pot_plan = 1;              // option "potential_plan": 1 = Epotential on the blocks takes the force call's

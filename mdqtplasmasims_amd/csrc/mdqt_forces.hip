@@ -992,21 +992,12 @@ void k_pairs_n3b(N3BArgs a) {
 // without a plan the fixed pairing (k, 7 - k)
 constexpr unsigned kN3BPairsDefault = (0u | 7u << 3) | (1u | 6u << 3) << 6 | (2u | 5u << 3) << 12 | (3u | 4u << 3) << 18;
 static_assert(BW == 8, "the paired-wave pairing word holds 8 tiles");
-// a tile pair's estimated VALU instructions per lane (the pairing's weights: per wave-step of each pair
-// form — exact, mid, far, very far, ultra far, f32 ultra far — uniform / per-pair image; the ragged
-// tile's exact form) from its plan word (class, sub-tile groups by level)
-__device__ __forceinline__ unsigned n3b_word_cost(uint2 w, bool rag, bool diag) {
-    const int cls = (int)(w.x & 15u) - 2;
-    const unsigned groups = w.y & 15u;
-    if (cls < 0 || !groups) return 0u;
-    const bool uni = cls & 1;
-    if (rag) return 52u * (diag ? 40u : 16u * __builtin_popcount(groups));
-    if (diag) return (uni ? 39u : 48u) * 40u;
+// a sub-tile group's estimated VALU instructions per lane (16 steps; the pairing's weights per wave-step of
+// each pair form — exact, mid, far, very far, ultra far, f32 ultra far — uniform image / per-pair image; the
+// ragged tile's exact form)
+__device__ __forceinline__ unsigned n3b_pair_cost(int level, bool uni, bool rag) {
     constexpr unsigned wu[6] = {39u, 36u, 31u, 27u, 25u, 9u}, wi[6] = {48u, 44u, 38u, 32u, 32u, 32u};
-    unsigned c = 0;
-#pragma unroll
-    for (int x = 0; x < 6; ++x) c += 16u * (uni ? wu[x] : wi[x]) * __builtin_popcount(level_groups(w.y, x));
-    return c;
+    return 16u * (rag ? 52u : uni ? wu[level] : wi[level]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1516,6 +1507,9 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
     uint2 w = make_uint2(1u, 0xFFu);                // class -1 where the block kernel never looks
     double gi[4] = {0., 0., 0., 0.}, gj[4] = {0., 0., 0., 0.};   // this tile pair's tail terms per sub-tile
     const bool half = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
+    // the paired-wave kernel's work estimate of this tile pair (n3b_pair_cost: from the geometry alone, the
+    // same with force_sort 1 and 2, so that both take the same pairing and stay bit-identical)
+    unsigned cest = 0;
     if (!half && I < a.T && J < a.T && (db > 0 || J >= I)) {
         const N3BRadii rad = n3b_radii<VARIANT, false>(a);
         const double invL = 1. / a.L;
@@ -1524,6 +1518,9 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
         const int pw = n3b_pack_class(n3b_classify<VARIANT == 1>(a, invL, rad, I, J, g2, &sm), VARIANT == 1 ? sm : 0);
         const int cls = (pw & 15) - 2;
         w.x = (unsigned)pw;
+        const bool rag = (a.N & 63) && (I == a.T - 1 || J == a.T - 1);
+        const bool uni = cls >= 0 && (cls & 1);
+        if (db == 0 && J == I && !(g2 > rad.rc2)) cest = (rag ? 52u : uni ? 39u : 48u) * 40u;
         if ((db > 0 || J > I) && (cls >= 0 || (tmeas && cls == -2))) {
             const int T4 = 4 * a.T;
             double sg[4][4];
@@ -1542,9 +1539,10 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
             const double hj4 = FARF && gmax > rad.ru32 ? 4. * raw_half2(a.boxes, a.T, J) : 0.;
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
+                int x = !FARF ? 0 : n3b_level(gm[d], rad);
+                if (x == 5 && !(gm[d] > hj4)) x = 4;
+                if (gm[d] <= rad.rc2 && !(g2 > rad.rc2)) cest += n3b_pair_cost(x, uni, rag);
                 if (a.use_sort != 1 || gm[d] <= rad.rc2) {
-                    int x = !FARF ? 0 : n3b_level(gm[d], rad);
-                    if (x == 5 && !(gm[d] > hj4)) x = 4;
                     groups |= 1u << d;
                     lvm |= 1u << (4 * x + d);
                 }
@@ -1594,8 +1592,7 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
     }
     // k_pairs_n3b_pw's pairing (.y of the J-step word): the tiles' estimated work over the 8 J steps (threads
     // q, q + 8, ... hold tile q's tile pairs), the busiest tile with the least busy, and so on
-    const bool runs = !half && I < a.T && J < a.T && (db > 0 || J >= I);   // (the tile pairs the kernel runs)
-    unsigned rc = runs ? n3b_word_cost(w, (a.N & 63) && (I == a.T - 1 || J == a.T - 1), db == 0 && J == I) : 0u;
+    unsigned rc = cest;
 #pragma unroll
     for (int off = BW; off < 64; off <<= 1) rc += __shfl_xor(rc, off);
     unsigned row[BW];

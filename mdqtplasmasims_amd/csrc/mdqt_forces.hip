@@ -1454,9 +1454,18 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                 for (int k = 0; k < BW; ++k) row[k] += c64[k + BW * b];
             for (int i = 1; i < BW; ++i)                // rows by cost, descending
                 for (int j = i; j > 0 && row[ord[j]] > row[ord[j - 1]]; --j) { const int x = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = x; }
-            unsigned long long hl = 0, fx = 0, f4 = 0;
+            unsigned long long hl = 0, fx = 0, f4 = 0, ps = 0;
             for (int b = 0; b < BW; ++b) {
-                unsigned long long m1 = 0, m2 = 0, m3 = 0;
+                unsigned long long m1 = 0, m2 = 0, m3 = 0, m4 = 0;
+                int os[BW];                             // this J step's own heavy-light pairing (bal[9])
+                for (int k = 0; k < BW; ++k) os[k] = k;
+                for (int i = 1; i < BW; ++i)
+                    for (int j = i; j > 0 && c64[os[j] + BW * b] > c64[os[j - 1] + BW * b]; --j) { const int x = os[j]; os[j] = os[j - 1]; os[j - 1] = x; }
+                for (int k = 0; k < BW / 2; ++k) {
+                    const unsigned long long p4 = c64[os[k] + BW * b] + c64[os[BW - 1 - k] + BW * b];
+                    m4 = p4 > m4 ? p4 : m4;
+                }
+                ps += m4;
                 for (int k = 0; k < BW / 2; ++k) {
                     const unsigned long long p1 = c64[ord[k] + BW * b] + c64[ord[BW - 1 - k] + BW * b];
                     const unsigned long long p2 = c64[k + BW * b] + c64[BW - 1 - k + BW * b];
@@ -1465,7 +1474,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                 }
                 hl += m1; fx += m2; f4 += m3;
             }
-            if (hl) { atomicAdd(bal + 6, hl); atomicAdd(bal + 7, fx); atomicAdd(bal + 8, f4); }
+            if (hl) { atomicAdd(bal + 6, hl); atomicAdd(bal + 7, fx); atomicAdd(bal + 8, f4); atomicAdd(bal + 9, ps); }
         }
     }
     __syncthreads();
@@ -1855,7 +1864,7 @@ hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStrea
     if (hipMemsetAsync(out, 0, 2 * kCensus * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
     if (bw && a.Phi > a.Plo && hipMemsetAsync(bw, 0, (size_t)(a.Phi - a.Plo) * sizeof(unsigned long long), s) != hipSuccess)
         return hipGetLastError();
-    if (bal && hipMemsetAsync(bal, 0, 9 * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
+    if (bal && hipMemsetAsync(bal, 0, 10 * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
     if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out, bw, bal);
     return hipGetLastError();
 }

@@ -1677,8 +1677,8 @@ extern "C" int mdqt_force_jstep_balance(mdqt_ctx* s, double* out, int n) {
     N3BArgs a;
     if (n3b_args(s, a)) return -1;
     unsigned long long* d = nullptr;
-    unsigned long long h[10];
-    HIPCHK(hipMalloc(&d, (2 * kCensus + 10) * sizeof(unsigned long long)));
+    unsigned long long h[11];
+    HIPCHK(hipMalloc(&d, (2 * kCensus + 11) * sizeof(unsigned long long)));
     hipError_t e = launch_n3b_census(a, d, s->stream, nullptr, d + 2 * kCensus);
     if (e == hipSuccess) e = hipMemcpyAsync(h, d + 2 * kCensus, sizeof h, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
@@ -1690,6 +1690,7 @@ extern "C" int mdqt_force_jstep_balance(mdqt_ctx* s, double* out, int n) {
     // 4 x the sum over J steps of the busiest wave's pair)
     if (n >= 9) { out[6] = 4. * (double)h[6]; out[7] = 4. * (double)h[7]; out[8] = 4. * (double)h[8]; }
     if (n >= 10) out[9] = 4. * (double)h[9];       // each J step paired heavy-light on its own
+    if (n >= 11) out[10] = 4. * (double)h[10];     // the best of the 105 pairings per (P, db)
     return 0;
 }
 

@@ -260,6 +260,18 @@ __device__ __forceinline__ void n3b_group(int b0, double w, double xi, double yi
                                           double* az, double& fx, double& fy, double& fz, const PairC& c,
                                           const double* nsh, double w_last = 1.) {
     N3B_REBASE(b0);
+    if constexpr (MDQT_N3_DEFER_J) {
+        // the j side one step late (n3_step_defer): each step's LDS reads queue behind the previous
+        // step's atomics only one step later — the same adds in the same order, bit for bit
+        double qx = 0., qy = 0., qz = 0.;
+#pragma unroll
+        for (int t = 0; t < NSTEP; ++t)
+            n3_step_defer<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX>(t, t == NSTEP - 1 ? w * w_last : w, xi, yi, zi,
+                                                                             mi, pjb, mjb, axb, ayb, azb, fx, fy, fz, c,
+                                                                             nsh, t - 1, qx, qy, qz);
+        n3_j_add<POT>(NSTEP - 1, axb, ayb, azb, qx, qy, qz);
+        return;
+    }
     LdsPJ p = lds_pj(pjb, 0);
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) {
@@ -325,7 +337,7 @@ __device__ __forceinline__ float row_rol2f(float v) {   // lane 16 a + m <- lane
 }
 // two rotation steps per v_pk_* instruction (MDQT_UF32_PK 1): gfx950 runs a packed f32 operation at half
 // the rate of a scalar one (tools/ubench_f64: the same VALU cycles per pair) but issues half the
-// instructions — A/B round 5 (tools/gpu/r05_uf32.sh): C4 force call 244.8 ms packed, 248.3 scalar,
+// instructions — A/B round 5 (profiles/r05h_uf32_force_ab.txt): C4 force call 244.8 ms packed, 248.3 scalar,
 // 254.1 with the round-4 form (f64 separations); N = 1M 198.0 / 200.3 / 205.3.  0: one step at a time
 #ifndef MDQT_UF32_PK
 #define MDQT_UF32_PK 1
@@ -992,6 +1004,8 @@ void k_pairs_n3b(N3BArgs a) {
 // without a plan the fixed pairing (k, 7 - k)
 constexpr unsigned kN3BPairsDefault = (0u | 7u << 3) | (1u | 6u << 3) << 6 | (2u | 5u << 3) << 12 | (3u | 4u << 3) << 18;
 static_assert(BW == 8, "the paired-wave pairing word holds 8 tiles");
+// the 105 pairings of 8 tiles (pairing words as kN3BPairsDefault)
+__constant__ const unsigned kN3BMatchings[105] = {0xfac688, 0xf74688, 0xd7c688, 0xfab888, 0xf73888, 0xd7b888, 0xfa3a88, 0xf33a88, 0xd3ba88, 0xf63c88, 0xf2bc88, 0xb3bc88, 0xd63e88, 0xd2be88, 0xb33e88, 0xfac650, 0xf74650, 0xd7c650, 0xfab850, 0xf73850, 0xd7b850, 0xfa3a50, 0xf33a50, 0xd3ba50, 0xf63c50, 0xf2bc50, 0xb3bc50, 0xd63e50, 0xd2be50, 0xb33e50, 0xfac458, 0xf74458, 0xd7c458, 0xfaa858, 0xf72858, 0xd7a858, 0xfa2a58, 0xf32a58, 0xd3aa58, 0xf62c58, 0xf2ac58, 0xb3ac58, 0xd62e58, 0xd2ae58, 0xb32e58, 0xfab460, 0xf73460, 0xd7b460, 0xfaa660, 0xf72660, 0xd7a660, 0xf9aa60, 0xef2a60, 0xcfaa60, 0xf5ac60, 0xeeac60, 0xafac60, 0xd5ae60, 0xceae60, 0xaf2e60, 0xfa3468, 0xf33468, 0xd3b468, 0xfa2668, 0xf32668, 0xd3a668, 0xf9a868, 0xef2868, 0xcfa868, 0xf1ac68, 0xee2c68, 0x8fac68, 0xd1ae68, 0xce2e68, 0x8f2e68, 0xf63470, 0xf2b470, 0xb3b470, 0xf62670, 0xf2a670, 0xb3a670, 0xf5a870, 0xeea870, 0xafa870, 0xf1aa70, 0xee2a70, 0x8faa70, 0xb1ae70, 0xae2e70, 0x8eae70, 0xd63478, 0xd2b478, 0xb33478, 0xd62678, 0xd2a678, 0xb32678, 0xd5a878, 0xcea878, 0xaf2878, 0xd1aa78, 0xce2a78, 0x8f2a78, 0xb1ac78, 0xae2c78, 0x8eac78};
 // a sub-tile group's estimated VALU instructions per lane (16 steps; the pairing's weights per wave-step of
 // each pair form — exact, mid, far, very far, ultra far, f32 ultra far — uniform image / per-pair image; the
 // ragged tile's exact form)
@@ -1131,7 +1145,9 @@ void k_pairs_n3b_pw(N3BArgs a) {
                     }
                 }
             }
+#if !defined(MDQT_EXPT_NOBAR)                       // (diagnostic build: no J-step barriers, wrong results)
             __syncthreads();
+#endif
             const double (*pj)[128] = sh.pj;
             const double* mj = sh.mjs[J == T - 1];
 #pragma unroll 1
@@ -1151,7 +1167,9 @@ void k_pairs_n3b_pw(N3BArgs a) {
                     else { bxA += tx; byA += ty; bzA += tz; }
                 }
             }
+#if !defined(MDQT_EXPT_NOBAR)
             __syncthreads();
+#endif
             if (q < (POT ? 1 : 3)) {                // j side of J's rows -> j-slot db: the 4 waves' two copies
                 const int l = lane_opaque(l0);
                 const int li = n3b_lds(l);
@@ -1474,7 +1492,21 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                 }
                 hl += m1; fx += m2; f4 += m3;
             }
-            if (hl) { atomicAdd(bal + 6, hl); atomicAdd(bal + 7, fx); atomicAdd(bal + 8, f4); atomicAdd(bal + 9, ps); }
+            unsigned long long bm = ~0ull;          // the best of the 105 pairings of this (P, db) (bal[10])
+            for (int m = 0; m < 105; ++m) {
+                const unsigned pw = kN3BMatchings[m];
+                unsigned long long cm = 0;
+                for (int b = 0; b < BW; ++b) {
+                    unsigned long long mx = 0;
+                    for (int k = 0; k < BW / 2; ++k) {
+                        const unsigned long long v = c64[((pw >> (6 * k)) & 7) + BW * b] + c64[((pw >> (6 * k + 3)) & 7) + BW * b];
+                        mx = v > mx ? v : mx;
+                    }
+                    cm += mx;
+                }
+                bm = cm < bm ? cm : bm;
+            }
+            if (hl) { atomicAdd(bal + 6, hl); atomicAdd(bal + 7, fx); atomicAdd(bal + 8, f4); atomicAdd(bal + 9, ps); atomicAdd(bal + 10, bm); }
         }
     }
     __syncthreads();
@@ -1864,7 +1896,7 @@ hipError_t launch_n3b_census(const N3BArgs& a, unsigned long long* out, hipStrea
     if (hipMemsetAsync(out, 0, 2 * kCensus * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
     if (bw && a.Phi > a.Plo && hipMemsetAsync(bw, 0, (size_t)(a.Phi - a.Plo) * sizeof(unsigned long long), s) != hipSuccess)
         return hipGetLastError();
-    if (bal && hipMemsetAsync(bal, 0, 10 * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
+    if (bal && hipMemsetAsync(bal, 0, 11 * sizeof(unsigned long long), s) != hipSuccess) return hipGetLastError();
     if (nblk > 0) hipLaunchKernelGGL(k_n3b_census, dim3(nblk), dim3(BW * BW), 0, s, a, out, bw, bal);
     return hipGetLastError();
 }

@@ -41,31 +41,41 @@ static __constant__ const double kExp2Tab64[64] = {
     0x1.d5818dcfba487p+0, 0x1.da9e603db3285p+0, 0x1.dfc97337b9b5fp+0, 0x1.e502ee78b3ff6p+0,
     0x1.ea4afa2a490dap+0, 0x1.efa1bee615a27p+0, 0x1.f50765b6e4540p+0, 0x1.fa7c1819e90d8p+0,
 };
-__device__ __forceinline__ double exp2_neg_cut_tab(double t64, bool keep, const double* tab) {
+// (cb: called right after the table read is issued — the deferred j side's atomics, n3_step_defer)
+struct NoCb {
+    __device__ __forceinline__ void operator()() const {}
+};
+template <typename CB = NoCb>
+__device__ __forceinline__ double exp2_neg_cut_tab(double t64, bool keep, const double* tab, CB cb = {}) {
     const double m = __builtin_rint(t64);
     const double g = t64 - m;
     const int mi = (int)m;
+    const double te = tab[mi & 63];
+    cb();
     double p = 0x1.5d87fe78a6731p-40;
     p = fma(p, g, 0x1.3b2ab6fba4e77p-31);
     p = fma(p, g, 0x1.c6b08d704a0c0p-23);
     p = fma(p, g, 0x1.ebfbdff82c58fp-15);
     p = fma(p, g, 0x1.62e42fefa39efp-7);
     p = fma(p, g, 1.0);
-    return ldexp(p * tab[mi & 63], keep ? (mi >> 6) : -1100);
+    return ldexp(p * te, keep ? (mi >> 6) : -1100);
 }
 // the mid tier's 2^t (Newton-3 blocks, pairs >= r_mid apart): the same table times a degree-4 fit of
 // 2^(g/64) on g in [-1/2, 1/2] (Chebyshev interpolation in long double, coefficients rounded to double;
 // 2.53e-15 relative in double Horner, measured on 200,001 points) — one FMA fewer (kTab4RelErr)
-__device__ __forceinline__ double exp2_neg_cut_tab4(double t64, bool keep, const double* tab) {
+template <typename CB = NoCb>
+__device__ __forceinline__ double exp2_neg_cut_tab4(double t64, bool keep, const double* tab, CB cb = {}) {
     const double m = __builtin_rint(t64);
     const double g = t64 - m;
     const int mi = (int)m;
+    const double te = tab[mi & 63];
+    cb();
     double p = 0x1.3b2ad028fa84ap-31;
     p = fma(p, g, 0x1.c6b0c40d96fd0p-23);
     p = fma(p, g, 0x1.ebfbdff82ac88p-15);
     p = fma(p, g, 0x1.62e42fefa0352p-7);
     p = fma(p, g, 1.0);
-    return ldexp(p * tab[mi & 63], keep ? (mi >> 6) : -1100);
+    return ldexp(p * te, keep ? (mi >> 6) : -1100);
 }
 // stage the table (threads 0..63 of the workgroup; before the kernel's first barrier)
 __device__ __forceinline__ void stage_exp_tab(double* etab) {
@@ -151,24 +161,27 @@ __device__ __forceinline__ double pair_u(double dx, double dy, double dz, const 
 // The fast variant for the Newton-3 tile kernels (no self pairs; pad ions at distinct points):
 // pair_ft<1> with the cutoff folded into the 2^t exponent shift (exp2_neg_cut: one 32-bit select
 // instead of a 64-bit select of the result; r = 0 must not occur).  Same values as pair_ft<1>.
-__device__ __forceinline__ double pair_ft_cut(double dx, double dy, double dz, const PairC& c) {
+template <typename CB = NoCb>
+__device__ __forceinline__ double pair_ft_cut(double dx, double dy, double dz, const PairC& c, CB cb = {}) {
     const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
     const double ri = rsq3(r2);
     const double dr = r2 * ri;
     if constexpr (MDQT_EXP_TAB)
-        return ((ri + c.invlDeb) * exp2_neg_cut_tab(dr * (c.invlDeb * (64. * kNegLog2e)), dr < c.Rcut, c.etab)) *
+        return ((ri + c.invlDeb) * exp2_neg_cut_tab(dr * (c.invlDeb * (64. * kNegLog2e)), dr < c.Rcut, c.etab, cb)) *
                (ri * ri);
+    cb();
     return ((ri + c.invlDeb) * exp2_neg_cut(dr * (c.invlDeb * kNegLog2e), dr < c.Rcut)) * (ri * ri);
 }
 
 // pair_ft_cut of a mid-range sub-tile group (Newton-3 blocks, gap >= r_mid; MDQT_EXP_TAB): rsq1 and
 // the table's 2^t with the degree-4 series — a term within (r/lDeb + 3)(kRsq1RelErr + 2^-52) +
 // kTab4RelErr of itself; the cutoff on the f64 r^2 (rsq1's r carries 2e-14: pairs at L/2 would flip)
-__device__ __forceinline__ double pair_ft_cut_mid(double dx, double dy, double dz, const PairC& c) {
+template <typename CB = NoCb>
+__device__ __forceinline__ double pair_ft_cut_mid(double dx, double dy, double dz, const PairC& c, CB cb = {}) {
     const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
     const double ri = rsq1(r2);
     const double dr = r2 * ri;
-    return ((ri + c.invlDeb) * exp2_neg_cut_tab4(dr * (c.invlDeb * (64. * kNegLog2e)), r2 < c.rc2, c.etab)) *
+    return ((ri + c.invlDeb) * exp2_neg_cut_tab4(dr * (c.invlDeb * (64. * kNegLog2e)), r2 < c.rc2, c.etab, cb)) *
            (ri * ri);
 }
 
@@ -300,12 +313,16 @@ __device__ __forceinline__ void lds_pj_opaque(LdsPJ& p) { asm volatile("" : "+v"
 // force of the physical pair from ds: F = ds (ri_s / L^2 + 1 / (lDeb L)) e^(-r/lDeb) ri_s^2 — the same
 // operation count as the unscaled form, 3 VALU fewer per pair
 template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
-          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128], bool SC = false>
+          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128], bool SC = false, typename CB = NoCb>
 __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi, double zi, double mi,
                                          PJ pj, const double* mj, double& fx, double& fy,
                                          double& fz, const PairC& c, const double* nsh, double& px, double& py,
-                                         double& pz) {
+                                         double& pz, CB cb = {}) {
+    // cb (n3_step_defer): after this step's LDS reads are issued — the 2^t table's read in the forms that
+    // have one, the J positions' otherwise
+    constexpr bool TAB = MDQT_EXP_TAB && !POT && (SC || FAR == 1 || (FAR == 0 && CUT));
     double dx = xi - pj_at(pj, 0, idx), dy = yi - pj_at(pj, 1, idx), dz = zi - pj_at(pj, 2, idx);   // :213-215
+    if constexpr (!TAB) cb();
     if constexpr (SC) {
         static_assert(VARIANT == 1 && CUT && !POT && !FAR && MAX < 0 && !SHIFT && MDQT_EXP_TAB, "the scaled tile form");
         dx -= __builtin_rint(dx);                   // minimum image in box units (SpeedUp:218-220)
@@ -314,7 +331,7 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
         const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
         const double ri = rsq3(r2);
         const double dr = r2 * ri;                  // r / L; the cutoff r < L/2 as r / L < 1/2
-        double ft = (fma(ri, c.sA, c.sB) * exp2_neg_cut_tab(dr * c.sT, dr < 0.5, c.etab)) * (ri * ri);
+        double ft = (fma(ri, c.sA, c.sB) * exp2_neg_cut_tab(dr * c.sT, dr < 0.5, c.etab, cb)) * (ri * ri);
         if (RAGGED) ft *= mi * mj[idx];
         ft *= m;
         px = dx * ft; py = dy * ft; pz = dz * ft;
@@ -352,8 +369,8 @@ __device__ __forceinline__ void n3_terms(int idx, double m, double xi, double yi
     double ft = FAR == 4 ? pair_ft_cut_ufar(dx, dy, dz, c)
               : FAR == 3 ? pair_ft_cut_vfar(dx, dy, dz, c)
               : FAR == 2 ? pair_ft_cut_far(dx, dy, dz, c)
-              : FAR == 1 ? pair_ft_cut_mid(dx, dy, dz, c)
-              : CUT ? pair_ft_cut(dx, dy, dz, c) : pair_ft<VARIANT>(dx, dy, dz, c);
+              : FAR == 1 ? pair_ft_cut_mid(dx, dy, dz, c, cb)
+              : CUT ? pair_ft_cut(dx, dy, dz, c, cb) : pair_ft<VARIANT>(dx, dy, dz, c);
     if (RAGGED) ft *= mi * mj[idx];
     ft *= m;
     px = dx * ft; py = dy * ft; pz = dz * ft;
@@ -381,6 +398,42 @@ __device__ __forceinline__ void n3_step(int idx, double m, double xi, double yi,
         __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 #endif
+}
+
+// the j-side atomics of one step (n3_step's, split out for the deferred form)
+template <bool POT>
+__device__ __forceinline__ void n3_j_add(int idx, double* ax, double* ay, double* az, double px, double py, double pz) {
+#if defined(MDQT_EXPT_NOJACC)
+    (void)idx; (void)ax; (void)ay; (void)az; (void)px; (void)py; (void)pz;
+#else
+    __hip_atomic_fetch_add(&ax[idx], px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if constexpr (!POT) {
+        __hip_atomic_fetch_add(&ay[idx], py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(&az[idx], pz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+#endif
+}
+// MDQT_N3_DEFER_J: one rotation step with its j side one step late — the pair terms of step idx, then the
+// previous step's j terms (q*, at index qidx >= 0) to LDS, and this step's kept in q* for the next.  A
+// wave's LDS operations complete in order, so the next step's position and table reads wait behind the
+// atomics issued before them; deferred, those atomics are a step older.  The same adds in the same order
+// per accumulator entry: bit for bit n3_step.
+#ifndef MDQT_N3_DEFER_J
+#define MDQT_N3_DEFER_J 0
+#endif
+template <int VARIANT, bool GUARD, bool RAGGED, bool SHIFT = false, bool CUT = false, bool POT = false,
+          int FAR = 0, int MAX = -1, typename PJ = const double (*)[128], bool SC = false>
+__device__ __forceinline__ void n3_step_defer(int idx, double m, double xi, double yi, double zi, double mi,
+                                              PJ pj, const double* mj, double* ax, double* ay,
+                                              double* az, double& fx, double& fy, double& fz, const PairC& c,
+                                              const double* nsh, int qidx, double& qx, double& qy, double& qz) {
+    double px, py, pz;
+    auto prev = [&]() {
+        if (qidx >= 0) n3_j_add<POT>(qidx, ax, ay, az, qx, qy, qz);
+    };
+    n3_terms<VARIANT, GUARD, RAGGED, SHIFT, CUT, POT, FAR, MAX, PJ, SC>(idx, m, xi, yi, zi, mi, pj, mj, fx, fy, fz, c, nsh,
+                                                                       px, py, pz, prev);
+    qx = px; qy = py; qz = pz;
 }
 
 #ifndef MDQT_N3_WAVES
@@ -481,8 +534,14 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
     auto set_base = [&](int b) {
         if constexpr (MDQT_LDS_SPLIT) { pb = lds_pj(pj, b); pbase = b; }
     };
+    double qx = 0., qy = 0., qz = 0.;              // MDQT_N3_DEFER_J: the previous step's j terms, at qidx
+    int qidx = -1;
     auto step = [&](int idx, double m) {
-        if constexpr (MDQT_LDS_SPLIT) {             // (the LDS bases opaque per step: ds_read_b64, no read2)
+        if constexpr (MDQT_N3_DEFER_J) {
+            n3_step_defer<VARIANT, GUARD, RAGGED, false, CUT, POT, 0, -1, const double (*)[128], SC>(
+                idx, m, xi, yi, zi, mi, pj, mj, ax, ay, az, fx, fy, fz, cs, nullptr, qidx, qx, qy, qz);
+            qidx = idx;
+        } else if constexpr (MDQT_LDS_SPLIT) {      // (the LDS bases opaque per step: ds_read_b64, no read2)
             lds_pj_opaque(pb);
             n3_step<VARIANT, GUARD, RAGGED, false, CUT, POT, 0, -1, LdsPJ, SC>(idx - pbase, m, xi, yi, zi, mi, pb,
                                                                               mj + pbase, ax + pbase, ay + pbase,
@@ -542,6 +601,9 @@ __device__ __forceinline__ void n3_tile(const N3Args& a, const PairC& c, int I, 
         step(b + 32 / N3W - 1, (q == N3W - 1 && l >= 32) ? 0. : 1.);  // lane distance 32: once per pair
     }
     if constexpr (MDQT_N3_PRIO) __builtin_amdgcn_s_setprio(0);
+    if constexpr (MDQT_N3_DEFER_J) {
+        if (qidx >= 0) n3_j_add<POT>(qidx, ax, ay, az, qx, qy, qz);
+    }
     ia[q][0][l] = fx; ia[q][1][l] = fy; ia[q][2][l] = fz;
     __syncthreads();
     const size_t slab3 = POT ? (size_t)S : (size_t)3 * S;   // potential: [ntiles][S], one plane per slot

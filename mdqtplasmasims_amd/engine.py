@@ -365,8 +365,8 @@ class Simulation:
     def force_jstep_balance(self):
         """the block kernel's J-step balance over a workgroup's 8 waves (diagnostic; include/mdqt.h
         mdqt_force_jstep_balance): {valu, valu_lockstep, jsteps, excess}"""
-        out = (C.c_double * 10)()
-        check(lib().mdqt_force_jstep_balance(self.h, out, 10), "force_jstep_balance")
+        out = (C.c_double * 11)()
+        check(lib().mdqt_force_jstep_balance(self.h, out, 11), "force_jstep_balance")
         return {"valu": out[0], "valu_lockstep": out[1], "jsteps": int(out[2]),
                 "excess": out[1] / out[0] if out[0] else None,
                 "pairs_lockstep": out[4], "pairs_best_two_substeps": out[3], "row_floor": out[5],
@@ -375,7 +375,8 @@ class Simulation:
                 "excess_pairs_heavy_light": out[6] / out[0] if out[0] else None,
                 "excess_pairs_q_7mq": out[7] / out[0] if out[0] else None,
                 "excess_pairs_q_qp4": out[8] / out[0] if out[0] else None,
-                "excess_pairs_per_jstep": out[9] / out[0] if out[0] else None}
+                "excess_pairs_per_jstep": out[9] / out[0] if out[0] else None,
+                "excess_pairs_best_of_105": out[10] / out[0] if out[0] else None}
 
     def kernel_time_totals(self):
         """(force_ms, n_force_launches, substep_ms, n_substep_launches) since the last call"""

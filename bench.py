@@ -1048,7 +1048,10 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     ru, ufar = sim.const("force_ufar_radius"), sim.const("force_ufar_bound")
     ru32 = sim.const("force_ufar32_radius")
     tail_eps = 10.0 ** -12                          # force_tail_exp default
-    bound_met = bool(rt >= L / 2 or (tmode == 1 and tail <= tail_eps) or tmode == 0)
+    fmode = int(sim.const("force_form_measured"))   # force_form_mode 1: the sums hold the forms' terms too
+    err_eps = sim.const("force_error_eps")          # what they are held to (tail eps + 1e-13 per active tier)
+    bound_met = bool((fmode and tail <= err_eps) or (not fmode and (rt >= L / 2 or (tmode == 1 and tail <= tail_eps)
+                                                                    or tmode == 0)))
     census = None                                  # the block kernel's work by tile-pair class
     imbalance = None
     if int(sim.const("force_scheme")) == 3 and int(sim.const("force_sort")) == 1:
@@ -1132,6 +1135,7 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "parity": parity if check else {"note": "world 1: this line is the reference the sharded runs are checked against"},
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail, "bound_met": bound_met,
                            "tail_mode": "measured+enforced" if tmode == 1 else "a priori",
+                           "form_mode": "measured+enforced" if fmode else "a priori", "error_eps": err_eps,
                            "tail_model_bound": tmodel if tmode == 1 else None,
                            "tiles_over_eps_fixed": fixed, "largest_tile_sum_before_fix": raw,
                            "mid_radius": rm, "mid_bound": mid,
@@ -1143,8 +1147,11 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
                                    "remaining sub-tile sum; a priori: (N - 1) g(skip_radius)); sub-tile groups >= mid_radius / "
                                    "far_radius / vfar_radius / ufar_radius apart take the mid / far / very-far / ultra-far pair "
                                    "forms; every ion's force is within bound + mid_bound + far_bound + vfar_bound + ufar_bound "
-                                   "of the exact sum to L/2 (mdqt_engine.cpp tail_radius / far_radius_l; 0 = exact). fp64 "
-                                   "rates count all N(N-1)/2 pairs (SURVEY 8d)"},
+                                   "of the exact sum to L/2 (mdqt_engine.cpp tail_radius / far_radius_l; 0 = exact); "
+                                   "form_mode measured+enforced (round 6): the tiers' radii from a density model, the sums "
+                                   "also hold n g(gap) err_form(gap) of every sub-block evaluated in an error-bounded form, "
+                                   "held to error_eps, and bound (their largest after the exact pass) is every ion's total "
+                                   "(the *_bound entries are then the model's). fp64 rates count all N(N-1)/2 pairs (SURVEY 8d)"},
             "substeps_ms_per_md_step": s_ms / max(ns, 1) if ns else None}
 
 

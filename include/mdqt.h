@@ -252,6 +252,18 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     (N - 1) g(L/2 (1 - 2^-20)) stays inside the budget) the pair terms in f32;
  *                     each shell's bound <= 10^-k; k = 13 default, 0 = off.  "force_ufar_radius",
  *                     "force_ufar32_radius", "force_ufar_bound" (both shells)
+ *   "force_form_mode": how the four tiers' radii are bounded (round 6).  1 (default, with
+ *                     force_tail_mode 1, spatial order and the fast variant) = measured and
+ *                     enforced: every force call's per-sub-tile sums also hold, for each sub-block
+ *                     evaluated in an error-bounded form, n g(gap) err_form(gap); they are held to
+ *                     "force_error_eps" (the tail's eps where r_t < L/2, + 10^-k per active tier) and
+ *                     a tile over it is recomputed exactly, as for the tail; the radii come from a
+ *                     density model of those sums (<= the a-priori radii) and widen with r_t when a
+ *                     configuration exceeded it; the f32 form only for groups whose pairs are all
+ *                     closer than L/2 (1 - 2^-20).  "force_tail_bound" is then the measured bound on
+ *                     every ion's total deviation from the exact sum to L/2, the *_bound
+ *                     constants the model's; "force_form_measured" 1 where mode 1 applies.  0 = the
+ *                     a-priori radii above
  *   "qt_enabled":     1 = qstep() runs in the substeps, 0 = skipped (t still advances): the
  *                     pumping programs' pump window (randomFrozenStartTag408Linear.cpp main)
  *   "qt_math":        0 = the reference's exact operations, 1 = FMA-contracted with a refined

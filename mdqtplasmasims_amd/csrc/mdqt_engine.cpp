@@ -72,6 +72,9 @@ inline cx cx_conj(cx a) { return {a.re, -a.im}; }
 #ifndef MDQT_TAIL_MODE
 #define MDQT_TAIL_MODE 1
 #endif
+#ifndef MDQT_FORM_MODE
+#define MDQT_FORM_MODE 1
+#endif
 struct mdqt_ctx {
     mdqt_params p;
     // derived constants (SpeedUp:79-85, :146-149, :295-297)
@@ -155,6 +158,15 @@ struct mdqt_ctx {
     // the ultra-far pair form (option "force_ufar_exp" k, 0 = off): raw rsq and v_exp_f32, r_ufar the
     // smallest radius with (N - 1) g(r) ((r/lDeb) (kRsqRawErr + 2^-24) + 3 kRsqRawErr + kExp2fRelErr) <= 10^-k
     int ufar_exp = 13;
+    // how the tiers' radii are bounded (option "force_form_mode", round 6): 0 a priori, (N - 1) g(r)
+    // err(r) <= 10^-k per tier (far_radius_l); 1 (default, where the tail is measured: force_tail_mode 1,
+    // spatial order, the fast variant) measured and enforced — every sub-block the plan evaluates in an
+    // error-bounded form adds n_b g(gap) err_form(gap) to its sub-tiles' sums (k_n3b_plan), a tile whose
+    // sum exceeds the call's eps (the tail's where r_t < L/2, + 10^-k per active tier: error_eps) is
+    // recomputed exactly (k_tail_fix), and the radii come from the density model of those sums
+    // (tier_radius) — so every ion meets that eps whatever the configuration
+    int form_mode = MDQT_FORM_MODE;
+    mutable double form_key[6][6] = {}, form_val[6][2] = {};   // tier_radius memo by level (N, L, lDeb, k, tail_exp, scale)
     uint32_t* dKeys = nullptr;     // [2][N] Hilbert keys, sorted keys
     int* dIon = nullptr;           // [2][N] identity, sorted index -> ion
     void* dSortTmp = nullptr;
@@ -996,7 +1008,11 @@ static double tail_radius_sum(const mdqt_ctx* s, double* bound);
 static bool tail_measured(const mdqt_ctx* s);
 static double skip_radius(const mdqt_ctx* s, double* bound);
 static double far_radius(int N, double L, double lDeb, int k, double* bound);
-static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound);
+static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound, bool cutterm = true);
+static bool form_measured(const mdqt_ctx* s);
+static double tier_radius(const mdqt_ctx* s, int k, int level, double* bound);
+static void tier_radii(const mdqt_ctx* s, N3BArgs& a);
+static double error_eps(const mdqt_ctx* s, const N3BArgs& a);
 extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
     if (!strcmp(n, "gamToEinsteinFreq")) return s->gamToE;
     if (!strcmp(n, "quantumTimestep")) return s->dtQ;
@@ -1029,9 +1045,14 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
         double bound;                                  // and its force bound (0: exact, r = L/2)
         const double r = (s->use_n3b && s->sort_mode == 1) ? skip_radius(s, &bound) : (bound = 0., s->L / 2.);
         if (n[6] == 's') return r;
-        if (s->use_n3b && tail_measured(s) && r < s->L / 2.) {
+        N3BArgs ea{};                                  // (what the call's sums hold: error_eps > 0)
+        ea.Rcut = s->L / 2.; ea.Rskip = r;
+        if (s->use_n3b) tier_radii(s, ea);
+        if (s->use_n3b && (tail_measured(s) || form_measured(s)) && error_eps(s, ea) > 0.) {
             // mode 1: the running maximum of the per-tile sums each call met after the exact pass
-            // (1e-12 relative: the device sum's rounding); NaN until a force call has measured
+            // (1e-12 relative: the device sum's rounding); NaN until a force call has measured.  With
+            // force_form_mode 1 the sums hold the error-bounded forms' terms too: the bound on every
+            // ion's total deviation from the exact sum to L/2 (held to force_error_eps)
             unsigned long long h[8];
             if (!s->dTailSt || hipStreamSynchronize(s->stream) != hipSuccess ||
                 hipMemcpy(h, s->dTailSt, sizeof h, hipMemcpyDeviceToHost) != hipSuccess || h[4] == 0) return NAN;
@@ -1057,36 +1078,47 @@ extern "C" double mdqt_get_const(const mdqt_ctx* s, const char* n) {
         return bound;
     }
     if (!strcmp(n, "force_tail_mode")) return s->tail_mode;
+    if (!strcmp(n, "force_form_mode")) return s->form_mode;
+    if (!strcmp(n, "force_form_measured")) return form_measured(s) ? 1. : 0.;
+    if (!strcmp(n, "force_error_eps")) {               // the eps the measured sums are held to (0: none)
+        if (!(s->use_n3b && (tail_measured(s) || form_measured(s)))) return 0.;
+        N3BArgs a{};
+        double b;
+        a.Rcut = s->L / 2.;
+        a.Rskip = skip_radius(s, &b);
+        tier_radii(s, a);
+        return error_eps(s, a);
+    }
     if (!strcmp(n, "force_far_radius") || !strcmp(n, "force_far_bound")) {   // the far pair form's radius
         double bound;                                  // and force bound (0: off, r = L/2)
         const double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
-                             ? far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound) : (bound = 0., s->L / 2.);
+                             ? tier_radius(s, s->far_exp, 1, &bound) : (bound = 0., s->L / 2.);
         return n[10] == 'r' ? r : bound;
     }
     if (!strcmp(n, "force_mid_radius") || !strcmp(n, "force_mid_bound")) {   // the mid form's radius
         double bound;                                  // and force bound (0: off, r = L/2)
         const double r = (MDQT_EXP_TAB && s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
-                             ? far_radius_l(s->N, s->L, s->lDeb, s->mid_exp, 5, &bound) : (bound = 0., s->L / 2.);
+                             ? tier_radius(s, s->mid_exp, 5, &bound) : (bound = 0., s->L / 2.);
         return n[10] == 'r' ? r : bound;
     }
     if (!strcmp(n, "force_ufar_radius") || !strcmp(n, "force_ufar_bound")) {   // the ultra-far form's
         double bound;                                  // radius and force bound (0: off, r = L/2)
         double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
-                       ? far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound) : (bound = 0., s->L / 2.);
+                       ? tier_radius(s, s->ufar_exp, 3, &bound) : (bound = 0., s->L / 2.);
         if (r < s->L / 2. && s->L / 2. > 80. * s->lDeb) { r = s->L / 2.; bound = 0.; }
         double b32 = 0.;                               // + the f32 shell beyond force_ufar32_radius
-        if (r < s->L / 2. && MDQT_UFAR32) far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 4, &b32);
+        if (r < s->L / 2. && MDQT_UFAR32) tier_radius(s, s->ufar_exp, 4, &b32);
         return n[11] == 'r' ? r : bound + b32;
     }
     if (!strcmp(n, "force_ufar32_radius")) {          // the f32 ultra-far form's radius (L/2: off)
         double bound;
         const double r3 = mdqt_get_const(s, "force_ufar_radius");
-        return (r3 < s->L / 2. && MDQT_UFAR32) ? far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 4, &bound) : s->L / 2.;
+        return (r3 < s->L / 2. && MDQT_UFAR32) ? tier_radius(s, s->ufar_exp, 4, &bound) : s->L / 2.;
     }
     if (!strcmp(n, "force_vfar_radius") || !strcmp(n, "force_vfar_bound")) {   // the very-far form's
         double bound;                                  // radius and force bound (0: off, r = L/2)
         const double r = (s->use_n3b && s->sort_mode != 0 && s->force_variant == 1 && !s->guard)
-                             ? far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound) : (bound = 0., s->L / 2.);
+                             ? tier_radius(s, s->vfar_exp, 2, &bound) : (bound = 0., s->L / 2.);
         return n[11] == 'r' ? r : bound;
     }
     if (!strcmp(n, "fused_step")) return s->fused_opt;
@@ -1409,8 +1441,9 @@ static double skip_radius(const mdqt_ctx* s, double* bound) {
 // r_t): the next calls take r_t for tail_scale = max(2 tail_scale, 2^ceil(log2 u)) — capped at the
 // a-priori radius — and stderr says so.  Every rank sees the same all-reduced sums, so ranks
 // widen alike.
+static double model_total(const mdqt_ctx* s);
 static int tail_check(mdqt_ctx* s) {
-    if (!s->dTailSt || !s->use_n3b || !tail_measured(s)) return 0;
+    if (!s->dTailSt || !s->use_n3b || !(tail_measured(s) || form_measured(s))) return 0;
     unsigned long long h[8];
     HIPCHK(hipMemcpyAsync(h, s->dTailSt, sizeof h, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
@@ -1418,13 +1451,14 @@ static int tail_check(mdqt_ctx* s) {
     double b0, b1;
     const double r0 = tail_radius_sum(s, &b0);
     const double raw = u64_as_double(h[1]);
+    b0 = model_total(s);                            // (the tail's model bound + the tiers', force_form_mode 1)
     const double u = b0 > 0. ? raw / b0 : INFINITY;
     // a power of two: the sums' last bits (atomic order, the ranks' partial sums) cannot move it
     s->tail_scale = std::max(2. * s->tail_scale, std::isfinite(u) && u < 1e300 ? exp2(ceil(log2(u))) : 1e300);
     const double r1 = tail_radius_sum(s, &b1);
     if (s->tail_warned++ < 8)                       // (rate-limited: a few lines per context)
-        fprintf(stderr, "mdqt: force tail over 1e-%d on %llu tile(s) so far (largest per-tile sum %.3e; the model's "
-                "%.3e at r_t = %.4f): corrected by the exact pass; r_t widened to %.4f\n", s->tail_exp,
+        fprintf(stderr, "mdqt: force error bound exceeded on %llu tile(s) so far (largest per-tile sum %.3e; the model's "
+                "%.3e at r_t = %.4f): corrected by the exact pass; r_t widened to %.4f (the tiers' radii likewise)\n",
                 (unsigned long long)h[2], raw, b0, r0, r1);
     s->tail_seen = h[2];
     return 0;
@@ -1433,7 +1467,7 @@ static int tail_check(mdqt_ctx* s) {
 // the enforcement after a force call's tail sums are complete: list the tiles over eps, add their
 // skipped pairs exactly (k_tail_fix) to `out` (F, or this rank's dense partial)
 static int tail_enforce(mdqt_ctx* s, const N3BArgs& a, double* out) {
-    const double eps = pow(10., -s->tail_exp);
+    const double eps = error_eps(s, a);
     HIPCHK(launch_tail_max(a.tailb, a.T, eps, s->dTailSt, s->dTailList, s->stream));
     HIPCHK(launch_tail_fix(a, s->dTailSt, s->dTailList, out, s->stream));
     return 0;
@@ -1478,14 +1512,15 @@ static double far_err(double r, double lDeb, int level) {
     if (level == 3) return (r / lDeb) * (kRsqRawErr + 0x1p-24) + 3. * kRsqRawErr + kExp2fRelErr;
     return level == 2 ? (r / lDeb + 3.) * kRsqRawErr + kExp5RelErr : kFarRelErr;
 }
-static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound) {
+static double far_radius_l(int N, double L, double lDeb, int k, int level, double* bound, bool cutterm) {
     const double Rcut = L / 2.;
     *bound = 0.;
     if (k <= 0 || N < 2) return Rcut;
     const double eps = pow(10., -k), n1 = (double)(N - 1);
     // level 4 (f32) decides the cutoff on its f32 r^2 (relative error <= 6 2^-24): pairs within
     // 3 2^-24 Rcut of L/2 may land on either side, each at most g(Rcut (1 - 2^-20)) — a constant term
-    const double cut = level == 4 ? n1 * tail_g(Rcut * (1. - 0x1p-20), lDeb) : 0.;
+    // (not with force_form_mode 1, cutterm false: the plan keeps the f32 form off the cutoff)
+    const double cut = level == 4 && cutterm ? n1 * tail_g(Rcut * (1. - 0x1p-20), lDeb) : 0.;
     auto b = [&](double r) { return n1 * tail_g(r, lDeb) * far_err(r, lDeb, level) + cut; };
     if (b(Rcut) > eps) return Rcut;
     double lo = 0., hi = Rcut;
@@ -1498,6 +1533,103 @@ static double far_radius_l(int N, double L, double lDeb, int k, int level, doubl
 }
 static double far_radius(int N, double L, double lDeb, int k, double* bound) {
     return far_radius_l(N, L, lDeb, k, 1, bound);
+}
+
+// force_form_mode 1 (round 6): the tiers' radii from a density model of the per-sub-tile form sums the
+// plan measures (k_n3b_plan), as tail_model for the tail: at density rho the sub-tiles with box gap in
+// [x, x + dx] hold about rho 4 pi (x + delta)^2 dx ions, so a sub-tile's sum over a tier's sub-blocks (gap
+// >= r) is about F(r) = rho int_r^hi 4 pi (x + delta)^2 g(x) err(x) dx, hi = r_t (nothing beyond it is
+// evaluated).  The radius is the smallest r with m s F(r) <= 10^-k (m = kTailMargin, s = tail_scale:
+// raised with r_t's when a call's sums exceeded its eps), never beyond the a-priori radius (rigorous for
+// any configuration; level 4 without the cutoff term).  The model only picks the radii: the plan measures
+// every tile's sum and k_tail_fix enforces the call's eps (error_eps).
+// (force_sort 1 and 2 alike: 2 runs the same plan without skipping, and must give the same forms)
+static bool form_measured(const mdqt_ctx* s) {
+    return s->form_mode == 1 && s->use_n3b && s->tail_mode == 1 && s->sort_mode >= 1 && s->force_variant == 1 &&
+           !s->guard;
+}
+static double form_model(double r, double hi, int N, double L, double lDeb, int level) {
+    const double rho = N / (L * L * L), delta = 2. * cbrt(16. / rho);
+    if (r >= hi) return 0.;
+    const int n = 2000;                             // Simpson on [r, hi]
+    const double h = (hi - r) / n;
+    auto f = [&](double x) { return 4. * M_PI * (x + delta) * (x + delta) * tail_g(x, lDeb) * far_err(x, lDeb, level); };
+    double acc = f(r) + f(hi);
+    for (int i = 1; i < n; ++i) acc += (i & 1 ? 4. : 2.) * f(r + i * h);
+    return rho * acc * h / 3.;
+}
+// a tier's radius (L/2: off) and bound: a priori (force_form_mode 0) or the model's (1; memoised per context)
+static double tier_radius(const mdqt_ctx* s, int k, int level, double* bound) {
+    if (!form_measured(s)) return far_radius_l(s->N, s->L, s->lDeb, k, level, bound);
+    const double Rcut = s->L / 2.;
+    *bound = 0.;
+    if (k <= 0 || s->N < 2) return Rcut;
+    const double sc = s->tail_scale;
+    double* key = s->form_key[level];
+    if (key[0] == s->N && key[1] == s->L && key[2] == s->lDeb && key[3] == k && key[4] == s->tail_exp && key[5] == sc) {
+        *bound = s->form_val[level][1];
+        return s->form_val[level][0];
+    }
+    double tb;
+    const double hi = tail_radius_sum(s, &tb);      // r_t (L/2 where the tail is exact)
+    double ba;
+    const double ra = far_radius_l(s->N, s->L, s->lDeb, k, level, &ba, false);
+    const double eps = pow(10., -k);
+    double lo = 0., up = hi;
+    for (int it = 0; it < 60 && up - lo > 1e-9 * Rcut; ++it) {
+        const double m = 0.5 * (lo + up);
+        if (m > 0 && kTailMargin * sc * form_model(m, hi, s->N, s->L, s->lDeb, level) <= eps) up = m; else lo = m;
+    }
+    double r = up, b = form_model(up, hi, s->N, s->L, s->lDeb, level);
+    if (r >= ra) { r = ra; b = ba; }                // the a-priori radius bounds any configuration
+    if (r >= hi) { r = Rcut; b = 0.; }              // (nothing evaluated that far: the tier is off)
+    key[0] = s->N; key[1] = s->L; key[2] = s->lDeb; key[3] = k; key[4] = s->tail_exp; key[5] = sc;
+    s->form_val[level][0] = r; s->form_val[level][1] = b;
+    *bound = b;
+    return r;
+}
+// the model's per-sub-tile sum at the current radii — the tail's where r_t < L/2, + the tiers' evaluated
+// inside r_t (force_form_mode 1) — that tail_check compares the measured sums with
+static double model_total(const mdqt_ctx* s) {
+    double b = 0., t;
+    const double rt = tail_radius_sum(s, &t);
+    if (rt < s->L / 2.) b += t;
+    if (form_measured(s)) {
+        if (MDQT_EXP_TAB && tier_radius(s, s->mid_exp, 5, &t) < rt) b += t;
+        if (tier_radius(s, s->far_exp, 1, &t) < rt) b += t;
+        if (tier_radius(s, s->vfar_exp, 2, &t) < rt) b += t;
+        if (tier_radius(s, s->ufar_exp, 3, &t) < rt) b += t;
+        if (MDQT_UFAR32 && tier_radius(s, s->ufar_exp, 4, &t) < rt) b += t;
+    }
+    return b;
+}
+// the eps a force call's per-sub-tile sums are held to (k_tail_max): the tail's where r_t < L/2, plus
+// (force_form_mode 1) 10^-k of every tier evaluated inside r_t
+static double error_eps(const mdqt_ctx* s, const N3BArgs& a) {
+    double e = a.Rskip < a.Rcut ? pow(10., -s->tail_exp) : 0.;
+    if (a.formm) {
+        if (MDQT_EXP_TAB && a.Rmid < a.Rskip && s->mid_exp > 0) e += pow(10., -s->mid_exp);
+        if (a.Rfar < a.Rskip && s->far_exp > 0) e += pow(10., -s->far_exp);
+        if (a.Rvfar < a.Rskip && s->vfar_exp > 0) e += pow(10., -s->vfar_exp);
+        if (a.Rufar < a.Rskip && s->ufar_exp > 0) e += pow(10., -s->ufar_exp);
+        if (MDQT_UFAR32 && a.Rufar32 < a.Rskip && s->ufar_exp > 0) e += pow(10., -s->ufar_exp);
+    }
+    return e;
+}
+
+// the tiers' radii of a force call (a.Rcut set): a priori or from the model (force_form_mode 1)
+static void tier_radii(const mdqt_ctx* s, N3BArgs& a) {
+    double bound;
+    a.Rmid = MDQT_EXP_TAB ? tier_radius(s, s->mid_exp, 5, &bound) : a.Rcut;
+    a.Rfar = tier_radius(s, s->far_exp, 1, &bound);
+    a.Rvfar = tier_radius(s, s->vfar_exp, 2, &bound);
+    a.Rufar = tier_radius(s, s->ufar_exp, 3, &bound);
+    a.Rufar32 = MDQT_UFAR32 ? tier_radius(s, s->ufar_exp, 4, &bound) : a.Rcut;
+    a.formm = form_measured(s) ? 1 : 0;
+    a.u32lim2 = (a.Rcut * (1. - 0x1p-20)) * (a.Rcut * (1. - 0x1p-20));
+    // f32's normal range: 2^t for t >= -126 (r <= 126 lDeb ln2 = 87 lDeb); never beyond it
+    if (a.Rufar < a.Rcut && a.Rcut > 80. * s->lDeb) a.Rufar = a.Rcut;
+    if (a.Rufar >= a.Rcut) a.Rufar32 = a.Rcut;
 }
 
 // the block-pair kernels' arguments for the current positions: with force_sort, the Hilbert order,
@@ -1515,15 +1647,8 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
     double bound;
     a.Rskip = skip_radius(s, &bound);
     a.tailb = nullptr;
-    a.Rmid = MDQT_EXP_TAB ? far_radius_l(s->N, s->L, s->lDeb, s->mid_exp, 5, &bound) : a.Rcut;
-    a.Rfar = far_radius(s->N, s->L, s->lDeb, s->far_exp, &bound);
-    a.Rvfar = far_radius_l(s->N, s->L, s->lDeb, s->vfar_exp, 2, &bound);
-    a.Rufar = far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 3, &bound);
-    a.Rufar32 = MDQT_UFAR32 ? far_radius_l(s->N, s->L, s->lDeb, s->ufar_exp, 4, &bound) : a.Rcut;
+    tier_radii(s, a);
     a.rc2 = a.Rcut * a.Rcut;
-    // f32's normal range: 2^t for t >= -126 (r <= 126 lDeb ln2 = 87 lDeb); never beyond it
-    if (a.Rufar < a.Rcut && a.Rcut > 80. * s->lDeb) a.Rufar = a.Rcut;
-    if (a.Rufar >= a.Rcut) a.Rufar32 = a.Rcut;
     if (s->sort_mode) {                            // Hilbert order + tile boxes (mdqt_sort.hip)
         SortArgs o;
         o.Rall = s->dR; o.N = s->N; o.S = s->S; o.Npad = a.Npad; o.L = s->L;
@@ -1532,7 +1657,9 @@ static int n3b_args(mdqt_ctx* s, N3BArgs& a) {
         o.subboxes = s->dSubBoxes;
         HIPCHK(launch_spatial_order(o, s->stream));
         a.use_sort = s->sort_mode; a.Rs = s->dRs; a.perm = o.perm; a.boxes = s->dBoxes; a.subboxes = s->dSubBoxes;
-        if (tail_measured(s) && a.Rskip < a.Rcut) a.tailb = s->dTail;
+        // the per-sub-tile sums: where the tail skips pairs, or (force_form_mode 1) a tier is evaluated
+        const bool tiers = a.formm && (a.Rmid < a.Rskip || a.Rfar < a.Rskip || a.Rvfar < a.Rskip || a.Rufar < a.Rskip);
+        if ((tail_measured(s) && a.Rskip < a.Rcut) || tiers) a.tailb = s->dTail;
         // the plan (k_n3b_plan): 256 tile-pair words per (P, db), then one J-step mask per (P, db)
         // and the per-J-tile masks of the block distances whose j-slots the block kernel writes (k_n3b_reduce
         // reads only those): T x ceil(nd / 64) words
@@ -2249,7 +2376,7 @@ static int potential_rows(mdqt_ctx* s, double* urow_dev) {
         if (s->timing && (s->tkinds & 4u) && take_events(s, 3, &e0, &e1)) return -1;
         HIPCHK(launch_potential_n3b(a, s->force_variant, urow_dev, s->stream, e0, e1));
         if (a.tailb) {                              // the enforcement (its own counters: dTailSt[8, 16))
-            HIPCHK(launch_tail_max(a.tailb, a.T, pow(10., -s->tail_exp), s->dTailSt + 8, s->dTailList, s->stream));
+            HIPCHK(launch_tail_max(a.tailb, a.T, error_eps(s, a), s->dTailSt + 8, s->dTailList, s->stream));
             HIPCHK(launch_tail_fix(a, s->dTailSt + 8, s->dTailList, urow_dev, s->stream, true));
         }
         return 0;
@@ -3042,21 +3169,29 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
     }
     if (!strcmp(name, "force_ufar_exp")) {             // ultra-far pair form: eps = 10^-value (0: off)
         if (value < 0 || value > 300) return fail("force_ufar_exp must be 0 (off) .. 300");
+        // (force_form_mode 1: the measured sums hold its terms — forget what earlier calls measured)
+        if (value != s->ufar_exp && form_measured(s) && (settle_forces(s) || tail_reset(s))) return -1;
         s->ufar_exp = value;
         return 0;
     }
     if (!strcmp(name, "force_vfar_exp")) {             // very-far pair form: eps = 10^-value (0: off)
         if (value < 0 || value > 300) return fail("force_vfar_exp must be 0 (off) .. 300");
+        // (force_form_mode 1: the measured sums hold its terms — forget what earlier calls measured)
+        if (value != s->vfar_exp && form_measured(s) && (settle_forces(s) || tail_reset(s))) return -1;
         s->vfar_exp = value;
         return 0;
     }
     if (!strcmp(name, "force_mid_exp")) {              // mid pair form: eps = 10^-value (0: off)
         if (value < 0 || value > 300) return fail("force_mid_exp must be 0 (off) .. 300");
+        // (force_form_mode 1: the measured sums hold its terms — forget what earlier calls measured)
+        if (value != s->mid_exp && form_measured(s) && (settle_forces(s) || tail_reset(s))) return -1;
         s->mid_exp = value;
         return 0;
     }
     if (!strcmp(name, "force_far_exp")) {              // far pair form: eps = 10^-value (0: off)
         if (value < 0 || value > 300) return fail("force_far_exp must be 0 (off) .. 300");
+        // (force_form_mode 1: the measured sums hold its terms — forget what earlier calls measured)
+        if (value != s->far_exp && form_measured(s) && (settle_forces(s) || tail_reset(s))) return -1;
         s->far_exp = value;
         return 0;
     }
@@ -3064,6 +3199,12 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         if (value < 0 || value > 300) return fail("force_tail_exp must be 0 (exact) .. 300");
         if (value != s->tail_exp && (settle_forces(s) || tail_reset(s))) return -1;
         s->tail_exp = value;
+        return 0;
+    }
+    if (!strcmp(name, "force_form_mode")) {            // the tiers' radii: 0 a priori, 1 measured and enforced
+        if (value < 0 || value > 1) return fail("force_form_mode must be 0 (a priori) or 1 (measured)");
+        if (value != s->form_mode && (settle_forces(s) || tail_reset(s))) return -1;
+        s->form_mode = value;
         return 0;
     }
     if (!strcmp(name, "force_tail_mode")) {            // 0: a-priori bound, 1: measured and enforced

@@ -559,6 +559,46 @@ __device__ __forceinline__ double tail_g(double g2, float invl, float cf) {
     const float e = __builtin_amdgcn_exp2f((s * ri) * cf);
     return (double)(((ri + invl) * e) * ri) * (1. + 0x1p-12);
 }
+// force_form_mode 1: the bound on the error of one pair term at distance >= the gap d (g2 = d^2) in the
+// pair form of level e >= 1: g(d) err_e(d) = g(d) (kFormErrA[e] d/lDeb + kFormErrB[e]) — both factors as
+// upper bounds in f32 (tail_g's; d/lDeb within 3 2^-23), the product x (1 + 2^-10).  g err_e decreases
+// in d for every form (its log-derivative is below 1/(1 + x) - 1/x - 1 < 0, x = d/lDeb), so each of the
+// sub-block's pairs (distance >= its gap) is bounded by it.
+// (the constants rounded up to f32; the whole term in f32 — f32 VALU issues at twice the f64 rate — and
+// x (1 + 2^-10) covers every rounding: tail_g's 2^-12 bound, d/lDeb's 3 2^-23, the err factor's and the
+// product's 2^-23 each)
+__constant__ const float kFormA[6] = {(float)kFormErrA[0], (float)(kFormErrA[1] * (1. + 0x1p-20)),
+                                      (float)kFormErrA[2], (float)(kFormErrA[3] * (1. + 0x1p-20)),
+                                      (float)(kFormErrA[4] * (1. + 0x1p-20)), (float)(kFormErrA[5] * (1. + 0x1p-20))};
+__constant__ const float kFormB[6] = {(float)kFormErrB[0], (float)(kFormErrB[1] * (1. + 0x1p-20)),
+                                      (float)(kFormErrB[2] * (1. + 0x1p-20)), (float)(kFormErrB[3] * (1. + 0x1p-20)),
+                                      (float)(kFormErrB[4] * (1. + 0x1p-20)), (float)(kFormErrB[5] * (1. + 0x1p-20))};
+__device__ __forceinline__ double form_term(double g2, float invl, float cf, int e) {
+    const float s = (float)g2;
+    const float ri = __builtin_amdgcn_rsqf(s);
+    const float r = s * ri;
+    const float ex = __builtin_amdgcn_exp2f(r * cf);
+    const float g = ((ri + invl) * ex) * ri;
+    return (double)(g * fmaf(r * invl, kFormA[e], kFormB[e])) * (1. + 0x1p-10);
+}
+// force_form_mode 1: the squared far distance of sub-tiles s and u under a uniform image's shifts nL (the
+// block kernel's xi - n L - xj): every pair's |dx| per axis is at most |c_s - c_u - n L| + h_s + h_u
+__device__ __forceinline__ double sub_far2(const double* __restrict__ SB, int T4, int s, int u, const double* nL) {
+    double f2 = 0.;
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) {
+        const double d = fabs((SB[(size_t)c3 * T4 + s] - SB[(size_t)c3 * T4 + u]) - nL[c3]) +
+                         (SB[(size_t)(3 + c3) * T4 + s] + SB[(size_t)(3 + c3) * T4 + u]);
+        f2 = fma(d, d, f2);
+    }
+    return f2;
+}
+// the uniform image's shifts n L of a class word (n3b_pack_class; the block kernel's nsh)
+__device__ __forceinline__ void class_shifts(int pw, double L, double* nL) {
+    nL[0] = (double)((pw << 20) >> 24) * L;
+    nL[1] = (double)((pw << 12) >> 24) * L;
+    nL[2] = (double)((pw << 4) >> 24) * L;
+}
 // a tile pair's class and uniform-image multiples in one LDS word: bits 0-3 class + 2, 4-11 / 12-19 /
 // 20-27 n_x, n_y, n_z (signed); a uniform image with a multiple beyond +-127 (positions that far
 // outside the box) is taken per pair instead.  A per-pair image that varies on ONE axis only (strad:
@@ -1387,6 +1427,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
         } else {
             const int T4 = 4 * a.T;
             const double hj2 = raw_half2(a.boxes, a.T, J);
+            const double nL[3] = {t4.x * a.L, t4.y * a.L, t4.z * a.L};   // (the uniform image's; formm)
             unsigned act = 0, mm = 0, mf = 0, mv = 0, mu = 0, m32 = 0;
             double np[4] = {0., 0., 0., 0.};       // ion pairs per group
             for (int sa = 0; sa < 4; ++sa)
@@ -1398,7 +1439,9 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                     if (sg > rad.rf2) mf |= bit;
                     if (sg > rad.rv2) mv |= bit;
                     if (sg > rad.ru2) mu |= bit;
-                    if (sg > rad.ru32 && sg > 4. * hj2) m32 |= bit;   // (k_n3b_plan's level 5)
+                    if (sg > rad.ru32 && sg > 4. * hj2 &&   // (k_n3b_plan's level 5)
+                        (!a.formm || !uni || sub_far2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, nL) < a.u32lim2))
+                        m32 |= bit;
                     np[(sb - sa) & 3] += sub_count(a.N, 4 * I + sa) * sub_count(a.N, 4 * J + sb);
                 }
             const unsigned g = a.use_sort == 1 ? sub_groups_of(act) : 0xFu;   // (2: nothing skipped)
@@ -1578,10 +1621,27 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
             // read only where a group is that far
             const double gmax = fmax(fmax(gm[0], gm[1]), fmax(gm[2], gm[3]));
             const double hj4 = FARF && gmax > rad.ru32 ? 4. * raw_half2(a.boxes, a.T, J) : 0.;
+            int xs[4];                              // the groups' levels (the measured form bound)
+            // (formm) the whole tile pair within u32lim2 under its image — tile boxes: every sub-block is
+            bool tile_in = false;
+            if (FARF && a.formm && gmax > rad.ru32 && uni) {
+                double nL[3];
+                class_shifts(pw, a.L, nL);
+                tile_in = sub_far2(a.boxes, a.T, I, J, nL) < a.u32lim2;   // ([12][T]: centers, half extents first)
+            }
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 int x = !FARF ? 0 : n3b_level(gm[d], rad);
                 if (x == 5 && !(gm[d] > hj4)) x = 4;
+                if (x == 5 && a.formm && uni && !tile_in) {   // f32 only where no pair can reach the cutoff (u32lim2)
+                    double nL[3];
+                    class_shifts(pw, a.L, nL);
+                    double f2 = 0.;
+#pragma unroll
+                    for (int sa = 0; sa < 4; ++sa) f2 = fmax(f2, sub_far2(a.subboxes, T4, 4 * I + sa, 4 * J + ((sa + d) & 3), nL));
+                    if (!(f2 < a.u32lim2)) x = 4;
+                }
+                xs[d] = x;
                 if (gm[d] <= rad.rc2 && !(g2 > rad.rc2)) cest += n3b_pair_cost(x, uni, rag);
                 if (a.use_sort != 1 || gm[d] <= rad.rc2) {
                     groups |= 1u << d;
@@ -1596,9 +1656,13 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
                 for (int sa = 0; sa < 4; ++sa)
 #pragma unroll
                     for (int sb = 0; sb < 4; ++sb) {
-                        const bool drop = cls == -2 || !((groups >> ((sb - sa) & 3)) & 1u);
-                        if (drop && sg[sa][sb] < rcut2) {
-                            const double gd = tail_g(sg[sa][sb], invl, cf);
+                        const int d = (sb - sa) & 3;
+                        const bool drop = cls == -2 || !((groups >> d) & 1u);
+                        // the form the block kernel takes for the group (n3b_tile_pair): exact on a ragged
+                        // tile pair, levels >= 3 in the very-far form with a per-pair image
+                        const int e = (drop || !a.formm || rag) ? 0 : uni ? xs[d] : min(xs[d], 3);
+                        if ((drop || e > 0) && sg[sa][sb] < rcut2) {
+                            const double gd = drop ? tail_g(sg[sa][sb], invl, cf) : form_term(sg[sa][sb], invl, cf, e);
                             gi[sa] += sub_count(a.N, 4 * J + sb) * gd;
                             gj[sb] += sub_count(a.N, 4 * I + sa) * gd;
                         }
@@ -1804,8 +1868,8 @@ static hipError_t launch_n3b_plan(const N3BArgs& a, int variant, hipStream_t s) 
             if (a.guard) hipLaunchKernelGGL((k_n3b_plan<0, true>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
             else hipLaunchKernelGGL((k_n3b_plan<0, false>), dim3(nplan), dim3(BW * BW), 0, s, a, a.plan);
         }
-    } else if (a.tailb) {
-        return hipErrorInvalidValue;                // the tail sums come from the plan
+    } else if (a.tailb && !a.plan) {
+        return hipErrorInvalidValue;                // the tail sums come from the plan (a rank without blocks: 0)
     }
     return hipGetLastError();
 }

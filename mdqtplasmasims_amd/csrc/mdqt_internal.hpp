@@ -303,13 +303,21 @@ constexpr double kExp2fRelErr = 0x1p-22;
 // rounded up).  The cutoff is decided on the f32 r^2 (<= 11u off): pairs within 6u Rcut of L/2 may
 // land on either side, each at most g(Rcut (1 - 2^-20)) — so far_radius_l's level 4 bounds every ion
 // by (N - 1) g(r) err(r) + (N - 1) g(Rcut (1 - 2^-20)), and the tier is off where that cannot meet
-// 10^-k (C5: N g(L/2) is ~1e-8; N = 1e6 at C2's parameters: ~5e-16).
+// 10^-k (C5: N g(L/2) is ~1e-8; N = 1e6 at C2's parameters: ~5e-16).  force_form_mode 1 (round 6) has
+// no such term: the plan gives a group the f32 form only if its far distance is below Rcut (1 - 2^-20)
+// (N3BArgs::u32lim2), so its f32 r^2 never decides a cutoff.
 #ifndef MDQT_UFAR32
 #define MDQT_UFAR32 1
 #endif
 constexpr double kRsqF32RelErr = 0x1p-23;
 constexpr double kUfar32A = 22. * 0x1p-24;
 constexpr double kUfar32B = 52. * 0x1p-24;
+// a term's relative error in the pair form of plan level e (0 exact, 1 mid, 2 far, 3 very far, 4 ultra
+// far, 5 ultra far in f32) as kFormErrA[e] r/lDeb + kFormErrB[e] (mdqt_engine.cpp far_err; the measured
+// form bound of k_n3b_plan, force_form_mode 1)
+constexpr double kFormErrA[6] = {0., kRsq1RelErr + 0x1p-52, 0., kRsqRawErr, kRsqRawErr + 0x1p-24, kUfar32A};
+constexpr double kFormErrB[6] = {0., 3. * (kRsq1RelErr + 0x1p-52) + kTab4RelErr, kFarRelErr,
+                                 3. * kRsqRawErr + kExp5RelErr, 3. * kRsqRawErr + kExp2fRelErr, kUfar32B};
 __device__ __forceinline__ double exp2_neg_cut5(double t, bool keep) {
     const double n = __builtin_rint(t);
     const double f = t - n;
@@ -446,6 +454,12 @@ struct N3BArgs {
                         // drops inside L/2 (tail-skipped tile pairs, skipped sub-tile groups) of
                         // n_b g(sub-block gap) — the measured bound on what each of its ions loses
                         // (zeroed before the launch, summed by k_n3b_plan; nullptr: not measured)
+    int formm;          // force_form_mode 1 (round 6): tailb also sums, over the sub-blocks evaluated in an
+                        // error-bounded form, n_b g(gap) err_form(gap) — the forms' measured bound, enforced
+                        // with the tail's (k_tail_max, k_tail_fix); the tier radii come from a density model
+    double u32lim2;     // formm: (Rcut (1 - 2^-20))^2 — a group takes the f32 ultra-far form only if every
+                        // pair of it is closer (its far distance under the tile pair's image), so the f32
+                        // r^2 never decides the cutoff (no a-priori cutoff term)
     const double* subboxes;   // [6][4T]: the 16-ion sub-tiles' centers and half extents (use_sort)
     uint2* plan;        // force calls in spatial order: [(Phi - Plo) nd][256] tile-pair words, then
                         // [(Phi - Plo) nd] J-step masks (.x), written by k_n3b_plan (launch_forces_n3b)

@@ -214,9 +214,10 @@ def test_error_bounded_tail_and_far_form(cfg):
     13: (N - 1) g(r) ((r/lDeb + 3) kRsqRawErr + kExp5RelErr) <= 1e-13), the ultra-far forms and the
     mid form beyond r_mid (force_mid_exp 13, round 4: (N - 1) g(r) ((r/lDeb + 3)(kRsq1RelErr + 2^-52)
     + kTab4RelErr) <= 1e-13) — each alone and all together, plus the summation-order rounding; r_t
-    is a no-op at C3 and C5"""
+    is a no-op at C3 and C5.  (force_form_mode 0: the a-priori tier radii; mode 1, the default, below)"""
     import mdqtplasmasims_amd as M
     s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg]).init()
+    s.set_option("force_form_mode", 0)                 # (the a-priori tier radii; form mode 1: the test below)
     L = s.const("L")
     rt, tb = s.const("force_skip_radius"), s.const("force_tail_bound")
     rm, mb0 = s.const("force_mid_radius"), s.const("force_mid_bound")
@@ -275,8 +276,56 @@ def test_error_bounded_tail_and_far_form(cfg):
     if cfg == "C5":                                    # r_t >= L/2 at C3 too: exact skipping only
         x = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS["C3"])
         x.set_state(*_tiny_state(x))
+        x.set_option("force_form_mode", 0)               # (the tail's own bound: no measured form sums)
         assert x.const("force_tail_bound") == 0 and x.const("force_skip_radius") == x.const("L") / 2
         x.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["C4", "C5"])
+def test_form_bound_measured_and_enforced(cfg):
+    """force_form_mode 1 (round 6, the default): the tiers' radii from the density model of the sums the
+    plan measures (mdqt_engine.cpp tier_radius) — below the a-priori radii of mode 0 — and every
+    sub-block evaluated in an error-bounded form adding n_b g(gap) err_form(gap) to its sub-tiles' sums
+    (k_n3b_plan), which k_tail_max holds to force_error_eps (the tail's eps where r_t < L/2 + 10^-13 per
+    active tier), recomputing any tile over it exactly.  On EVERY ion, against the same engine with the
+    tail and every form off: |dF_i| <= the measured bound of that call (force_tail_bound, the largest
+    per-sub-tile sum after the exact pass) + the summation-order rounding, for the defaults and each
+    tier alone; the measured bound <= force_error_eps; on these uniform configurations no tile over it"""
+    import mdqtplasmasims_amd as M
+    s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg]).init()
+    L = s.const("L")
+    assert s.const("force_form_mode") == 1 and s.const("force_form_measured") == 1
+    tiers = ("mid", "far", "vfar", "ufar", "ufar32")
+    r1 = {k: s.const(f"force_{k}_radius") for k in tiers}
+    s.set_option("force_form_mode", 0)
+    r0 = {k: s.const(f"force_{k}_radius") for k in tiers}
+    s.set_option("force_form_mode", 1)
+    print(f"{cfg}: radii form mode 1 {dict((k, round(v, 3)) for k, v in r1.items())}, mode 0 "
+          f"{dict((k, round(v, 3)) for k, v in r0.items())}, L/2 {L / 2:.3f}; force_error_eps "
+          f"{s.const('force_error_eps'):.2e}")
+    assert r1["mid"] < r1["far"] < r1["vfar"] <= r1["ufar"] <= r1["ufar32"] <= L / 2
+    for k in ("mid", "far", "vfar", "ufar"):
+        assert r1[k] < r0[k]
+    out, tb, eps = {}, {}, {}
+    combos = ((12, 13, 13, 13, 13), (0, 13, 0, 0, 0), (0, 0, 13, 0, 0), (0, 0, 0, 13, 0), (0, 0, 0, 0, 13),
+              (0, 0, 0, 0, 0))
+    for key in combos:
+        for o, v in zip(("force_tail_exp", "force_mid_exp", "force_far_exp", "force_vfar_exp", "force_ufar_exp"), key):
+            s.set_option(o, v)
+        s.forces()
+        out[key] = s.get_state()["F"]
+        tb[key], eps[key] = s.const("force_tail_bound"), s.const("force_error_eps")
+        assert s.const("force_tail_fixed_tiles") == 0
+    Fe = out[0, 0, 0, 0, 0]
+    assert eps[0, 0, 0, 0, 0] == 0 and tb[0, 0, 0, 0, 0] == 0      # (nothing approximate: nothing measured)
+    scale = 1e-13 * np.abs(Fe).max()
+    for key in combos[:-1]:
+        d = np.abs(out[key] - Fe).max()
+        print(f"{cfg} {key}: max_i |dF_i| {d:.3e}, measured bound {tb[key]:.3e}, eps {eps[key]:.2e}")
+        assert 0 < tb[key] <= eps[key]
+        assert d <= tb[key] + scale
+    s.close()
 
 
 def clustered_state(N0, L, frac, rc, seed=5):
@@ -326,6 +375,9 @@ def test_tail_bound_enforced_on_clustered_ions(cfg, orc):
     assert rt0 < L / 2
     fb = (s.const("force_far_bound") + s.const("force_vfar_bound") + s.const("force_ufar_bound")
           + s.const("force_mid_bound"))
+    # force_form_mode 1: the sums hold the forms' terms too, held to force_error_eps (eps + the tiers')
+    ea = s.const("force_error_eps") if s.const("force_form_measured") else eps
+    fb = max(fb, ea - eps)
     out = {}
     # A: the product defaults; the model's r_t is too small here
     s.forces()
@@ -334,15 +386,15 @@ def test_tail_bound_enforced_on_clustered_ions(cfg, orc):
     scale, rt1 = s.const("force_tail_scale"), s.const("force_skip_radius")
     print(f"{cfg}: N={s.N} L/2={L / 2:.3f} eps={eps:.0e}: model r_t {rt0:.3f}; tiles over eps {fixed:.0f}, largest "
           f"per-tile sum {raw:.3e}, bound met after the exact pass {tb:.3e}; r_t widened to {rt1:.3f} (scale {scale:.2f})")
-    assert fixed > 0 and raw > eps                      # the model radius was too small: caught
-    assert tb <= eps                                     # and enforced
+    assert fixed > 0 and raw > ea                       # the model radius was too small: caught
+    assert tb <= ea                                      # and enforced
     assert scale > 1 and rt0 < rt1 <= L / 2              # widened for the calls to come
     # B: the next call at the widened radius
     s.forces()
     out["B"] = s.get_state()["F"]
     fixed_b = s.const("force_tail_fixed_tiles") - fixed
     print(f"{cfg}: at r_t {rt1:.3f}: tiles over eps {fixed_b:.0f}, bound {s.const('force_tail_bound'):.3e}")
-    assert s.const("force_tail_bound") <= eps
+    assert s.const("force_tail_bound") <= ea
     # new positions of the same system keep the widened radius (a driver that uploads R every MD step
     # does not rerun the exact pass at every call)
     s.set_state(*state)
@@ -395,6 +447,57 @@ def test_tail_bound_enforced_on_clustered_ions(cfg, orc):
     print(f"{cfg}: {len(idx)} of the {len(loose)} ball ions against the compensated oracle: max |dF_i| {dA.max():.3e}, "
           f"max |dF_i| / P_i {(dA / P[idx]).max():.2e}")
     assert np.all(dA <= eps + fb + rnd[idx])
+
+
+@pytest.mark.gpu
+def test_form_bound_enforced_on_clustered_ions():
+    """force_form_mode 1 on a configuration its density model gets wrong (round 6): the 70k clustered
+    state with the tail off, so the sums hold the error-bounded forms' terms alone — the ions around the
+    ball see ~35,000 ions at the mid / far radii, far more than the model's uniform density.  The first
+    call must list the tiles whose sums exceed force_error_eps and recompute them exactly (k_tail_fix),
+    the host widens the model (force_tail_scale; every tier radius grows), and EVERY ion's force is
+    within force_error_eps of the exact sum to L/2 (the engine with every form off) + the rounding of
+    the sums (as in test_tail_bound_enforced_on_clustered_ions)"""
+    import mdqtplasmasims_amd as M
+    N0, _, frac, rc = CLUSTERED["70k"]
+    s = M.Simulation(N0=N0, seed=SEED, job=1, rng_mode=1)
+    L = s.const("L")
+    state = clustered_state(N0, L, frac, rc)
+    s.set_state(*state)
+    s.set_option("force_tail_exp", 0)
+    assert s.const("force_form_measured") == 1 and s.const("force_skip_radius") == L / 2
+    ea = s.const("force_error_eps")
+    rad0 = {k: s.const(f"force_{k}_radius") for k in ("mid", "far", "vfar", "ufar")}
+    assert ea > 0 and rad0["mid"] < L / 2
+    s.forces()
+    FA = s.get_state()["F"]                             # (a sync: the host reacts)
+    fixed, raw, tb = s.const("force_tail_fixed_tiles"), s.const("force_tail_raw_bound"), s.const("force_tail_bound")
+    rad1 = {k: s.const(f"force_{k}_radius") for k in ("mid", "far", "vfar", "ufar")}
+    print(f"70k clustered, forms only: eps {ea:.2e}; tiles over it {fixed:.0f}, largest sum {raw:.3e}, bound after "
+          f"the exact pass {tb:.3e}; radii {rad0} -> {rad1} (scale {s.const('force_tail_scale'):.0f})")
+    assert fixed > 0 and raw > ea and tb <= ea
+    assert s.const("force_tail_scale") > 1 and all(rad1[k] > rad0[k] for k in rad0 if rad0[k] < L / 2)
+    s.forces()
+    FB = s.get_state()["F"]
+    assert s.const("force_tail_bound") <= ea
+    for o in ("force_mid_exp", "force_far_exp", "force_vfar_exp", "force_ufar_exp"):
+        s.set_option(o, 0)
+    s.forces()
+    Fe = s.get_state()["F"]
+    lD = s.const("lDeb")
+    s.close()
+    from scipy.spatial import cKDTree
+    R = state[0]
+    r = cKDTree(R.T, boxsize=L).query(R.T, k=17)[0][:, 1:]
+    P = np.maximum(np.abs(Fe).max(axis=0), ((1 / r + 1 / lD) * np.exp(-r / lD) / r).sum(axis=1))
+    rnd = 1e-15 * P
+    dA, dB = np.abs(FA - Fe).max(axis=0), np.abs(FB - Fe).max(axis=0)
+    sharp = rnd < ea / 10
+    print(f"70k clustered, forms only: max_i |dF_i| first call {dA.max():.3e}, after widening {dB.max():.3e}; "
+          f"sharp check on {sharp.mean():.1%} of the ions (there: {dA[sharp].max():.3e}); elsewhere max |dF_i| / "
+          f"(eps + 1e-15 P_i) {(dA / (ea + rnd)).max():.3f}")
+    assert sharp.mean() > 0.4                            # (the ball's half of the ions: rounding-scale sums)
+    assert np.all(dA <= ea + rnd) and np.all(dB <= ea + rnd)
 
 
 @pytest.mark.gpu
@@ -687,8 +790,8 @@ def test_epotential_on_the_plan(cfg, orc):
     """Epotential() (SpeedUp:244-281) on the Newton-3 blocks with the force call's plan (round 6, VERDICT
     r05 item 2; option potential_plan 1): skip radius, sub-tile groups, the error-bounded pair forms for
     u = e^(-r/lDeb)/r and the enforced tail.  Since u(r) < lDeb g(r) and each form's relative error on u is
-    at most its error on the force, every U_i stays within lDeb x (the tail eps 1e-12 + the tiers' bounds)
-    of the sum to L/2 — checked on ~640 sampled ions against the oracle's compensated rows
+    at most its error on the force, every U_i stays within lDeb x (the tail eps 1e-12 + the tiers' bounds;
+    force_form_mode 1: the eps the call's measured sums are held to, force_error_eps) of the sum to L/2 — checked on ~640 sampled ions against the oracle's compensated rows
     (orc_potentials_index), beside the exact block path (potential_plan 0); Epot = sum U_i / 2N within
     1e-12 relative of the exact path's (north_star asks 1e-6 relative for energies)"""
     import mdqtplasmasims_amd as M
@@ -705,12 +808,14 @@ def test_epotential_on_the_plan(cfg, orc):
     e0 = s.Epotential()
     R = s.get_state()["R"]
     bounds = sum(s.const(k) for k in ("force_mid_bound", "force_far_bound", "force_vfar_bound", "force_ufar_bound"))
+    # force_form_mode 1: the force sums are held to force_error_eps (tail + tiers, measured and enforced)
+    per_ion = max(1e-12 + bounds, s.const("force_error_eps"))
     s.close()
     rng = np.random.default_rng(5)
     idx = sample_ions(N, 640, rng)
     G = orc.potentials_index(R, idx, L, lDeb, nthreads=threads())
     d1, d0 = np.abs(U1[idx] - G).max(), np.abs(U0[idx] - G).max()
-    gate = lDeb * (1e-12 + bounds) + 1e-13 * np.abs(G).max()
+    gate = lDeb * per_ion + 1e-13 * np.abs(G).max()
     rel = abs(e1 - e0) / abs(e0)
     print(f"{cfg}: N={N} sampled {len(idx)}: plan max|dU| = {d1:.3e} (gate {gate:.3e}), exact max|dU| = {d0:.3e}; "
           f"Epot plan {e1:.15g} exact {e0:.15g} rel {rel:.2e}; max|U_plan - U_exact| over all ions "

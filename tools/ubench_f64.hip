@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <vector>
 #include <algorithm>
+#include <stdlib.h>
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -18,7 +19,9 @@ __device__ __forceinline__ double dppd(double v) {
 
 // OP 0: fma f64; 1: add f64; 2: fma f32; 3: x = x + dpp_ror8(x) (2 movs + add); 4: rsq f64 + fma;
 // 5: mul f64; 6: packed fma f32 (v_pk_fma_f32); 7: packed mul f32 (v_pk_mul_f32); 8: exp f32 + fma f32;
-// 9: rsq f32 + fma f32
+// 9: rsq f32 + fma f32; (round 6, the block kernel's far forms) 10: cvt f64->f32->f64 + fma f64; 11: rndne f64 +
+// fma f64; 12: cvt_i32_f64 + ldexp f64; 13: exp f32 between conversions + fma f64 (the ultra-far form's 2^t);
+// 14: rsq f64 alone (x = rsq(x)); 15: ldexp f64 + fma f64
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int OP, int CH>
 __global__ __launch_bounds__(256) void k(double* out, long long* cyc, int iters, double a, double b) {
@@ -45,6 +48,12 @@ __global__ __launch_bounds__(256) void k(double* out, long long* cyc, int iters,
                 else if (OP == 7) xp[c] = xp[c] * f32x2{af, bf};
                 else if (OP == 8) xf[c] = fmaf(__builtin_amdgcn_exp2f(xf[c]), af, -bf);
                 else if (OP == 9) xf[c] = fmaf(__builtin_amdgcn_rsqf(xf[c]), af, bf);
+                else if (OP == 10) x[c] = fma((double)(float)x[c], a, b);
+                else if (OP == 11) x[c] = fma(__builtin_rint(x[c]), a, b);
+                else if (OP == 12) x[c] = ldexp(x[c], ((int)x[c] & 1) - 1);
+                else if (OP == 13) x[c] = fma((double)__builtin_amdgcn_exp2f((float)x[c]), a, -b);
+                else if (OP == 14) x[c] = __builtin_amdgcn_rsq(x[c]);
+                else if (OP == 15) x[c] = fma(ldexp(x[c], -1), a, b);
                 else x[c] = x[c] * a;
             }
         }
@@ -88,6 +97,24 @@ int main() {
     CHK(hipMalloc(&dout, (size_t)maxb * 256 * sizeof(double)));
     CHK(hipMalloc(&dcyc, (size_t)maxb * 256 * sizeof(long long)));
     const int it = 2000;
+    if (getenv("UBENCH_FORMS")) {                  // round 6: the far forms' instructions, throughput
+        run<0, 4>("fma_f64", 4, dout, dcyc, it);
+        run<5, 4>("mul_f64", 4, dout, dcyc, it);
+        run<1, 4>("add_f64", 4, dout, dcyc, it);
+        run<2, 4>("fma_f32", 4, dout, dcyc, it);
+        run<6, 4>("pkfma_f32", 4, dout, dcyc, it);
+        run<10, 4>("cvt2+fma", 4, dout, dcyc, it / 4);
+        run<11, 4>("rndne+fma", 4, dout, dcyc, it / 4);
+        run<12, 4>("cvti+ldexp", 4, dout, dcyc, it / 4);
+        run<15, 4>("ldexp+fma", 4, dout, dcyc, it / 4);
+        run<13, 4>("cvt-exp-cvt+fma", 4, dout, dcyc, it / 4);
+        run<14, 4>("rsq_f64", 4, dout, dcyc, it / 4);
+        run<4, 4>("rsq+fma", 4, dout, dcyc, it / 4);
+        run<8, 4>("exp+fma32", 4, dout, dcyc, it / 4);
+        run<9, 4>("rsq+fma32", 4, dout, dcyc, it / 4);
+        run<3, 4>("dpp+fma", 4, dout, dcyc, it);
+        return 0;
+    }
     for (int wps : {1, 2, 4}) {
         run<0, 1>("fma_f64", wps, dout, dcyc, it);
         run<0, 2>("fma_f64", wps, dout, dcyc, it);

@@ -140,13 +140,13 @@ int         mdqt_potentials_raw(int N, double L, double lDeb, const double* R, s
 
 /* ---- diagnostics / output ---- */
 /* Work census of the Newton-3 block force kernel (N > 65,536, spatial order; this rank's block
- * pairs) for the current positions — the tile pairs of forces() by the path they take: out[0..14)
+ * pairs) for the current positions — the tile pairs of forces() by the path they take: out[0..15)
  * lane-steps (64 per step of a wave: 16 steps per evaluated sub-tile group, 4,096 per skipped tile
- * pair, 2,560 on a diagonal tile), out[14..28) distinct ion pairs; classes 0 skipped beyond L/2,
+ * pair, 2,560 on a diagonal tile), out[15..30) distinct ion pairs; classes 0 skipped beyond L/2,
  * 1 skipped by the tail radius, 2 ragged last tile, 3 exact per-pair image, 4 exact uniform image,
  * 5 far per-pair, 6 far uniform, 7 very far per-pair, 8 very far uniform, 9 ultra far (f64)
  * uniform, 10 ultra far in f32, 11 skipped sub-tile groups of evaluated tile pairs, 12 mid
- * per-pair, 13 mid uniform.  n >= 28.  Not
+ * per-pair, 13 mid uniform, 14 ultra far (f64) with a one-axis per-pair image (round 6).  n >= 30.  Not
  * part of the reference's seam: the benchmark's roofline bookkeeping (VALU per evaluated pair). */
 int         mdqt_force_census(mdqt_ctx* c, double* out, int n);
 int         mdqt_epotential(mdqt_ctx* c, double* Epot);      /* Epotential(), SpeedUp:244-281   */

@@ -174,7 +174,8 @@ constexpr int BW = kN3BBlock;                       // tiles per block = waves p
 #define MDQT_N3B_AX1 1                              // the one-axis per-pair image (n3b_pack_class); 0: all three axes
 #endif
 #ifndef MDQT_N3B_AX1_LEVELS
-#define MDQT_N3B_AX1_LEVELS 0xE                     // bit x: far level x takes it (1 mid, 2 far, 3 very/ultra far)
+#define MDQT_N3B_AX1_LEVELS 0x1E                    // bit x: far level x takes it (1 mid, 2 far, 3 very far,
+                                                    // 4 ultra far and its f32 level: the f64 ultra-far form, round 6)
 #endif
 #if defined(MDQT_EXPT_CLS)
 // diagnostic build only: tile-pair classes of k_pairs_n3b (skip, per pair, uniform image)
@@ -695,11 +696,17 @@ __device__ __forceinline__ void n3b_tile_pair(const N3BArgs& a, const PairC& c, 
             const double sx = fma(-(double)((tw << 20) >> 24), a.L, xi);   // (0 on the varying axis:
             const double sy = fma(-(double)((tw << 12) >> 24), a.L, yi);   //  fma(-0, L, x) = x)
             const double sz = fma(-(double)((tw << 4) >> 24), a.L, zi);
-            const unsigned g3 = level_groups(word, 3) | level_groups(word, 4) | level_groups(word, 5),
-                           g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
             constexpr unsigned LV = MDQT_N3B_AX1_LEVELS;   // the levels that take it (bit x: level x)
+            // (levels 4 and 5 in the f64 ultra-far form with the one-axis image — the f32 form needs a
+            // uniform image; without LV bit 4 they ride in the very-far form)
+            const unsigned g45 = level_groups(word, 4) | level_groups(word, 5);
+            const unsigned g3 = level_groups(word, 3) | ((LV & 16u) ? 0u : g45), g4 = (LV & 16u) ? g45 : 0u,
+                           g2 = level_groups(word, 2), g1 = level_groups(word, 1), g0 = level_groups(word, 0);
             auto one_axis = [&](auto axc) {
                 constexpr int AX = decltype(axc)::value;
+                if ((LV & 16u) && g4)
+                    n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 4, AX>(false, g4, l, sx, sy, sz, mi, pj, mj,
+                                                                            ax, ay, az, tx, ty, tz, c);
                 if ((LV & 8u) && g3)
                     n3b_pair<VARIANT, GUARD, false, false, CUT, POT, 3, AX>(false, g3, l, sx, sy, sz, mi, pj, mj,
                                                                             ax, ay, az, tx, ty, tz, c);
@@ -1366,6 +1373,15 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
     }
 }
 
+// the AXP instance where tile pairs whose image varies on one axis can be evaluated: their pairs are >=
+// L/2 - (the two tiles' extents) apart on that axis, so only when the skip radius reaches within two tile
+// widths (L (64/N)^(1/3)) of L/2 (C3, C5: r_s = L/2; not N = 1M, r_s = 61 < 80.6 - 12.9).  A function of
+// the call's parameters alone: every rank of a sharded run, and every call of one configuration, takes
+// the same kernel.
+__host__ __device__ static bool n3b_axp(const N3BArgs& a) {
+    return a.ax1 && a.use_sort != 0 && a.Rskip > 0.5 * a.L - 2. * a.L * cbrt(64. / a.N);
+}
+
 // Census of the block kernel's work (diagnostic; bench.py's large lines): k_pairs_n3b's loop over
 // this rank's block pairs without the pair terms — every tile pair classified by n3b_classify and
 // its sub-tile groups by the same sub-block gaps, counted by the path the kernel takes, as
@@ -1375,7 +1391,8 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
 // image), 3 exact per-pair image, 4 exact uniform image, 5 far per-pair, 6 far uniform, 7 very far
 // per-pair (ultra far with a per-pair image included), 8 very far uniform, 9 ultra far uniform (f64),
 // 10 ultra far uniform in f32, 11 skipped sub-tile groups of evaluated tile pairs, 12 mid per-pair,
-// 13 mid uniform (round 4: appended, the earlier indices kept).  One workgroup
+// 13 mid uniform (round 4: appended, the earlier indices kept), 14 ultra far with a one-axis per-pair image
+// (round 6: the f64 ultra-far form on the AXP path).  One workgroup
 // per (block P, block distance db); thread (b, q) takes tile pair (16 P + q, 16 Q + b) as the
 // kernel's wave q at J-step b does.
 // bw (optional): the evaluated lane-steps (every class but the skipped ones) per block of this rank,
@@ -1384,7 +1401,7 @@ __global__ __launch_bounds__(256) void k_tail_fix(N3BArgs a, const unsigned long
 // instructions estimated from its groups' classes (kCensusValu: per wave-step of each form, from the ISA
 // counts in docs/FORCES.md) — bal[0] += sum over the waves, bal[1] += the busiest wave's, bal[2] += 1 per
 // J step with work: bal[1] / (bal[0] / 8) is the barrier-bound excess of the lock-step J loop
-__constant__ const unsigned kCensusValu[kCensus] = {0, 0, 52, 48, 39, 38, 31, 32, 27, 25, 9, 0, 44, 36};
+__constant__ const unsigned kCensusValu[kCensus] = {0, 0, 52, 48, 39, 38, 31, 32, 27, 25, 9, 0, 44, 36, 28};
 __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long long* __restrict__ out,
                                                     unsigned long long* __restrict__ bw,
                                                     unsigned long long* __restrict__ bal) {
@@ -1409,8 +1426,12 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
     if (!half && I < a.T && J < a.T && (db > 0 || J >= I)) {
         const N3BRadii rad = n3b_radii<1, false>(a);
         double g2;
-        const double4 t4 = n3b_classify<true>(a, 1. / a.L, rad, I, J, g2);
+        int sm = 0;
+        const double4 t4 = n3b_classify<true>(a, 1. / a.L, rad, I, J, g2, &sm);
         const bool diag = db == 0 && J == I;
+        // (a per-pair image on one axis, AXP instance: levels 4 and 5 in the f64 ultra-far form, class 14)
+        constexpr bool AX1U = MDQT_N3B_AX1 != 0 && (MDQT_N3B_AX1_LEVELS & 16u) != 0;
+        const bool ax1p = AX1U && n3b_axp(a) && ((n3b_pack_class(t4, sm) >> 28) & 3);
         const double nI = (double)min(64, a.N - I * 64), nJ = (double)min(64, a.N - J * 64);
         const bool rag = (a.N & 63) && (I == a.T - 1 || J == a.T - 1);
         const bool uni = ((int)t4.w & 1) != 0;
@@ -1418,7 +1439,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
         auto cls_of = [&](unsigned gl) {
             if (rag) return 2;
             if (uni) return gl == 5 ? 10 : gl == 4 ? 9 : gl == 3 ? 8 : gl == 2 ? 6 : gl == 1 ? 13 : 4;
-            return gl >= 3 ? 7 : gl == 2 ? 5 : gl == 1 ? 12 : 3;
+            return (ax1p && gl >= 4) ? 14 : gl >= 3 ? 7 : gl == 2 ? 5 : gl == 1 ? 12 : 3;
         };
         if (t4.w < 0.) {
             add(t4.w == -2. ? 1 : 0, 4096ull, (unsigned long long)(nI * nJ));
@@ -1652,6 +1673,8 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
             if (tmeas) {
                 const double rcut2 = a.Rcut * a.Rcut;
                 const float invl = (float)a.invlDeb, cf = (float)(a.invlDeb * kNegLog2e);
+                constexpr bool AX1U = FARF && MDQT_N3B_AX1 != 0 && (MDQT_N3B_AX1_LEVELS & 16u) != 0;
+                const bool ax1p = AX1U && n3b_axp(a) && ((pw >> 28) & 3);
 #pragma unroll
                 for (int sa = 0; sa < 4; ++sa)
 #pragma unroll
@@ -1659,8 +1682,10 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
                         const int d = (sb - sa) & 3;
                         const bool drop = cls == -2 || !((groups >> d) & 1u);
                         // the form the block kernel takes for the group (n3b_tile_pair): exact on a ragged
-                        // tile pair, levels >= 3 in the very-far form with a per-pair image
-                        const int e = (drop || !a.formm || rag) ? 0 : uni ? xs[d] : min(xs[d], 3);
+                        // tile pair; with a per-pair image levels >= 3 in the very-far form, but levels 4
+                        // and 5 in the f64 ultra-far form on the one-axis path (AXP instance, LV bit 4)
+                        const int e = (drop || !a.formm || rag) ? 0 : uni ? xs[d]
+                                    : (ax1p && xs[d] >= 4) ? 4 : min(xs[d], 3);
                         if ((drop || e > 0) && sg[sa][sb] < rcut2) {
                             const double gd = drop ? tail_g(sg[sa][sb], invl, cf) : form_term(sg[sa][sb], invl, cf, e);
                             gi[sa] += sub_count(a.N, 4 * J + sb) * gd;
@@ -1874,14 +1899,6 @@ static hipError_t launch_n3b_plan(const N3BArgs& a, int variant, hipStream_t s) 
     return hipGetLastError();
 }
 
-// the AXP instance where tile pairs whose image varies on one axis can be evaluated: their pairs are >=
-// L/2 - (the two tiles' extents) apart on that axis, so only when the skip radius reaches within two tile
-// widths (L (64/N)^(1/3)) of L/2 (C3, C5: r_s = L/2; not N = 1M, r_s = 61 < 80.6 - 12.9).  A function of
-// the call's parameters alone: every rank of a sharded run, and every call of one configuration, takes
-// the same kernel.
-static bool n3b_axp(const N3BArgs& a) {
-    return a.ax1 && a.use_sort != 0 && a.Rskip > 0.5 * a.L - 2. * a.L * cbrt(64. / a.N);
-}
 
 hipError_t launch_forces_n3b(const N3BArgs& a, int variant, double* out, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
                              hipEvent_t* marks) {

@@ -496,7 +496,7 @@ hipError_t launch_tail_max(const double* tailb, int T, double eps, unsigned long
 hipError_t launch_tail_fix(const N3BArgs& a, const unsigned long long* st, const int* list, double* out,
                            hipStream_t s, bool pot = false);
 // census of k_pairs_n3b's work by tile-pair class (mdqt_forces.hip k_n3b_census): out[2 kCensus]
-constexpr int kCensus = 14;
+constexpr int kCensus = 15;                 // (round 6: + 14 ufar_image)
 // tiles per block of the Newton-3 block kernel (= its waves per workgroup): 8 (round 4, A/B vs 16:
 // C3 -2.7 %, C5 -2.5 %, N = 1M -4.3 % per force call — three 8-wave workgroups per CU at 80 VGPRs
 // instead of two 16-wave ones at 64: shorter J-step barriers, fewer spills; 4: slower)

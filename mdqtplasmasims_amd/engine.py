@@ -341,7 +341,7 @@ class Simulation:
 
     CENSUS_CLASSES = ("skip_cut", "skip_tail", "ragged", "exact_image", "exact_uniform", "far_image",
                       "far_uniform", "vfar_image", "vfar_uniform", "ufar_uniform", "ufar32_uniform", "skip_sub",
-                      "mid_image", "mid_uniform")
+                      "mid_image", "mid_uniform", "ufar_image")
 
     def force_census(self):
         """the Newton-3 block kernel's work by tile-pair class for the current positions (this rank's

@@ -336,6 +336,15 @@ int         mdqt_force_block_work(mdqt_ctx* c, double* out, int n, int* nblocks)
  * instructions of all its tile pairs (per-form counts), out[1] 8 x the sum over J steps of the busiest
  * wave's, out[2] the J steps with work; out[1] / out[0] = the max-over-mean excess the J-step barriers cost */
 int         mdqt_force_jstep_balance(mdqt_ctx* c, double* out, int n);
+/* force_form_mode 1's tier radius for given parameters, without a context (host arithmetic only, for
+ * tests): level 1 far, 2 very far, 3 ultra far, 4 ultra far in f32, 5 mid; k the tier's exponent (eps =
+ * 10^-k); hi the skip radius the density model integrates to (L/2 without a tail); scale the model's
+ * scale (1 until a configuration exceeded its bound).  apriori 0: the model radius (the smallest r with
+ * 1.25 scale rho int_r^hi 4 pi (x + delta)^2 g(x) err(x) dx <= eps, capped by the a-priori radius);
+ * 1: force_form_mode 0's a-priori radius ((N - 1) g(r) err(r) <= eps, + the f32 tier's cutoff term);
+ * 2: the a-priori radius without that term.  *radius = L/2 when the tier is off; *bound its bound. */
+int         mdqt_tier_radius_model(int N, double L, double lDeb, int k, int level, double hi, double scale,
+                                   int apriori, double* radius, double* bound);
 int         mdqt_kernel_time_totals(mdqt_ctx* c, double* force_ms, int* nforce, double* substep_ms,
                                     int* nsub);
 /* the same with the Newton-3 block kernel (k_pairs_n3b, N > 65,536) timed on its own inside every

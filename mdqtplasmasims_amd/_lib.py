@@ -147,6 +147,8 @@ SIGNATURES = [
     ("mdqt_force_breakdown", C.c_int, [C.c_void_p, _dp, C.c_int]),
     ("mdqt_potential_rows", C.c_int, [C.c_void_p, _dp, C.c_int]),
     ("mdqt_force_jstep_balance", C.c_int, [C.c_void_p, _dp, C.c_int]),
+    ("mdqt_tier_radius_model", C.c_int, [C.c_int, C.c_double, C.c_double, C.c_int, C.c_int, C.c_double, C.c_double,
+                                         C.c_int, _dp, _dp]),
     ("mdqt_force_block_work", C.c_int, [C.c_void_p, _dp, C.c_int, C.POINTER(C.c_int)]),
     ("mdqt_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("mdqt_enable_timing_kinds", C.c_int, [C.c_void_p, C.c_int, C.c_int]),

@@ -1558,12 +1558,31 @@ static double form_model(double r, double hi, int N, double L, double lDeb, int 
     for (int i = 1; i < n; ++i) acc += (i & 1 ? 4. : 2.) * f(r + i * h);
     return rho * acc * h / 3.;
 }
+// the model radius of a tier (context-free; mdqt_tier_radius_model exports it for the CPU tests): the
+// smallest r with m s F(r) <= 10^-k on [0, hi], hi = r_t, capped by the a-priori radius; L/2 = off
+static double model_tier_radius(int N, double L, double lDeb, int k, int level, double hi, double sc, double* bound) {
+    const double Rcut = L / 2.;
+    *bound = 0.;
+    if (k <= 0 || N < 2) return Rcut;
+    double ba;
+    const double ra = far_radius_l(N, L, lDeb, k, level, &ba, false);
+    const double eps = pow(10., -k);
+    double lo = 0., up = hi;
+    for (int it = 0; it < 60 && up - lo > 1e-9 * Rcut; ++it) {
+        const double m = 0.5 * (lo + up);
+        if (m > 0 && kTailMargin * sc * form_model(m, hi, N, L, lDeb, level) <= eps) up = m; else lo = m;
+    }
+    double r = up, b = form_model(up, hi, N, L, lDeb, level);
+    if (r >= ra) { r = ra; b = ba; }                // the a-priori radius bounds any configuration
+    if (r >= hi) { r = Rcut; b = 0.; }              // (nothing evaluated that far: the tier is off)
+    *bound = b;
+    return r;
+}
 // a tier's radius (L/2: off) and bound: a priori (force_form_mode 0) or the model's (1; memoised per context)
 static double tier_radius(const mdqt_ctx* s, int k, int level, double* bound) {
     if (!form_measured(s)) return far_radius_l(s->N, s->L, s->lDeb, k, level, bound);
-    const double Rcut = s->L / 2.;
     *bound = 0.;
-    if (k <= 0 || s->N < 2) return Rcut;
+    if (k <= 0 || s->N < 2) return s->L / 2.;
     const double sc = s->tail_scale;
     double* key = s->form_key[level];
     if (key[0] == s->N && key[1] == s->L && key[2] == s->lDeb && key[3] == k && key[4] == s->tail_exp && key[5] == sc) {
@@ -1572,21 +1591,25 @@ static double tier_radius(const mdqt_ctx* s, int k, int level, double* bound) {
     }
     double tb;
     const double hi = tail_radius_sum(s, &tb);      // r_t (L/2 where the tail is exact)
-    double ba;
-    const double ra = far_radius_l(s->N, s->L, s->lDeb, k, level, &ba, false);
-    const double eps = pow(10., -k);
-    double lo = 0., up = hi;
-    for (int it = 0; it < 60 && up - lo > 1e-9 * Rcut; ++it) {
-        const double m = 0.5 * (lo + up);
-        if (m > 0 && kTailMargin * sc * form_model(m, hi, s->N, s->L, s->lDeb, level) <= eps) up = m; else lo = m;
-    }
-    double r = up, b = form_model(up, hi, s->N, s->L, s->lDeb, level);
-    if (r >= ra) { r = ra; b = ba; }                // the a-priori radius bounds any configuration
-    if (r >= hi) { r = Rcut; b = 0.; }              // (nothing evaluated that far: the tier is off)
+    double b;
+    const double r = model_tier_radius(s->N, s->L, s->lDeb, k, level, hi, sc, &b);
     key[0] = s->N; key[1] = s->L; key[2] = s->lDeb; key[3] = k; key[4] = s->tail_exp; key[5] = sc;
     s->form_val[level][0] = r; s->form_val[level][1] = b;
     *bound = b;
     return r;
+}
+// C ABI for the CPU tests (no device needed): a tier's model radius and bound for given parameters,
+// level as far_err (1 far, 2 very far, 3 ultra far, 4 ultra far in f32, 5 mid); hi = the skip radius
+// the integral ends at (L/2 without a tail); apriori 1: force_form_mode 0's a-priori radius instead, 2: the
+// a-priori radius without the f32 tier's cutoff term (the cap the model radius takes)
+extern "C" int mdqt_tier_radius_model(int N, double L, double lDeb, int k, int level, double hi, double scale,
+                                      int apriori, double* radius, double* bound) {
+    if (!radius || !bound || N < 1 || !(L > 0.) || !(lDeb > 0.) || level < 1 || level > 5 || !(hi > 0.) ||
+        !(scale > 0.) || apriori < 0 || apriori > 2)
+        return -1;
+    *radius = apriori ? far_radius_l(N, L, lDeb, k, level, bound, apriori == 1)
+                      : model_tier_radius(N, L, lDeb, k, level, std::min(hi, L / 2.), scale, bound);
+    return 0;
 }
 // the model's per-sub-tile sum at the current radii — the tail's where r_t < L/2, + the tiers' evaluated
 // inside r_t (force_form_mode 1) — that tail_check compares the measured sums with

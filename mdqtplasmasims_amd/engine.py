@@ -406,4 +406,17 @@ class Simulation:
         return d
 
 
-__all__ = ["forces_raw", "potentials_raw", "Simulation", "MdqtError", "default_params", "device_count", "slab", "NBINS", "NUM_STATES"]
+def tier_radius_model(N: int, L: float, lDeb: float, k: int, level: int, hi: float | None = None,
+                      scale: float = 1.0, apriori: int = 0):
+    """force_form_mode 1's radius of a pair-form tier and its bound, for given parameters, without a
+    context or device (include/mdqt.h mdqt_tier_radius_model): level 1 far, 2 very far, 3 ultra far, 4
+    ultra far in f32, 5 mid; hi the skip radius the model integrates to (default L/2); apriori 1: force_form_mode
+    0's radius, 2: the a-priori cap the model takes"""
+    r, b = C.c_double(), C.c_double()
+    check(lib().mdqt_tier_radius_model(int(N), float(L), float(lDeb), int(k), int(level),
+                                       float(L / 2 if hi is None else hi), float(scale), int(apriori),
+                                       C.byref(r), C.byref(b)), "tier_radius_model")
+    return r.value, b.value
+
+
+__all__ = ["forces_raw", "potentials_raw", "tier_radius_model", "Simulation", "MdqtError", "default_params", "device_count", "slab", "NBINS", "NUM_STATES"]

@@ -113,6 +113,23 @@ def main(cfg="C5", samples=20000, seed=1):
     for d in range(4):
         diag += act[:, np.arange(4), (np.arange(4) + d) % 4].any(axis=1)
     match = matchings(act)
+    # (round 6) 8-ion quadrants: group d's 16 steps as two 8-step halves, half h covering the quadrant
+    # pairs (I half e, J half (e + h) mod 2) of each of the 4 lane rows; a half runs iff one of its 8
+    # quadrant pairs has 8-ion boxes < r_s apart
+    c8, h8 = boxes(Rs, 8, L)
+    a8 = 8 * I[:, None] + np.arange(8)[None, :]
+    b8 = 8 * J[:, None] + np.arange(8)[None, :]
+    q8 = gap2(c8[:, a8][:, :, :, None], h8[:, a8][:, :, :, None], c8[:, b8][:, :, None, :], h8[:, b8][:, :, None, :], L)
+    qact = (q8 < rs * rs) & run[:, None, None]        # [n, 8, 8]: I eighth 2a + e, J eighth 2b + f
+    quad = np.zeros(n)
+    for d in range(4):
+        for h in range(2):
+            on = np.zeros(n, dtype=bool)
+            for a_ in range(4):
+                b_ = (a_ + d) % 4
+                for e in range(2):
+                    on |= qact[:, 2 * a_ + e, 2 * b_ + (e + h) % 2]
+            quad += on
     # per rotation step s of the present kernel: lane l (sub-tile l // 16) meets J index (l + s) % 64
     l = np.arange(64)
     steps = np.zeros(n)
@@ -129,7 +146,8 @@ def main(cfg="C5", samples=20000, seed=1):
     tot = n * 4096.0
     print(f"{cfg}: N={N} L={L:.3f} r_s={rs:.3f}; {n} tile pairs sampled; evaluated tile pairs {run.mean():.3f}")
     print(f"  lane-steps per pair: now {run.sum() * 4096 / tot:.3f}, per-step ballot {steps.sum() * 64 / tot:.3f}, "
-          f"cyclic diagonals {diag.sum() * 1024 / tot:.3f}, matchings {match.sum() * 1024 / tot:.3f}")
+          f"cyclic diagonals {diag.sum() * 1024 / tot:.3f}, matchings {match.sum() * 1024 / tot:.3f}, "
+          f"8-ion quadrant halves {quad.sum() * 512 / tot:.3f}")
     print(f"  pairs inside L/2 among the evaluated tile pairs: {frac_in:.3f} "
           f"(all pairs inside L/2: {np.pi / 6:.3f}); inside r_s: of all pairs "
           f"{4 * np.pi / 3 * rs ** 3 / L ** 3:.3f}")

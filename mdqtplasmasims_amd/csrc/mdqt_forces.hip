@@ -1056,8 +1056,17 @@ __constant__ const unsigned kN3BMatchings[105] = {0xfac688, 0xf74688, 0xd7c688, 
 // a sub-tile group's estimated VALU instructions per lane (16 steps; the pairing's weights per wave-step of
 // each pair form — exact, mid, far, very far, ultra far, f32 ultra far — uniform image / per-pair image; the
 // ragged tile's exact form)
+#ifndef MDQT_N3B_PAIR_COST
+#define MDQT_N3B_PAIR_COST 0
+#endif
 __device__ __forceinline__ unsigned n3b_pair_cost(int level, bool uni, bool rag) {
+#if MDQT_N3B_PAIR_COST
+    // (round 6 A/B) issue slots per step from the forms' instruction costs (profiles/r06f_ubench_forms.txt:
+    // v_rsq_f64 ~3.3 slots, f32 transcendentals ~2.4, plain f32 0.5)
+    constexpr unsigned wu[6] = {43u, 41u, 38u, 33u, 28u, 18u}, wi[6] = {50u, 47u, 44u, 38u, 31u, 31u};
+#else
     constexpr unsigned wu[6] = {39u, 36u, 31u, 27u, 25u, 9u}, wi[6] = {48u, 44u, 38u, 32u, 32u, 32u};
+#endif
     return 16u * (rag ? 52u : uni ? wu[level] : wi[level]);
 }
 

@@ -723,6 +723,9 @@ def compact_secondary(name, v):
     r = v.get("roofline")
     if isinstance(r, dict):
         c["roofline"] = _pick(r, LINE_ROOF_KEYS)
+        pm = r.get("pmc")
+        if isinstance(pm, dict) and pm.get("status") == "ok" and "valu_busy_frac" in pm:
+            c["roofline"]["valu_busy_frac"] = pm["valu_busy_frac"]   # (the committed PMC summary of this tree)
     p = v.get("parity")
     if isinstance(p, dict):
         c["parity_ok"] = p.get("ok", None)
@@ -971,6 +974,14 @@ def large_roofline(cfg, census, f_avg, k_avg, N, world, imbalance=None, pairs=0)
              valu_per_evaluated_pair=e["SQ_INSTS_VALU"] / w, salu_per_evaluated_pair=e.get("SQ_INSTS_SALU", 0) / w,
              lds_per_evaluated_pair=e.get("SQ_INSTS_LDS", 0) / w,
              valu_issue_frac=e["SQ_INSTS_VALU"] * 4.0 / (1024.0 * cyc) if cyc else None)
+    if cyc and "SQ_ACTIVE_INST_VALU" in e:
+        # the hardware's VALU occupancy (rocprofv3's VALUBusy: quad-cycles summed over the SIMDs / (CUs x the
+        # kernel's cycles)) — each instruction at its real cost (the quarter-rate v_rsq_f64, the f32
+        # transcendentals), where valu_issue_frac prices every VALU instruction at 4 cycles
+        p.update(valu_busy_frac=e["SQ_ACTIVE_INST_VALU"] / (256.0 * cyc),
+                 valu_dual_issue_frac=e.get("SQ_ACTIVE_INST_VALU2", 0.0) / (256.0 * cyc),
+                 trans_per_valu=(e.get("SQ_INSTS_VALU_TRANS_F64", 0.0) + e.get("SQ_INSTS_VALU_TRANS_F32", 0.0))
+                 / e["SQ_INSTS_VALU"])
     if e.get("duration_us"):
         ks = e["duration_us"] * 1e-6
         p.update(kernel_us=e["duration_us"], clock_ghz=cyc / ks / 1e9 if cyc else None,

@@ -582,23 +582,20 @@ __device__ __forceinline__ double form_term(double g2, float invl, float cf, int
     const float g = ((ri + invl) * ex) * ri;
     return (double)(g * fmaf(r * invl, kFormA[e], kFormB[e])) * (1. + 0x1p-10);
 }
-// force_form_mode 1: the squared far distance of sub-tiles s and u under a uniform image's shifts nL (the
-// block kernel's xi - n L - xj): every pair's |dx| per axis is at most |c_s - c_u - n L| + h_s + h_u
-__device__ __forceinline__ double sub_far2(const double* __restrict__ SB, int T4, int s, int u, const double* nL) {
+// force_form_mode 1: an upper bound on the squared distance of any pair of boxes s and u in the minimum
+// image — a uniform-image tile pair's pairs are each at their minimum image in the block kernel (its shift
+// is every pair's rint(dx / L)), and per axis min_k |x_i - x_j - k L| <= |mi(c_s - c_u)| + h_s + h_u, whatever
+// frame the boxes' centres were taken in (a box is the min / max about its first ion, k_tile_boxes)
+__device__ __forceinline__ double sub_far2(const double* __restrict__ SB, int T4, int s, int u, double L, double invL) {
     double f2 = 0.;
 #pragma unroll
     for (int c3 = 0; c3 < 3; ++c3) {
-        const double d = fabs((SB[(size_t)c3 * T4 + s] - SB[(size_t)c3 * T4 + u]) - nL[c3]) +
-                         (SB[(size_t)(3 + c3) * T4 + s] + SB[(size_t)(3 + c3) * T4 + u]);
-        f2 = fma(d, d, f2);
+        double d = SB[(size_t)c3 * T4 + s] - SB[(size_t)c3 * T4 + u];
+        d = fma(-__builtin_rint(d * invL), L, d);
+        const double f = fabs(d) + (SB[(size_t)(3 + c3) * T4 + s] + SB[(size_t)(3 + c3) * T4 + u]);
+        f2 = fma(f, f, f2);
     }
     return f2;
-}
-// the uniform image's shifts n L of a class word (n3b_pack_class; the block kernel's nsh)
-__device__ __forceinline__ void class_shifts(int pw, double L, double* nL) {
-    nL[0] = (double)((pw << 20) >> 24) * L;
-    nL[1] = (double)((pw << 12) >> 24) * L;
-    nL[2] = (double)((pw << 4) >> 24) * L;
 }
 // a tile pair's class and uniform-image multiples in one LDS word: bits 0-3 class + 2, 4-11 / 12-19 /
 // 20-27 n_x, n_y, n_z (signed); a uniform image with a multiple beyond +-127 (positions that far
@@ -1457,7 +1454,6 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
         } else {
             const int T4 = 4 * a.T;
             const double hj2 = raw_half2(a.boxes, a.T, J);
-            const double nL[3] = {t4.x * a.L, t4.y * a.L, t4.z * a.L};   // (the uniform image's; formm)
             unsigned act = 0, mm = 0, mf = 0, mv = 0, mu = 0, m32 = 0;
             double np[4] = {0., 0., 0., 0.};       // ion pairs per group
             for (int sa = 0; sa < 4; ++sa)
@@ -1470,7 +1466,7 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
                     if (sg > rad.rv2) mv |= bit;
                     if (sg > rad.ru2) mu |= bit;
                     if (sg > rad.ru32 && sg > 4. * hj2 &&   // (k_n3b_plan's level 5)
-                        (!a.formm || !uni || sub_far2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, nL) < a.u32lim2))
+                        (!a.formm || !uni || sub_far2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, 1. / a.L) < a.u32lim2))
                         m32 |= bit;
                     np[(sb - sa) & 3] += sub_count(a.N, 4 * I + sa) * sub_count(a.N, 4 * J + sb);
                 }
@@ -1654,21 +1650,17 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
             int xs[4];                              // the groups' levels (the measured form bound)
             // (formm) the whole tile pair within u32lim2 under its image — tile boxes: every sub-block is
             bool tile_in = false;
-            if (FARF && a.formm && gmax > rad.ru32 && uni) {
-                double nL[3];
-                class_shifts(pw, a.L, nL);
-                tile_in = sub_far2(a.boxes, a.T, I, J, nL) < a.u32lim2;   // ([12][T]: centers, half extents first)
-            }
+            if (FARF && a.formm && gmax > rad.ru32 && uni)
+                tile_in = sub_far2(a.boxes, a.T, I, J, a.L, invL) < a.u32lim2;   // ([12][T]: centers, half extents first)
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 int x = !FARF ? 0 : n3b_level(gm[d], rad);
                 if (x == 5 && !(gm[d] > hj4)) x = 4;
                 if (x == 5 && a.formm && uni && !tile_in) {   // f32 only where no pair can reach the cutoff (u32lim2)
-                    double nL[3];
-                    class_shifts(pw, a.L, nL);
                     double f2 = 0.;
 #pragma unroll
-                    for (int sa = 0; sa < 4; ++sa) f2 = fmax(f2, sub_far2(a.subboxes, T4, 4 * I + sa, 4 * J + ((sa + d) & 3), nL));
+                    for (int sa = 0; sa < 4; ++sa)
+                        f2 = fmax(f2, sub_far2(a.subboxes, T4, 4 * I + sa, 4 * J + ((sa + d) & 3), a.L, invL));
                     if (!(f2 < a.u32lim2)) x = 4;
                 }
                 xs[d] = x;

@@ -458,8 +458,8 @@ struct N3BArgs {
                         // error-bounded form, n_b g(gap) err_form(gap) — the forms' measured bound, enforced
                         // with the tail's (k_tail_max, k_tail_fix); the tier radii come from a density model
     double u32lim2;     // formm: (Rcut (1 - 2^-20))^2 — a group takes the f32 ultra-far form only if every
-                        // pair of it is closer (its far distance under the tile pair's image), so the f32
-                        // r^2 never decides the cutoff (no a-priori cutoff term)
+                        // pair of it is closer (its boxes' far distance in the minimum image, sub_far2), so
+                        // the f32 r^2 never decides the cutoff (no a-priori cutoff term)
     const double* subboxes;   // [6][4T]: the 16-ion sub-tiles' centers and half extents (use_sort)
     uint2* plan;        // force calls in spatial order: [(Phi - Plo) nd][256] tile-pair words, then
                         // [(Phi - Plo) nd] J-step masks (.x), written by k_n3b_plan (launch_forces_n3b)

@@ -1059,7 +1059,8 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
     ru, ufar = sim.const("force_ufar_radius"), sim.const("force_ufar_bound")
     ru32 = sim.const("force_ufar32_radius")
     tail_eps = 10.0 ** -12                          # force_tail_exp default
-    fmode = int(sim.const("force_form_measured"))   # force_form_mode 1: the sums hold the forms' terms too
+    fmode = int(sim.const("force_form_measured"))   # force_form_mode >= 1: the sums hold the forms' terms too
+    fshare = fmode and int(sim.const("force_form_mode")) == 2
     err_eps = sim.const("force_error_eps")          # what they are held to (tail eps + 1e-13 per active tier)
     bound_met = bool((fmode and tail <= err_eps) or (not fmode and (rt >= L / 2 or (tmode == 1 and tail <= tail_eps)
                                                                     or tmode == 0)))
@@ -1146,7 +1147,8 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
             "parity": parity if check else {"note": "world 1: this line is the reference the sharded runs are checked against"},
             "force_tail": {"skip_radius": rt, "half_box": L / 2, "bound": tail, "bound_met": bound_met,
                            "tail_mode": "measured+enforced" if tmode == 1 else "a priori",
-                           "form_mode": "measured+enforced" if fmode else "a priori", "error_eps": err_eps,
+                           "form_mode": ("measured+enforced, shared budget" if fshare else "measured+enforced") if fmode
+                           else "a priori", "error_eps": err_eps,
                            "tail_model_bound": tmodel if tmode == 1 else None,
                            "tiles_over_eps_fixed": fixed, "largest_tile_sum_before_fix": raw,
                            "mid_radius": rm, "mid_bound": mid,
@@ -1162,7 +1164,9 @@ def sharded_run(cfg, steps, rank, world, local, dist, barrier):
                                    "form_mode measured+enforced (round 6): the tiers' radii from a density model, the sums "
                                    "also hold n g(gap) err_form(gap) of every sub-block evaluated in an error-bounded form, "
                                    "held to error_eps, and bound (their largest after the exact pass) is every ion's total "
-                                   "(the *_bound entries are then the model's). fp64 rates count all N(N-1)/2 pairs (SURVEY 8d)"},
+                                   "(the *_bound entries are then the model's); shared budget (force_form_mode 2): where the tail skips "
+                                   "nothing its unused 1e-12 is split among the active tiers, so error_eps is the same "
+                                   "1.5e-12 per ion as where the tail is active. fp64 rates count all N(N-1)/2 pairs (SURVEY 8d)"},
             "substeps_ms_per_md_step": s_ms / max(ns, 1) if ns else None}
 
 

@@ -262,7 +262,10 @@ int         mdqt_get_spin_up_list(mdqt_ctx* c, int* tags, int* n_up);
  *                     configuration exceeded it; the f32 form only for groups whose pairs are all
  *                     closer than L/2 (1 - 2^-20).  "force_tail_bound" is then the measured bound on
  *                     every ion's total deviation from the exact sum to L/2, the *_bound
- *                     constants the model's; "force_form_measured" 1 where mode 1 applies.  0 = the
+ *                     constants the model's; "force_form_measured" 1 where mode 1 applies.  2 = as
+ *                     1, and where the tail skips nothing (r_t = L/2) the active tiers share its
+ *                     unused 10^-force_tail_exp equally (each tier's eps 10^-k + that share), so
+ *                     every configuration's per-ion total is the one an active tail has.  0 = the
  *                     a-priori radii above
  *   "qt_enabled":     1 = qstep() runs in the substeps, 0 = skipped (t still advances): the
  *                     pumping programs' pump window (randomFrozenStartTag408Linear.cpp main)

@@ -73,7 +73,7 @@ inline cx cx_conj(cx a) { return {a.re, -a.im}; }
 #define MDQT_TAIL_MODE 1
 #endif
 #ifndef MDQT_FORM_MODE
-#define MDQT_FORM_MODE 1
+#define MDQT_FORM_MODE 2
 #endif
 struct mdqt_ctx {
     mdqt_params p;
@@ -164,7 +164,8 @@ struct mdqt_ctx {
     // error-bounded form adds n_b g(gap) err_form(gap) to its sub-tiles' sums (k_n3b_plan), a tile whose
     // sum exceeds the call's eps (the tail's where r_t < L/2, + 10^-k per active tier: error_eps) is
     // recomputed exactly (k_tail_fix), and the radii come from the density model of those sums
-    // (tier_radius) — so every ion meets that eps whatever the configuration
+    // (tier_radius) — so every ion meets that eps whatever the configuration; 2 as 1, and where the tail
+    // is exact (r_t = L/2) the tiers share its unused 10^-tail_exp (tier_eps): the same total per ion
     int form_mode = MDQT_FORM_MODE;
     mutable double form_key[6][6] = {}, form_val[6][2] = {};   // tier_radius memo by level (N, L, lDeb, k, tail_exp, scale)
     uint32_t* dKeys = nullptr;     // [2][N] Hilbert keys, sorted keys
@@ -1545,8 +1546,22 @@ static double far_radius(int N, double L, double lDeb, int k, double* bound) {
 // every tile's sum and k_tail_fix enforces the call's eps (error_eps).
 // (force_sort 1 and 2 alike: 2 runs the same plan without skipping, and must give the same forms)
 static bool form_measured(const mdqt_ctx* s) {
-    return s->form_mode == 1 && s->use_n3b && s->tail_mode == 1 && s->sort_mode >= 1 && s->force_variant == 1 &&
+    return s->form_mode >= 1 && s->use_n3b && s->tail_mode == 1 && s->sort_mode >= 1 && s->force_variant == 1 &&
            !s->guard;
+}
+// a tier's eps (k > 0): 10^-k, + (force_form_mode 2, where the tail skips nothing: r_t = L/2) an equal
+// share of the tail's 10^-tail_exp among the tiers with k > 0 — the per-ion total stays 10^-tail_exp + sum
+// 10^-k, as where the tail is active
+static double tier_eps(const mdqt_ctx* s, int k) {
+    if (k <= 0) return 0.;
+    double e = pow(10., -k);
+    double tb;
+    if (s->form_mode == 2 && form_measured(s) && s->tail_exp > 0 && tail_radius_sum(s, &tb) >= s->L / 2.) {
+        const int n = (MDQT_EXP_TAB && s->mid_exp > 0) + (s->far_exp > 0) + (s->vfar_exp > 0) +
+                      (s->ufar_exp > 0) * (MDQT_UFAR32 ? 2 : 1);
+        e += pow(10., -s->tail_exp) / n;
+    }
+    return e;
 }
 static double form_model(double r, double hi, int N, double L, double lDeb, int level) {
     const double rho = N / (L * L * L), delta = 2. * cbrt(16. / rho);
@@ -1559,14 +1574,15 @@ static double form_model(double r, double hi, int N, double L, double lDeb, int 
     return rho * acc * h / 3.;
 }
 // the model radius of a tier (context-free; mdqt_tier_radius_model exports it for the CPU tests): the
-// smallest r with m s F(r) <= 10^-k on [0, hi], hi = r_t, capped by the a-priori radius; L/2 = off
-static double model_tier_radius(int N, double L, double lDeb, int k, int level, double hi, double sc, double* bound) {
+// smallest r with m s F(r) <= eps (10^-k, or tier_eps) on [0, hi], hi = r_t, capped by the a-priori
+// radius of 10^-k (its bound <= 10^-k <= eps); L/2 = off
+static double model_tier_radius(int N, double L, double lDeb, int k, double eps, int level, double hi, double sc,
+                                double* bound) {
     const double Rcut = L / 2.;
     *bound = 0.;
     if (k <= 0 || N < 2) return Rcut;
     double ba;
     const double ra = far_radius_l(N, L, lDeb, k, level, &ba, false);
-    const double eps = pow(10., -k);
     double lo = 0., up = hi;
     for (int it = 0; it < 60 && up - lo > 1e-9 * Rcut; ++it) {
         const double m = 0.5 * (lo + up);
@@ -1583,17 +1599,18 @@ static double tier_radius(const mdqt_ctx* s, int k, int level, double* bound) {
     if (!form_measured(s)) return far_radius_l(s->N, s->L, s->lDeb, k, level, bound);
     *bound = 0.;
     if (k <= 0 || s->N < 2) return s->L / 2.;
-    const double sc = s->tail_scale;
+    const double sc = s->tail_scale, eps = tier_eps(s, k);
     double* key = s->form_key[level];
-    if (key[0] == s->N && key[1] == s->L && key[2] == s->lDeb && key[3] == k && key[4] == s->tail_exp && key[5] == sc) {
+    if (key[0] == s->N && key[1] == s->L && key[2] == s->lDeb && key[3] == eps && key[4] == s->tail_exp &&
+        key[5] == sc) {
         *bound = s->form_val[level][1];
         return s->form_val[level][0];
     }
     double tb;
     const double hi = tail_radius_sum(s, &tb);      // r_t (L/2 where the tail is exact)
     double b;
-    const double r = model_tier_radius(s->N, s->L, s->lDeb, k, level, hi, sc, &b);
-    key[0] = s->N; key[1] = s->L; key[2] = s->lDeb; key[3] = k; key[4] = s->tail_exp; key[5] = sc;
+    const double r = model_tier_radius(s->N, s->L, s->lDeb, k, eps, level, hi, sc, &b);
+    key[0] = s->N; key[1] = s->L; key[2] = s->lDeb; key[3] = eps; key[4] = s->tail_exp; key[5] = sc;
     s->form_val[level][0] = r; s->form_val[level][1] = b;
     *bound = b;
     return r;
@@ -1608,7 +1625,7 @@ extern "C" int mdqt_tier_radius_model(int N, double L, double lDeb, int k, int l
         !(scale > 0.) || apriori < 0 || apriori > 2)
         return -1;
     *radius = apriori ? far_radius_l(N, L, lDeb, k, level, bound, apriori == 1)
-                      : model_tier_radius(N, L, lDeb, k, level, std::min(hi, L / 2.), scale, bound);
+                      : model_tier_radius(N, L, lDeb, k, pow(10., -k), level, std::min(hi, L / 2.), scale, bound);
     return 0;
 }
 // the model's per-sub-tile sum at the current radii — the tail's where r_t < L/2, + the tiers' evaluated
@@ -1627,15 +1644,15 @@ static double model_total(const mdqt_ctx* s) {
     return b;
 }
 // the eps a force call's per-sub-tile sums are held to (k_tail_max): the tail's where r_t < L/2, plus
-// (force_form_mode 1) 10^-k of every tier evaluated inside r_t
+// (force_form_mode >= 1) the eps of every tier evaluated inside r_t (tier_eps)
 static double error_eps(const mdqt_ctx* s, const N3BArgs& a) {
     double e = a.Rskip < a.Rcut ? pow(10., -s->tail_exp) : 0.;
     if (a.formm) {
-        if (MDQT_EXP_TAB && a.Rmid < a.Rskip && s->mid_exp > 0) e += pow(10., -s->mid_exp);
-        if (a.Rfar < a.Rskip && s->far_exp > 0) e += pow(10., -s->far_exp);
-        if (a.Rvfar < a.Rskip && s->vfar_exp > 0) e += pow(10., -s->vfar_exp);
-        if (a.Rufar < a.Rskip && s->ufar_exp > 0) e += pow(10., -s->ufar_exp);
-        if (MDQT_UFAR32 && a.Rufar32 < a.Rskip && s->ufar_exp > 0) e += pow(10., -s->ufar_exp);
+        if (MDQT_EXP_TAB && a.Rmid < a.Rskip) e += tier_eps(s, s->mid_exp);
+        if (a.Rfar < a.Rskip) e += tier_eps(s, s->far_exp);
+        if (a.Rvfar < a.Rskip) e += tier_eps(s, s->vfar_exp);
+        if (a.Rufar < a.Rskip) e += tier_eps(s, s->ufar_exp);
+        if (MDQT_UFAR32 && a.Rufar32 < a.Rskip) e += tier_eps(s, s->ufar_exp);
     }
     return e;
 }
@@ -3225,7 +3242,8 @@ extern "C" int mdqt_set_option(mdqt_ctx* s, const char* name, int value) {
         return 0;
     }
     if (!strcmp(name, "force_form_mode")) {            // the tiers' radii: 0 a priori, 1 measured and enforced
-        if (value < 0 || value > 1) return fail("force_form_mode must be 0 (a priori) or 1 (measured)");
+        if (value < 0 || value > 2)
+            return fail("force_form_mode must be 0 (a priori), 1 (measured) or 2 (measured, sharing an exact tail's eps)");
         if (value != s->form_mode && (settle_forces(s) || tail_reset(s))) return -1;
         s->form_mode = value;
         return 0;

@@ -284,29 +284,38 @@ def test_error_bounded_tail_and_far_form(cfg):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["C4", "C5"])
 def test_form_bound_measured_and_enforced(cfg):
-    """force_form_mode 1 (round 6, the default): the tiers' radii from the density model of the sums the
+    """force_form_mode 1 and 2 (round 6; 2 the default): the tiers' radii from the density model of the sums the
     plan measures (mdqt_engine.cpp tier_radius) — below the a-priori radii of mode 0 — and every
     sub-block evaluated in an error-bounded form adding n_b g(gap) err_form(gap) to its sub-tiles' sums
     (k_n3b_plan), which k_tail_max holds to force_error_eps (the tail's eps where r_t < L/2 + 10^-13 per
-    active tier), recomputing any tile over it exactly.  On EVERY ion, against the same engine with the
+    active tier; mode 2, where the tail skips nothing, each tier + a fifth of the tail's 1e-12), recomputing
+    any tile over it exactly.  On EVERY ion, against the same engine with the
     tail and every form off: |dF_i| <= the measured bound of that call (force_tail_bound, the largest
     per-sub-tile sum after the exact pass) + the summation-order rounding, for the defaults and each
     tier alone; the measured bound <= force_error_eps; on these uniform configurations no tile over it"""
     import mdqtplasmasims_amd as M
     s = M.Simulation(seed=SEED, job=1, rng_mode=1, **CONFIGS[cfg]).init()
     L = s.const("L")
-    assert s.const("force_form_mode") == 1 and s.const("force_form_measured") == 1
+    assert s.const("force_form_mode") == 2 and s.const("force_form_measured") == 1
     tiers = ("mid", "far", "vfar", "ufar", "ufar32")
-    r1 = {k: s.const(f"force_{k}_radius") for k in tiers}
+    r2, e2 = {k: s.const(f"force_{k}_radius") for k in tiers}, s.const("force_error_eps")
     s.set_option("force_form_mode", 0)
     r0 = {k: s.const(f"force_{k}_radius") for k in tiers}
     s.set_option("force_form_mode", 1)
-    print(f"{cfg}: radii form mode 1 {dict((k, round(v, 3)) for k, v in r1.items())}, mode 0 "
-          f"{dict((k, round(v, 3)) for k, v in r0.items())}, L/2 {L / 2:.3f}; force_error_eps "
-          f"{s.const('force_error_eps'):.2e}")
+    r1, e1 = {k: s.const(f"force_{k}_radius") for k in tiers}, s.const("force_error_eps")
+    print(f"{cfg}: radii form mode 1 {dict((k, round(v, 3)) for k, v in r1.items())}, mode 2 "
+          f"{dict((k, round(v, 3)) for k, v in r2.items())}, mode 0 {dict((k, round(v, 3)) for k, v in r0.items())}, "
+          f"L/2 {L / 2:.3f}; force_error_eps mode 1 {e1:.2e}, mode 2 {e2:.2e}")
     assert r1["mid"] < r1["far"] < r1["vfar"] <= r1["ufar"] <= r1["ufar32"] <= L / 2
     for k in ("mid", "far", "vfar", "ufar"):
         assert r1[k] < r0[k]
+    # mode 2: where the tail skips nothing (C5) the tiers share its 1e-12 — one total per ion, 1.5e-12
+    if s.const("force_skip_radius") >= L / 2:
+        assert e2 == pytest.approx(1.5e-12, rel=1e-12) and e1 == pytest.approx(5e-13, rel=1e-12)
+        assert all(r2[k] <= r1[k] for k in tiers) and r2["far"] < r1["far"]
+    else:
+        assert e2 == e1 and r2 == r1
+    s.set_option("force_form_mode", 2)
     out, tb, eps = {}, {}, {}
     combos = ((12, 13, 13, 13, 13), (0, 13, 0, 0, 0), (0, 0, 13, 0, 0), (0, 0, 0, 13, 0), (0, 0, 0, 0, 13),
               (0, 0, 0, 0, 0))

@@ -478,47 +478,56 @@ __device__ __forceinline__ int n3b_level(double g2, const N3BRadii& r) {
     return g2 > r.ru32 ? 5 : g2 > r.ru2 ? 4 : g2 > r.rv2 ? 3 : g2 > r.rf2 ? 2 : g2 > r.rm2 ? 1 : 0;
 }
 // strad (when asked): bit c = axis c's minimum-image multiple varies over the tile pair's pairs
+// (the core on two box columns: Bi = box column of Iw, Bj = of J, row stride ld — global [12][T], or the
+// plan's LDS copy of its workgroup's tiles; the same operations in the same order either way)
 template <bool FAST>
-__device__ __forceinline__ double4 n3b_classify(const N3BArgs& a, double invL, const N3BRadii& r, int Iw, int J,
-                                                double& g2, int* strad = nullptr) {
-    const double* B = a.boxes;
-    const int T = a.T;
+__device__ __forceinline__ double4 n3b_classify_p(const double* Bi, const double* Bj, int ld, double L, double invL,
+                                                  double Rcut, int use_sort, const N3BRadii& r, double& g2,
+                                                  int* strad = nullptr) {
     g2 = 0.;
     bool uni = true;
     int sm = 0;
     double n[3];
 #pragma unroll
     for (int c3 = 0; c3 < 3; ++c3) {
-        double d = B[(size_t)c3 * T + Iw] - B[(size_t)c3 * T + J];
-        d = fma(-__builtin_rint(d * invL), a.L, d);
-        const double gap = fabs(d) - (B[(size_t)(3 + c3) * T + Iw] + B[(size_t)(3 + c3) * T + J]);
+        double d = Bi[c3 * ld] - Bj[c3 * ld];
+        d = fma(-__builtin_rint(d * invL), L, d);
+        const double gap = fabs(d) - (Bi[(3 + c3) * ld] + Bj[(3 + c3) * ld]);
         g2 = gap > 0. ? fma(gap, gap, g2) : g2;
-        const double lo = B[(size_t)(6 + c3) * T + Iw] - B[(size_t)(9 + c3) * T + J];
-        const double hi = B[(size_t)(9 + c3) * T + Iw] - B[(size_t)(6 + c3) * T + J];
+        const double lo = Bi[(6 + c3) * ld] - Bj[(9 + c3) * ld];
+        const double hi = Bi[(9 + c3) * ld] - Bj[(6 + c3) * ld];
         const double nlo = __builtin_rint(lo * invL), nhi = __builtin_rint(hi * invL);
         uni = uni && (nlo == nhi);
         sm |= (nlo == nhi ? 0 : 1) << c3;
         n[c3] = nlo;
     }
     if (strad) *strad = sm;
-    const double cls = (a.use_sort == 1 && g2 > r.rc2) ? (g2 < a.Rcut * a.Rcut ? -2. : -1.)
-                                                        : ((FAST && uni) ? 1. : 0.) +
-                                                              2. * n3b_level(g2, r);
+    const double cls = (use_sort == 1 && g2 > r.rc2) ? (g2 < Rcut * Rcut ? -2. : -1.)
+                                                      : ((FAST && uni) ? 1. : 0.) + 2. * n3b_level(g2, r);
     return make_double4(n[0], n[1], n[2], cls);
+}
+template <bool FAST>
+__device__ __forceinline__ double4 n3b_classify(const N3BArgs& a, double invL, const N3BRadii& r, int Iw, int J,
+                                                double& g2, int* strad = nullptr) {
+    return n3b_classify_p<FAST>(a.boxes + Iw, a.boxes + J, a.T, a.L, invL, a.Rcut, a.use_sort, r, g2, strad);
 }
 
 // the squared minimum-image gap between the boxes of 16-ion sub-tiles s and u ([6][T4] layout)
-__device__ __forceinline__ double sub_gap2(const double* __restrict__ SB, int T4, int s, int u, double L,
-                                           double invL) {
+// (the core on two box columns Bs, Bu of row stride ld, as n3b_classify_p)
+__device__ __forceinline__ double sub_gap2_p(const double* Bs, const double* Bu, int ld, double L, double invL) {
     double g2 = 0.;
 #pragma unroll
     for (int c3 = 0; c3 < 3; ++c3) {
-        double d = SB[(size_t)c3 * T4 + s] - SB[(size_t)c3 * T4 + u];
+        double d = Bs[c3 * ld] - Bu[c3 * ld];
         d = fma(-__builtin_rint(d * invL), L, d);
-        const double gap = fabs(d) - (SB[(size_t)(3 + c3) * T4 + s] + SB[(size_t)(3 + c3) * T4 + u]);
+        const double gap = fabs(d) - (Bs[(3 + c3) * ld] + Bu[(3 + c3) * ld]);
         g2 = gap > 0. ? fma(gap, gap, g2) : g2;
     }
     return g2;
+}
+__device__ __forceinline__ double sub_gap2(const double* __restrict__ SB, int T4, int s, int u, double L,
+                                           double invL) {
+    return sub_gap2_p(SB + s, SB + u, T4, L, invL);
 }
 // the sub-blocks (a, (a + d) & 3) of sub-tile group d as bits 4 a + b
 constexpr unsigned kGroupBits[4] = {0x8421u, 0x1842u, 0x2184u, 0x4218u};
@@ -586,16 +595,19 @@ __device__ __forceinline__ double form_term(double g2, float invl, float cf, int
 // image — a uniform-image tile pair's pairs are each at their minimum image in the block kernel (its shift
 // is every pair's rint(dx / L)), and per axis min_k |x_i - x_j - k L| <= |mi(c_s - c_u)| + h_s + h_u, whatever
 // frame the boxes' centres were taken in (a box is the min / max about its first ion, k_tile_boxes)
-__device__ __forceinline__ double sub_far2(const double* __restrict__ SB, int T4, int s, int u, double L, double invL) {
+__device__ __forceinline__ double sub_far2_p(const double* Bs, const double* Bu, int ld, double L, double invL) {
     double f2 = 0.;
 #pragma unroll
     for (int c3 = 0; c3 < 3; ++c3) {
-        double d = SB[(size_t)c3 * T4 + s] - SB[(size_t)c3 * T4 + u];
+        double d = Bs[c3 * ld] - Bu[c3 * ld];
         d = fma(-__builtin_rint(d * invL), L, d);
-        const double f = fabs(d) + (SB[(size_t)(3 + c3) * T4 + s] + SB[(size_t)(3 + c3) * T4 + u]);
+        const double f = fabs(d) + (Bs[(3 + c3) * ld] + Bu[(3 + c3) * ld]);
         f2 = fma(f, f, f2);
     }
     return f2;
+}
+__device__ __forceinline__ double sub_far2(const double* __restrict__ SB, int T4, int s, int u, double L, double invL) {
+    return sub_far2_p(SB + s, SB + u, T4, L, invL);
 }
 // a tile pair's class and uniform-image multiples in one LDS word: bits 0-3 class + 2, 4-11 / 12-19 /
 // 20-27 n_x, n_y, n_z (signed); a uniform image with a multiple beyond +-127 (positions that far
@@ -620,15 +632,16 @@ __device__ __forceinline__ double sub_count(int N, int s) { return (double)max(0
 // tile J's raw box (the exact min / max of its coordinates, boxes [6, 12)): its squared half-diagonal —
 // the f32 ultra-far form (n3b_group_uf32) stages J relative to J's first ion and takes a sub-tile group
 // only where the box diagonal (twice this) is within the group's gap (kUfar32A/B's premise)
-__device__ __forceinline__ double raw_half2(const double* B, int T, int J) {
+__device__ __forceinline__ double raw_half2_p(const double* Bj, int ld) {
     double h2 = 0.;
 #pragma unroll
     for (int c3 = 0; c3 < 3; ++c3) {
-        const double h = 0.5 * (B[(size_t)(9 + c3) * T + J] - B[(size_t)(6 + c3) * T + J]);
+        const double h = 0.5 * (Bj[(9 + c3) * ld] - Bj[(6 + c3) * ld]);
         h2 = fma(h, h, h2);
     }
     return h2;
 }
+__device__ __forceinline__ double raw_half2(const double* B, int T, int J) { return raw_half2_p(B + J, T); }
 
 
 // One tile pair (I, J) of the block kernels (k_pairs_n3b, k_pairs_n3b_pw): its sub-tile groups of `word`
@@ -1601,8 +1614,18 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
 //    sum_a n_a g(gap_ab); counted once per unordered tile pair, summed per sub-tile in LDS over the
 //    workgroup and added to tailb (128 atomics per workgroup).
 // One workgroup per (P, db), thread (b, q) — the census's decomposition.
+// the plan kernel's occupancy (round 6, A/B r06p_plan_ab.txt, bit-identical): 3 waves per SIMD (168 VGPRs,
+// 2 spilled) with the LDS boxes: plan stage N = 1M 9.4 -> 7.8 ms, C5 0.75 -> 0.58 ms; 4 (128 VGPRs, 37
+// spilled) is slower than 2
+#ifndef MDQT_PLAN_WPE
+#define MDQT_PLAN_WPE 3
+#endif
+#ifndef MDQT_PLAN_LDS
+#define MDQT_PLAN_LDS 1
+#endif
 template <int VARIANT, bool GUARD>
-__global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MDQT_PLAN_WPE)))
+void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
     __shared__ double ti[BW][4], tj[BW][4];
     __shared__ unsigned jm;
     constexpr bool FARF = VARIANT == 1 && !GUARD && MDQT_N3_CUT;
@@ -1613,7 +1636,32 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
     const bool tmeas = a.tailb != nullptr;
     if (tmeas && t < 4 * BW) { ti[t >> 2][t & 3] = 0.; tj[t >> 2][t & 3] = 0.; }
     if (t == 0) jm = 0u;
+    // the workgroup's boxes in LDS (MDQT_PLAN_LDS): the BW I tiles' and BW J tiles' [12] box columns and
+    // their 4 BW sub-tiles' [6] — each read once, coalesced, instead of per tile pair from L2 (the kernel's
+    // ~190 global loads held ~200 VGPRs: 2 waves per SIMD); the same values, the same operations
+    __shared__ double bI[12][BW], bJ[12][BW], sI[6][4 * BW], sJ[6][4 * BW];
+    if constexpr (MDQT_PLAN_LDS) {
+        const int T4 = 4 * a.T;
+        for (int k = t; k < 12 * BW; k += BW * BW) {
+            const int row = k / BW, c = k % BW;
+            bI[row][c] = P * BW + c < a.T ? a.boxes[(size_t)row * a.T + P * BW + c] : 0.;
+            bJ[row][c] = Q * BW + c < a.T ? a.boxes[(size_t)row * a.T + Q * BW + c] : 0.;
+        }
+        if (a.subboxes)
+            for (int k = t; k < 6 * 4 * BW; k += BW * BW) {
+                const int row = k / (4 * BW), c = k % (4 * BW);
+                sI[row][c] = 4 * P * BW + c < T4 ? a.subboxes[(size_t)row * T4 + 4 * P * BW + c] : 0.;
+                sJ[row][c] = 4 * Q * BW + c < T4 ? a.subboxes[(size_t)row * T4 + 4 * Q * BW + c] : 0.;
+            }
+    }
     __syncthreads();
+    // box column accessors: LDS (row stride BW / 4 BW) or global ([12][T] / [6][4T])
+    const double* const Bi = MDQT_PLAN_LDS ? &bI[0][q] : a.boxes + I;
+    const double* const Bj = MDQT_PLAN_LDS ? &bJ[0][b] : a.boxes + J;
+    const int bld = MDQT_PLAN_LDS ? BW : a.T;
+    auto SBi = [&](int sa) -> const double* { return MDQT_PLAN_LDS ? &sI[0][4 * q + sa] : a.subboxes + 4 * I + sa; };
+    auto SBj = [&](int sb) -> const double* { return MDQT_PLAN_LDS ? &sJ[0][4 * b + sb] : a.subboxes + 4 * J + sb; };
+    const int sld = MDQT_PLAN_LDS ? 4 * BW : 4 * a.T;
     uint2 w = make_uint2(1u, 0xFFu);                // class -1 where the block kernel never looks
     double gi[4] = {0., 0., 0., 0.}, gj[4] = {0., 0., 0., 0.};   // this tile pair's tail terms per sub-tile
     const bool half = !(a.NB & 1) && db == a.NB / 2 && P >= a.NB / 2;
@@ -1625,19 +1673,19 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
         const double invL = 1. / a.L;
         double g2;
         int sm;
-        const int pw = n3b_pack_class(n3b_classify<VARIANT == 1>(a, invL, rad, I, J, g2, &sm), VARIANT == 1 ? sm : 0);
+        const int pw = n3b_pack_class(n3b_classify_p<VARIANT == 1>(Bi, Bj, bld, a.L, invL, a.Rcut, a.use_sort, rad, g2, &sm),
+                                       VARIANT == 1 ? sm : 0);
         const int cls = (pw & 15) - 2;
         w.x = (unsigned)pw;
         const bool rag = (a.N & 63) && (I == a.T - 1 || J == a.T - 1);
         const bool uni = cls >= 0 && (cls & 1);
         if (db == 0 && J == I && !(g2 > rad.rc2)) cest = (rag ? 52u : uni ? 39u : 48u) * 40u;
         if ((db > 0 || J > I) && (cls >= 0 || (tmeas && cls == -2))) {
-            const int T4 = 4 * a.T;
             double sg[4][4];
 #pragma unroll
             for (int sa = 0; sa < 4; ++sa)
 #pragma unroll
-                for (int sb = 0; sb < 4; ++sb) sg[sa][sb] = sub_gap2(a.subboxes, T4, 4 * I + sa, 4 * J + sb, a.L, invL);
+                for (int sb = 0; sb < 4; ++sb) sg[sa][sb] = sub_gap2_p(SBi(sa), SBj(sb), sld, a.L, invL);
             unsigned groups = 0u, lvm = 0u;
             double gm[4];
 #pragma unroll
@@ -1646,12 +1694,12 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
             // the f32 level needs J's raw box diagonal within the group's gap (kUfar32A/B): J's extents
             // read only where a group is that far
             const double gmax = fmax(fmax(gm[0], gm[1]), fmax(gm[2], gm[3]));
-            const double hj4 = FARF && gmax > rad.ru32 ? 4. * raw_half2(a.boxes, a.T, J) : 0.;
+            const double hj4 = FARF && gmax > rad.ru32 ? 4. * raw_half2_p(Bj, bld) : 0.;
             int xs[4];                              // the groups' levels (the measured form bound)
             // (formm) the whole tile pair within u32lim2 under its image — tile boxes: every sub-block is
             bool tile_in = false;
             if (FARF && a.formm && gmax > rad.ru32 && uni)
-                tile_in = sub_far2(a.boxes, a.T, I, J, a.L, invL) < a.u32lim2;   // ([12][T]: centers, half extents first)
+                tile_in = sub_far2_p(Bi, Bj, bld, a.L, invL) < a.u32lim2;   // ([12][T]: centers, half extents first)
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 int x = !FARF ? 0 : n3b_level(gm[d], rad);
@@ -1660,7 +1708,7 @@ __global__ __launch_bounds__(256) void k_n3b_plan(N3BArgs a, uint2* __restrict__
                     double f2 = 0.;
 #pragma unroll
                     for (int sa = 0; sa < 4; ++sa)
-                        f2 = fmax(f2, sub_far2(a.subboxes, T4, 4 * I + sa, 4 * J + ((sa + d) & 3), a.L, invL));
+                        f2 = fmax(f2, sub_far2_p(SBi(sa), SBj((sa + d) & 3), sld, a.L, invL));
                     if (!(f2 < a.u32lim2)) x = 4;
                 }
                 xs[d] = x;

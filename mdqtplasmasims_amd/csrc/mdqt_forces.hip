@@ -1623,6 +1623,10 @@ __global__ __launch_bounds__(256) void k_n3b_census(N3BArgs a, unsigned long lon
 #ifndef MDQT_PLAN_LDS
 #define MDQT_PLAN_LDS 1
 #endif
+#ifndef MDQT_EXPT_PLAN
+#define MDQT_EXPT_PLAN 0                            // diagnostic builds only (wrong plans): bit 0 no tail terms, 1 no pairing sort,
+                                                    // 2 no sub-tile work
+#endif
 template <int VARIANT, bool GUARD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MDQT_PLAN_WPE)))
 void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
@@ -1680,7 +1684,7 @@ void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
         const bool rag = (a.N & 63) && (I == a.T - 1 || J == a.T - 1);
         const bool uni = cls >= 0 && (cls & 1);
         if (db == 0 && J == I && !(g2 > rad.rc2)) cest = (rag ? 52u : uni ? 39u : 48u) * 40u;
-        if ((db > 0 || J > I) && (cls >= 0 || (tmeas && cls == -2))) {
+        if ((db > 0 || J > I) && (cls >= 0 || (tmeas && cls == -2)) && !(MDQT_EXPT_PLAN & 4)) {   // (bit 2: timing only)
             double sg[4][4];
 #pragma unroll
             for (int sa = 0; sa < 4; ++sa)
@@ -1719,7 +1723,7 @@ void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
                 }
             }
             if (cls >= 0) w.y = groups | (lvm << 4);
-            if (tmeas) {
+            if (tmeas && !(MDQT_EXPT_PLAN & 1)) {        // (EXPT_PLAN bit 0: timing only)
                 const double rcut2 = a.Rcut * a.Rcut;
                 const float invl = (float)a.invlDeb, cf = (float)(a.invlDeb * kNegLog2e);
                 constexpr bool AX1U = FARF && MDQT_N3B_AX1 != 0 && (MDQT_N3B_AX1_LEVELS & 16u) != 0;
@@ -1774,19 +1778,25 @@ void k_n3b_plan(N3BArgs a, uint2* __restrict__ plan) {
     unsigned rc = cest;
 #pragma unroll
     for (int off = BW; off < 64; off <<= 1) rc += __shfl_xor(rc, off);
-    unsigned row[BW];
+    // lanes 0 .. BW-1 hold the BW tiles' sums (lane t: tile t mod BW); each of them takes its tile's place in
+    // the order (descending by work, ties by tile: the stable insertion sort's order) and its field of the
+    // pairing word — the busiest tile with the least busy, and so on, 6 bits per pair — OR-ed over the lanes
+    // (round 6: one thread's serial sort cost the plan stage ~1.5 ms of 8 at N = 1M)
+    unsigned pr = 0;
+    {
+        unsigned row[BW];
 #pragma unroll
-    for (int k = 0; k < BW; ++k) row[k] = __shfl(rc, k);
-    __syncthreads();
-    if (t == 0) {
-        int ord[BW];
-        for (int k = 0; k < BW; ++k) ord[k] = k;
-        for (int u = 1; u < BW; ++u)                // descending by work, ties by tile (deterministic)
-            for (int v = u; v > 0 && row[ord[v]] > row[ord[v - 1]]; --v) { const int x = ord[v]; ord[v] = ord[v - 1]; ord[v - 1] = x; }
-        unsigned pr = 0;
-        for (int k = 0; k < BW / 2; ++k) pr |= ((unsigned)ord[k] | (unsigned)ord[BW - 1 - k] << 3) << (6 * k);
-        plan[(size_t)(a.Phi - a.Plo) * a.nd * (BW * BW) + (size_t)Pl * a.nd + db] = make_uint2(jm, pr);
+        for (int k = 0; k < BW; ++k) row[k] = __shfl(rc, k);
+        int rk = 0;
+#pragma unroll
+        for (int k = 0; k < BW; ++k) rk += (row[k] > rc || (row[k] == rc && k < t)) ? 1 : 0;
+        if (t < BW) pr = rk < BW / 2 ? (unsigned)t << (6 * rk) : (unsigned)t << (3 + 6 * (BW - 1 - rk));
+#pragma unroll
+        for (int off = 1; off < BW; off <<= 1) pr |= __shfl_xor(pr, off);
     }
+    __syncthreads();
+    if (t == 0 && !(MDQT_EXPT_PLAN & 2))          // (EXPT_PLAN bit 1: timing only)
+        plan[(size_t)(a.Phi - a.Plo) * a.nd * (BW * BW) + (size_t)Pl * a.nd + db] = make_uint2(jm, pr);
     // the reduction's per-J-tile masks: J step b has work -> the block kernel writes J's j-slot db
     if (a.tmask && t < BW && ((jm >> t) & 1u))
         atomicOr(a.tmask + (size_t)(Q * BW + t) * a.tmw + (db >> 6), 1ull << (db & 63));

@@ -210,3 +210,40 @@ def test_block_partials_reduce_to_the_oracle_forces_gloo_world2(orc):
         assert "error" not in out, out
         assert out["rel"] < 1e-13, out
     assert res[0]["slab"][1] == res[1]["slab"][0]
+
+
+# ---------------------------------------------------------------------------------------------
+# k_n3b_plan's pairing word (round 6): the lane-parallel form — each of lanes 0..BW-1 counts the tiles
+# ahead of its own (strictly more work, or equal work and a lower tile) and writes its 3-bit field —
+# against the serial stable insertion sort it replaced (mdqt_forces.hip k_n3b_plan)
+# ---------------------------------------------------------------------------------------------
+def _pairing_serial(row):
+    BW = len(row)
+    ord_ = list(range(BW))
+    for u in range(1, BW):
+        v = u
+        while v > 0 and row[ord_[v]] > row[ord_[v - 1]]:
+            ord_[v], ord_[v - 1] = ord_[v - 1], ord_[v]
+            v -= 1
+    pr = 0
+    for k in range(BW // 2):
+        pr |= (ord_[k] | ord_[BW - 1 - k] << 3) << (6 * k)
+    return pr
+
+
+def _pairing_lanes(row):
+    BW = len(row)
+    pr = 0
+    for t in range(BW):
+        rk = sum(1 for k in range(BW) if row[k] > row[t] or (row[k] == row[t] and k < t))
+        pr |= (t << (6 * rk)) if rk < BW // 2 else (t << (3 + 6 * (BW - 1 - rk)))
+    return pr
+
+
+def test_plan_pairing_word_lane_parallel_matches_serial_sort():
+    rng = np.random.default_rng(7)
+    cases = [[0] * 8, list(range(8)), list(range(8))[::-1], [5, 5, 1, 1, 9, 9, 0, 0]]
+    cases += [list(rng.integers(0, 4, 8)) for _ in range(2000)]          # many ties
+    cases += [list(rng.integers(0, 1 << 20, 8)) for _ in range(2000)]
+    for row in cases:
+        assert _pairing_lanes(row) == _pairing_serial(row), row
